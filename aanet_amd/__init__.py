@@ -1,0 +1,13 @@
+"""aanet_amd -- MI355X-native (gfx950) AANet cost-volume hot path.
+
+Layers: include/aanet_mi355x.h (C ABI, HIP kernels in aanet_amd/csrc) -> aanet_amd._lib (ctypes)
+-> aanet_amd.ops (autograd ops) -> aanet_amd.nets (drop-in modules mirroring the reference's
+nets/ API).  No CPU fallback: ops raise on non-HIP tensors or a missing library.
+"""
+from . import _lib, ops  # noqa: F401
+
+__version__ = "0.1.0"
+
+
+def native_library_path():
+    return _lib.LIB_PATH

@@ -1,0 +1,102 @@
+"""ctypes binding of the gfx950 C-ABI library ``libaanet_mi355x.so`` (include/aanet_mi355x.h).
+
+This is the only way the Python package reaches the GPU: every op passes raw device pointers
+and torch's current HIP stream to an ``extern "C"`` entry point.  There is NO CPU fallback:
+if the library is missing or a tensor is not on a ROCm device, the call raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("AANET_MI355X_LIB", os.path.join(_HERE, "libaanet_mi355x.so"))
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+_F = ctypes.c_float
+
+# name -> argtypes (every function returns int status)
+_SIGNATURES = {
+    "aanet_corr_volume_f32": [_P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "aanet_corr_volume_bwd_f32": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "aanet_concat_volume_f32": [_P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "aanet_diff_volume_f32": [_P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "aanet_concat_volume_bwd_f32": [_P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "aanet_diff_volume_bwd_f32": [_P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "aanet_corr_pyramid_f32": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _P],
+    "aanet_disp_regress_f32": [_P, _P, _I, _I, _I, _I, _I, _P],
+    "aanet_disp_regress_bwd_f32": [_P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "aanet_mdcn_fwd_f32": [_P, _P, _P, _P, _P, _P] + [_I] * 12 + [_P],
+    "aanet_mdcn_fwd_fused_f32": [_P, _P, _L, _P, _L, _I, _F, _P, _P, _P, _P, _I, _P] + [_I] * 12 + [_P],
+    "aanet_mdcn_bwd_f32": [_P] * 10 + [_I] * 12 + [_P],
+    "aanet_mdcn_im2col_f32": [_P, _P, _P, _P] + [_I] * 9 + [_P],
+    "aanet_mdcn_sample_index": [_P, _P, _P, _P] + [_I] * 9 + [_P],
+}
+
+_lib = None
+
+
+class AanetError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load the HIP library (raises loudly when it is absent -- never falls back)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"aanet_amd: HIP library not found at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (make -C aanet_amd/csrc)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, argtypes in _SIGNATURES.items():
+            f = getattr(L, name)
+            f.argtypes = argtypes
+            f.restype = _I
+        L.aanet_status_string.argtypes = [_I]
+        L.aanet_status_string.restype = ctypes.c_char_p
+        L.aanet_version.restype = _I
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return ["aanet_version", "aanet_status_string"] + list(_SIGNATURES)
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().aanet_status_string(rc).decode()
+        raise AanetError(f"{name} failed: {msg} (status {rc})")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def require_gpu(*tensors, names=None):
+    """fp32, contiguous, on the same ROCm device: the C ABI takes raw NCHW pointers."""
+    dev = None
+    for i, t in enumerate(tensors):
+        if t is None:
+            continue
+        nm = names[i] if names else f"arg{i}"
+        if not t.is_cuda:
+            raise NotImplementedError(
+                f"aanet_amd ops run only on the MI355X (HIP) device; {nm} is on {t.device}")
+        if t.dtype != torch.float32:
+            raise TypeError(f"aanet_amd ops compute in fp32; {nm} is {t.dtype}")
+        if not t.is_contiguous():
+            raise ValueError(f"{nm} must be contiguous")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise ValueError(f"{nm} is on {t.device}, expected {dev}")
+    return dev

@@ -1,0 +1,345 @@
+// cost_volume.hip -- cost-volume construction for gfx950 (replaces nets/cost.py:19-76).
+//
+// Correlation (cost.py:40-48) is a banded contraction over channels:
+//   P[x][x'] = sum_c L[c][x] * R[c][x'],  out[d][x] = P[x][x-d] / C  for 0 <= d < D.
+// One workgroup owns a 64-wide x tile of one (b, y) row and a chunk of <=64 disparities.
+// Channels stream through LDS in 16-channel stages (double buffered: the next stage's
+// global loads are issued before the current stage's MFMAs).  Each of the 4 waves owns 16 x
+// and computes the 16 x (16*NJ) band of P with v_mfma_f32_16x16x4_f32 (exact fp32), so
+// every L / R element is read from HBM once and the FMAs run on the matrix pipe.  The band
+// is transposed through LDS to [d][x] and stored as full 256-B rows.  x' < 0 reads are
+// zero, which produces the x < d zero fill of cost.py:41 for free.
+#include "common.h"
+
+namespace {
+
+constexpr int TX = 64;      // x positions per workgroup
+constexpr int CC = 16;      // channels per LDS stage
+constexpr int NTHREADS = 256;
+
+template <int NJ>
+struct CorrSmem {
+  static constexpr int RW = TX + 16 * (NJ - 1);       // right-feature window width
+  static constexpr int DC = 16 * (NJ - 1) + 1 > 64 ? 64 : 16 * (NJ - 1) + 1;
+  static constexpr int STAGE = CC * TX + CC * RW;      // floats per stage
+  static constexpr int OUTP = TX + 1;                  // padded [d][x] output pitch
+  static constexpr int BYTES_STAGE = 2 * STAGE * 4;
+  static constexpr int BYTES_OUT = 64 * OUTP * 4;
+  static constexpr int BYTES = BYTES_STAGE > BYTES_OUT ? BYTES_STAGE : BYTES_OUT;
+};
+
+// grid: (ceil(W/TX) * nchunks, H, N).  dchunk = disparities per chunk (<= 16*(NJ-1)+1).
+template <int NJ>
+__global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
+    const float *__restrict__ L, const float *__restrict__ R, float *__restrict__ out, int C,
+    int H, int W, int D, int dchunk, int ntx) {
+  using S = CorrSmem<NJ>;
+  constexpr int RW = S::RW;
+  __shared__ __attribute__((aligned(16))) float smem[S::BYTES / 4];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tx = blockIdx.x % ntx, chunk = blockIdx.x / ntx;
+  const int y = blockIdx.y, b = blockIdx.z;
+  const int x0 = tx * TX, d0 = chunk * dchunk;
+  const int xr0 = x0 - d0 - 16 * (NJ - 1);  // first x' of the right window
+  const long HW = (long)H * W;
+  const float *Lrow = L + (long)b * C * HW + (long)y * W;
+  const float *Rrow = R + (long)b * C * HW + (long)y * W;
+
+  constexpr int LPT = CC * TX / NTHREADS;                 // L floats per thread per stage
+  constexpr int RPT = (CC * RW + NTHREADS - 1) / NTHREADS;  // R floats per thread per stage
+  float lreg[LPT], rreg[RPT];
+
+  auto load_stage = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int e = tid + i * NTHREADS, row = e / TX, col = e % TX;
+      const int c = c0 + row, x = x0 + col;
+      lreg[i] = (c < C && x < W) ? Lrow[(long)c * HW + x] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int e = tid + i * NTHREADS, row = e / RW, col = e % RW;
+      const int c = c0 + row, x = xr0 + col;
+      rreg[i] = (e < CC * RW && c < C && x >= 0 && x < W) ? Rrow[(long)c * HW + x] : 0.f;
+    }
+  };
+  auto store_stage = [&](int buf) {
+    float *sL = smem + buf * S::STAGE, *sR = sL + CC * TX;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) sL[tid + i * NTHREADS] = lreg[i];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int e = tid + i * NTHREADS;
+      if (e < CC * RW) sR[e] = rreg[i];
+    }
+  };
+
+  f32x4 acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nstages = (C + CC - 1) / CC;
+  load_stage(0);
+  store_stage(0);
+  __syncthreads();
+  const int kr = lane >> 4, jj = lane & 15;
+  for (int s = 0; s < nstages; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nstages) load_stage((s + 1) * CC);
+    const float *sL = smem + buf * S::STAGE, *sR = sL + CC * TX;
+#pragma unroll
+    for (int ks = 0; ks < CC / 4; ++ks) {
+      const int row = 4 * ks + kr;
+      const float a = sL[row * TX + 16 * wave + jj];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float bv = sR[row * RW + 16 * wave + jj + 16 * (NJ - 1 - j)];
+        acc[j] = mfma16x16x4(a, bv, acc[j]);
+      }
+    }
+    if (s + 1 < nstages) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+  // Band -> [d][x] tile in LDS.  Lane holds x' column jj, rows i = 4*kr + r (x).
+  float *sO = smem;
+  const float Cf = (float)C;
+  const int dmax = min(dchunk, D - d0);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * kr + r;
+      const int dl = 16 * j + i - jj;
+      if (dl >= 0 && dl < dmax) sO[dl * S::OUTP + 16 * wave + i] = acc[j][r] / Cf;
+    }
+  __syncthreads();
+  for (int e = tid; e < dmax * TX; e += NTHREADS) {
+    const int dl = e / TX, xl = e % TX;
+    if (x0 + xl < W) out[(((long)b * D + d0 + dl) * H + y) * W + x0 + xl] = sO[dl * S::OUTP + xl];
+  }
+}
+
+template <int NJ>
+int launch_corr(const float *L, const float *R, float *out, int n, int c, int h, int w, int D,
+                hipStream_t st) {
+  const int dchunk = CorrSmem<NJ>::DC;
+  const int nchunks = host_div_up(D, dchunk), ntx = host_div_up(w, TX);
+  dim3 grid(ntx * nchunks, h, n);
+  hipLaunchKernelGGL(corr_volume_kernel<NJ>, grid, dim3(NTHREADS), 0, st, L, R, out, c, h, w, D,
+                     dchunk, ntx);
+  return aanet_launch_status();
+}
+
+// --------------------------------------------------------------- correlation backward ----
+// grad_L[c][x]  = (1/C) sum_d gO[d][x]   * R[c][x-d]   (x-d >= 0)
+// grad_R[c][x'] = (1/C) sum_d gO[d][x'+d] * L[c][x'+d] (x'+d < W)
+// One workgroup = one (b, y) row x 64-wide x tile; gO band staged in LDS once, channels
+// looped.  VALU kernel (training path, not the timed inference path).
+constexpr int BTX = 64;
+__global__ __launch_bounds__(256) void corr_volume_bwd_kernel(
+    const float *__restrict__ L, const float *__restrict__ R, const float *__restrict__ gO,
+    float *__restrict__ gL, float *__restrict__ gR, int C, int H, int W, int D, int ntx) {
+  extern __shared__ float sm[];
+  const int tid = threadIdx.x;
+  const int tx = blockIdx.x % ntx, y = blockIdx.y, b = blockIdx.z;
+  const int x0 = tx * BTX;
+  const int G0 = x0 - (D - 1);         // window start (for R at x-d and gO at x'+d)
+  const int GW = BTX + 2 * (D - 1);    // window width
+  const long HW = (long)H * W;
+  float *sG = sm;                      // [D][GW] grad_out rows at x in window
+  float *sLw = sG + (long)D * GW;      // [4][GW]
+  float *sRw = sLw + 4 * GW;           // [4][GW]
+  for (int e = tid; e < D * GW; e += 256) {
+    const int d = e / GW, xx = G0 + e % GW;
+    sG[e] = (xx >= 0 && xx < W) ? gO[(((long)b * D + d) * H + y) * W + xx] : 0.f;
+  }
+  const int xl = tid & 63, cq = tid >> 6;
+  const int x = x0 + xl;
+  const float invC = 1.f / (float)C;
+  for (int c0 = 0; c0 < C; c0 += 4) {
+    __syncthreads();
+    for (int e = tid; e < 4 * GW; e += 256) {
+      const int cc = c0 + e / GW, xx = G0 + e % GW;
+      const bool ok = cc < C && xx >= 0 && xx < W;
+      sLw[e] = ok ? L[((long)b * C + cc) * HW + (long)y * W + xx] : 0.f;
+      sRw[e] = ok ? R[((long)b * C + cc) * HW + (long)y * W + xx] : 0.f;
+    }
+    __syncthreads();
+    const int c = c0 + cq;
+    if (c < C && x < W) {
+      float gl = 0.f, gr = 0.f;
+      const int xi = x - G0;  // index of x in the window
+      for (int d = 0; d < D; ++d) {
+        gl += sG[d * GW + xi] * sRw[cq * GW + xi - d];          // zero when x-d < 0
+        gr += sG[d * GW + xi + d] * sLw[cq * GW + xi + d];      // zero when x+d >= W
+      }
+      gL[((long)b * C + c) * HW + (long)y * W + x] = gl * invC;
+      gR[((long)b * C + c) * HW + (long)y * W + x] = gr * invC;
+    }
+  }
+}
+
+// ----------------------------------------------------------------- concat / difference ---
+// Output-indexed, write-bound: out[b][oc][d][y][x]; 4 consecutive x per thread.
+template <bool CONCAT>
+__global__ __launch_bounds__(256) void shift_volume_kernel(const float *__restrict__ L,
+                                                           const float *__restrict__ R,
+                                                           float *__restrict__ out, int C, int H,
+                                                           int W, int D, long total4, int W4) {
+  const int OC = CONCAT ? 2 * C : C;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total4; e += (long)gridDim.x * 256) {
+    const int xq = (int)(e % W4);
+    long t = e / W4;
+    const int y = (int)(t % H);
+    t /= H;
+    const int d = (int)(t % D);
+    t /= D;
+    const int oc = (int)(t % OC);
+    const int b = (int)(t / OC);
+    const int x = 4 * xq;
+    const long HW = (long)H * W;
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int xx = x + u;
+      float r = 0.f;
+      if (xx < W && xx >= d) {
+        if (CONCAT) {
+          r = oc < C ? L[((long)b * C + oc) * HW + (long)y * W + xx]
+                     : R[((long)b * C + oc - C) * HW + (long)y * W + xx - d];
+        } else {
+          r = L[((long)b * C + oc) * HW + (long)y * W + xx] -
+              R[((long)b * C + oc) * HW + (long)y * W + xx - d];
+        }
+      }
+      v[u] = r;
+    }
+    float *o = out + ((((long)b * OC + oc) * D + d) * H + y) * W + x;
+    if ((W & 3) == 0) {
+      *reinterpret_cast<float4 *>(o) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (x + u < W) o[u] = v[u];
+    }
+  }
+}
+
+template <bool CONCAT>
+__global__ __launch_bounds__(256) void shift_volume_bwd_kernel(const float *__restrict__ gO,
+                                                               float *__restrict__ gL,
+                                                               float *__restrict__ gR, int C,
+                                                               int H, int W, int D, long total) {
+  const int OC = CONCAT ? 2 * C : C;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int x = (int)(e % W);
+    long t = e / W;
+    const int y = (int)(t % H);
+    t /= H;
+    const int c = (int)(t % C);
+    const int b = (int)(t / C);
+    const long plane = (long)H * W, base = (long)y * W;
+    float gl = 0.f, gr = 0.f;
+    const int ocr = CONCAT ? C + c : c;
+    for (int d = 0; d < D; ++d) {
+      if (x >= d) gl += gO[(((long)b * OC + c) * D + d) * plane + base + x];
+      if (x + d < W) gr += gO[(((long)b * OC + ocr) * D + d) * plane + base + x + d];
+    }
+    gL[((long)b * C + c) * plane + base + x] = gl;
+    gR[((long)b * C + c) * plane + base + x] = CONCAT ? gr : -gr;
+  }
+}
+
+int grid_for(long work) {
+  long g = (work + 255) / 256;
+  return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+extern "C" int aanet_corr_volume_f32(const float *left, const float *right, float *out, int n,
+                                     int c, int h, int w, int max_disp, aanet_stream_t stream) {
+  AANET_HOST_CHECK(left && right && out && n > 0 && c > 0 && h > 0 && w > 0 && max_disp > 0);
+  hipStream_t st = as_hip(stream);
+  const int dneed = max_disp < 64 ? max_disp : 64;
+  const int nj = dneed <= 1 ? 1 : 1 + (dneed - 1 + 15) / 16;
+  switch (nj) {
+    case 1: return launch_corr<1>(left, right, out, n, c, h, w, max_disp, st);
+    case 2: return launch_corr<2>(left, right, out, n, c, h, w, max_disp, st);
+    case 3: return launch_corr<3>(left, right, out, n, c, h, w, max_disp, st);
+    case 4: return launch_corr<4>(left, right, out, n, c, h, w, max_disp, st);
+    default: return launch_corr<5>(left, right, out, n, c, h, w, max_disp, st);
+  }
+}
+
+extern "C" int aanet_corr_pyramid_f32(int num_scales, const float *const *left,
+                                      const float *const *right, float *const *out, const int *c,
+                                      const int *h, const int *w, int n, int max_disp,
+                                      aanet_stream_t stream) {
+  AANET_HOST_CHECK(num_scales > 0 && left && right && out && c && h && w);
+  for (int s = 0; s < num_scales; ++s) {
+    const int d = max_disp >> s;
+    const int rc = aanet_corr_volume_f32(left[s], right[s], out[s], n, c[s], h[s], w[s], d, stream);
+    if (rc != AANET_OK) return rc;
+  }
+  return AANET_OK;
+}
+
+extern "C" int aanet_corr_volume_bwd_f32(const float *left, const float *right,
+                                         const float *grad_out, float *grad_left,
+                                         float *grad_right, int n, int c, int h, int w,
+                                         int max_disp, aanet_stream_t stream) {
+  AANET_HOST_CHECK(left && right && grad_out && grad_left && grad_right && n > 0 && c > 0 &&
+                   h > 0 && w > 0 && max_disp > 0);
+  const int GW = BTX + 2 * (max_disp - 1);
+  const size_t smem = sizeof(float) * ((size_t)max_disp * GW + 8 * GW);
+  if (smem > 160 * 1024) return AANET_EUNSUPPORTED;
+  const int ntx = host_div_up(w, BTX);
+  hipLaunchKernelGGL(corr_volume_bwd_kernel, dim3(ntx, h, n), dim3(256), smem, as_hip(stream),
+                     left, right, grad_out, grad_left, grad_right, c, h, w, max_disp, ntx);
+  return aanet_launch_status();
+}
+
+extern "C" int aanet_concat_volume_f32(const float *left, const float *right, float *out, int n,
+                                       int c, int h, int w, int max_disp, aanet_stream_t stream) {
+  AANET_HOST_CHECK(left && right && out && n > 0 && c > 0 && h > 0 && w > 0 && max_disp > 0);
+  const int W4 = (w + 3) / 4;
+  const long total4 = (long)n * 2 * c * max_disp * h * W4;
+  hipLaunchKernelGGL(shift_volume_kernel<true>, dim3(grid_for(total4)), dim3(256), 0,
+                     as_hip(stream), left, right, out, c, h, w, max_disp, total4, W4);
+  return aanet_launch_status();
+}
+
+extern "C" int aanet_diff_volume_f32(const float *left, const float *right, float *out, int n,
+                                     int c, int h, int w, int max_disp, aanet_stream_t stream) {
+  AANET_HOST_CHECK(left && right && out && n > 0 && c > 0 && h > 0 && w > 0 && max_disp > 0);
+  const int W4 = (w + 3) / 4;
+  const long total4 = (long)n * c * max_disp * h * W4;
+  hipLaunchKernelGGL(shift_volume_kernel<false>, dim3(grid_for(total4)), dim3(256), 0,
+                     as_hip(stream), left, right, out, c, h, w, max_disp, total4, W4);
+  return aanet_launch_status();
+}
+
+extern "C" int aanet_concat_volume_bwd_f32(const float *grad_out, float *grad_left,
+                                           float *grad_right, int n, int c, int h, int w,
+                                           int max_disp, aanet_stream_t stream) {
+  AANET_HOST_CHECK(grad_out && grad_left && grad_right && n > 0 && c > 0 && h > 0 && w > 0 &&
+                   max_disp > 0);
+  const long total = (long)n * c * h * w;
+  hipLaunchKernelGGL(shift_volume_bwd_kernel<true>, dim3(grid_for(total)), dim3(256), 0,
+                     as_hip(stream), grad_out, grad_left, grad_right, c, h, w, max_disp, total);
+  return aanet_launch_status();
+}
+
+extern "C" int aanet_diff_volume_bwd_f32(const float *grad_out, float *grad_left,
+                                         float *grad_right, int n, int c, int h, int w,
+                                         int max_disp, aanet_stream_t stream) {
+  AANET_HOST_CHECK(grad_out && grad_left && grad_right && n > 0 && c > 0 && h > 0 && w > 0 &&
+                   max_disp > 0);
+  const long total = (long)n * c * h * w;
+  hipLaunchKernelGGL(shift_volume_bwd_kernel<false>, dim3(grid_for(total)), dim3(256), 0,
+                     as_hip(stream), grad_out, grad_left, grad_right, c, h, w, max_disp, total);
+  return aanet_launch_status();
+}

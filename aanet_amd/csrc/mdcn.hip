@@ -1,0 +1,604 @@
+// mdcn.hip -- modulated deformable convolution (DCNv2) for gfx950.
+// Replaces nets/deform_conv/src/deform_conv_cuda.cpp:490-685 and
+// deform_conv_cuda_kernel.cu:467-866 (modulated kernels only; AANet never uses DCNv1).
+//
+// Forward = implicit GEMM.  A workgroup owns 64 output pixels of one image and up to 64
+// output channels.  The K dimension (C_in * kh * kw) is walked in chunks of one tap k and
+// <= 32 channels of one deformable group, so the sampling coordinates / bilinear weights of a
+// (pixel, k, group) are computed ONCE in registers and reused for every channel of the chunk.
+// The chunk's im2col tile is built in LDS (never written to HBM, unlike the reference's
+// 122.7 MB-per-image `columns` buffer) and contracted with the weights by
+// v_mfma_f32_16x16x4_f32 (exact fp32).
+//
+// Bit-exactness: the coordinate h = float(int) + offset is one fp32 add (kernel.cu:615-616);
+// floor / bilinear follow kernel.cu:467-497 with fp contraction disabled, so im2col values
+// and sampling indices equal the CPU oracle's bit for bit (tests/test_gpu_mdcn.py).
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int PT = 64;     // pixels per workgroup tile
+constexpr int KC = 32;     // max channels per K chunk
+constexpr int CP = PT + 16;  // sCol pitch (floats): rows r, r+1 land 16 banks apart
+
+struct MdcnArgs {
+  const float *x;
+  const float *offset;
+  long off_bs;
+  const float *mask;
+  long mask_bs;
+  int mask_logits;
+  float mask_scale;
+  const float *weight;
+  const float *bias;
+  const float *post_scale;
+  const float *post_shift;
+  int act;
+  float *out;
+  int N, C, H, W, Co, kh, kw, stride, pad, dil, groups, dg, Ho, Wo;
+};
+
+// Bilinear sampling state of one (pixel, tap, deformable group).  Invalid corners get
+// weight 0 and a clamped (valid) address, which reproduces the reference's `v = 0` branch
+// exactly: w*0 adds a zero term, as 0-valued v does in kernel.cu:478-493.
+struct Samp {
+  int i1, i2, i3, i4;
+  float w1, w2, w3, w4;
+  float m;
+  float lh, lw;   // fractional parts (backward)
+  int valid;
+  int ok;         // corner validity bits (backward)
+};
+
+__device__ __forceinline__ void make_samp(Samp &s, float h, float w, int H, int W, float m) {
+#pragma clang fp contract(off)
+  const bool valid = h > -1.f && w > -1.f && h < (float)H && w < (float)W;
+  const int hl = (int)floorf(h), wl = (int)floorf(w);
+  const float lh = h - (float)hl, lw = w - (float)wl;
+  const float hh = 1.f - lh, hw = 1.f - lw;
+  const bool ok1 = valid && hl >= 0 && wl >= 0;
+  const bool ok2 = valid && hl >= 0 && wl + 1 <= W - 1;
+  const bool ok3 = valid && hl + 1 <= H - 1 && wl >= 0;
+  const bool ok4 = valid && hl + 1 <= H - 1 && wl + 1 <= W - 1;
+  s.w1 = ok1 ? hh * hw : 0.f;
+  s.w2 = ok2 ? hh * lw : 0.f;
+  s.w3 = ok3 ? lh * hw : 0.f;
+  s.w4 = ok4 ? lh * lw : 0.f;
+  s.i1 = ok1 ? hl * W + wl : 0;
+  s.i2 = ok2 ? hl * W + wl + 1 : 0;
+  s.i3 = ok3 ? (hl + 1) * W + wl : 0;
+  s.i4 = ok4 ? (hl + 1) * W + wl + 1 : 0;
+  s.m = m;
+  s.lh = lh;
+  s.lw = lw;
+  s.valid = valid;
+  s.ok = (ok1 ? 1 : 0) | (ok2 ? 2 : 0) | (ok3 ? 4 : 0) | (ok4 ? 8 : 0);
+}
+
+// kernel.cu:494-496 then `val * mask` (kernel.cu:627): ((w1 v1 + w2 v2) + w3 v3) + w4 v4.
+__device__ __forceinline__ float samp_val(const float *__restrict__ im, const Samp &s) {
+#pragma clang fp contract(off)
+  const float v = s.w1 * im[s.i1] + s.w2 * im[s.i2] + s.w3 * im[s.i3] + s.w4 * im[s.i4];
+  return v * s.m;
+}
+
+__device__ __forceinline__ float load_mask(const MdcnArgs &a, int n, int g, int k, int K, long P,
+                                           long p) {
+  const float v = a.mask[(long)n * a.mask_bs + ((long)g * K + k) * P + p];
+  if (!a.mask_logits) return v;
+  return a.mask_scale * (1.f / (1.f + expf(-v)));  // deform.py:86-89
+}
+
+// Sampling state for output pixel p of image n, tap k (= i*kw + j), deformable group g.
+__device__ __forceinline__ void pixel_samp(Samp &s, const MdcnArgs &a, int n, int g, int k, long p,
+                                           int ho, int wo) {
+#pragma clang fp contract(off)
+  const int K = a.kh * a.kw;
+  const long P = (long)a.Ho * a.Wo;
+  const int i = k / a.kw, j = k % a.kw;
+  const float *off = a.offset + (long)n * a.off_bs + (long)g * 2 * K * P;
+  const float oh = off[(long)(2 * k) * P + p], ow = off[(long)(2 * k + 1) * P + p];
+  const float m = load_mask(a, n, g, k, K, P, p);
+  const float h = (float)(ho * a.stride - a.pad + i * a.dil) + oh;
+  const float w = (float)(wo * a.stride - a.pad + j * a.dil) + ow;
+  make_samp(s, h, w, a.H, a.W, m);
+}
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == 1) return v > 0.f ? v : 0.f;
+  if (act == 2) return v > 0.f ? v : 0.2f * v;
+  return v;
+}
+
+// ------------------------------------------------------------------------ forward -------
+// grid: x = N * ceil(P/64), y = groups * ceil(Cog/CO_T).
+template <int CO_T>
+__global__ __launch_bounds__(NT) void mdcn_fwd_kernel(MdcnArgs a) {
+  constexpr int NCB = CO_T / 16;  // 16-wide output-channel blocks per wave
+  constexpr int WP = 34;          // sW pitch: conflict-free A reads (2*i + kr distinct)
+  __shared__ __attribute__((aligned(16))) float sCol[KC * CP];
+  __shared__ __attribute__((aligned(16))) float sW[CO_T * WP];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long P = (long)a.Ho * a.Wo;
+  const int ntiles = (int)((P + PT - 1) / PT);
+  const int n = blockIdx.x / ntiles, tile = blockIdx.x % ntiles;
+  const int Cg = a.C / a.groups, Cog = a.Co / a.groups, K = a.kh * a.kw, cpg = a.C / a.dg;
+  const int ncot = (Cog + CO_T - 1) / CO_T;
+  const int gc = blockIdx.y / ncot, cot = blockIdx.y % ncot;
+  const int co0 = gc * Cog + cot * CO_T, co_end = min(co0 + CO_T, (gc + 1) * Cog);
+  const long p = (long)tile * PT + lane;
+  const bool pvalid = p < P;
+  const int ho = pvalid ? (int)(p / a.Wo) : 0, wo = pvalid ? (int)(p % a.Wo) : 0;
+  const long HW = (long)a.H * a.W;
+  const float *xn = a.x + (long)n * a.C * HW;
+
+  f32x4 acc[NCB];
+#pragma unroll
+  for (int m = 0; m < NCB; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int kr = lane >> 4, jj = lane & 15;
+  const int cbeg = gc * Cg, cend = (gc + 1) * Cg;
+  for (int k = 0; k < K; ++k) {
+    for (int c0 = cbeg; c0 < cend;) {
+      const int g = c0 / cpg;
+      const int c1 = min(min(c0 + KC, (g + 1) * cpg), cend);
+      const int rows = c1 - c0;
+      Samp s;
+      pixel_samp(s, a, n, g, k, pvalid ? p : 0, ho, wo);
+#pragma unroll
+      for (int ii = 0; ii < KC / 4; ++ii) {
+        const int cl = wave + 4 * ii;
+        float v = 0.f;
+        if (cl < rows && pvalid) v = samp_val(xn + (long)(c0 + cl) * HW, s);
+        sCol[cl * CP + lane] = v;
+      }
+      for (int e = tid; e < KC * CO_T; e += NT) {
+        const int cl = e % KC, col = e / KC;
+        const int co = co0 + col;
+        float v = 0.f;
+        if (cl < rows && co < co_end) v = a.weight[((long)co * Cg + (c0 + cl - cbeg)) * K + k];
+        sW[col * WP + cl] = v;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int ks = 0; ks < KC / 4; ++ks) {
+        const float bv = sCol[(4 * ks + kr) * CP + 16 * wave + jj];
+#pragma unroll
+        for (int m = 0; m < NCB; ++m) {
+          const float av = sW[(16 * m + jj) * WP + 4 * ks + kr];
+          acc[m] = mfma16x16x4(av, bv, acc[m]);
+        }
+      }
+      __syncthreads();
+      c0 = c1;
+    }
+  }
+
+  // Epilogue: lane holds pixel column jj, output channels 16m + 4kr + r.
+  const long pe = (long)tile * PT + 16 * wave + jj;
+  if (pe < P) {
+#pragma unroll
+    for (int m = 0; m < NCB; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + 16 * m + 4 * kr + r;
+        if (co < co_end) {
+          float v = acc[m][r];
+          if (a.bias) v += a.bias[co];
+          if (a.post_scale) v = v * a.post_scale[co] + a.post_shift[co];
+          a.out[((long)n * a.Co + co) * P + pe] = apply_act(v, a.act);
+        }
+      }
+  }
+}
+
+// --------------------------------------------------------------- debug: im2col / index --
+__global__ void mdcn_im2col_kernel(MdcnArgs a, float *__restrict__ col) {
+  const long P = (long)a.Ho * a.Wo;
+  const int K = a.kh * a.kw, cpg = a.C / a.dg;
+  const long total = (long)a.C * K * P;
+  const long HW = (long)a.H * a.W;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long)gridDim.x * blockDim.x) {
+    const long p = e % P;
+    const int ck = (int)(e / P), c = ck / K, k = ck % K;
+    Samp s;
+    pixel_samp(s, a, 0, c / cpg, k, p, (int)(p / a.Wo), (int)(p % a.Wo));
+    col[e] = samp_val(a.x + (long)c * HW, s);
+  }
+}
+
+__global__ void mdcn_sample_index_kernel(MdcnArgs a, int *__restrict__ hl, int *__restrict__ wl,
+                                         int *__restrict__ vd) {
+#pragma clang fp contract(off)
+  const long P = (long)a.Ho * a.Wo;
+  const int K = a.kh * a.kw;
+  const long total = (long)a.N * a.dg * K * P;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long)gridDim.x * blockDim.x) {
+    const long p = e % P;
+    long t = e / P;
+    const int k = (int)(t % K);
+    t /= K;
+    const int g = (int)(t % a.dg), n = (int)(t / a.dg);
+    const int i = k / a.kw, j = k % a.kw, ho = (int)(p / a.Wo), wo = (int)(p % a.Wo);
+    const float *off = a.offset + (long)n * a.off_bs + (long)g * 2 * K * P;
+    const float h = (float)(ho * a.stride - a.pad + i * a.dil) + off[(long)(2 * k) * P + p];
+    const float w = (float)(wo * a.stride - a.pad + j * a.dil) + off[(long)(2 * k + 1) * P + p];
+    hl[e] = (int)floorf(h);
+    wl[e] = (int)floorf(w);
+    vd[e] = (h > -1.f && w > -1.f && h < (float)a.H && w < (float)a.W) ? 1 : 0;
+  }
+}
+
+// ---------------------------------------------------------------------- backward --------
+// (1) data/coordinate gradients.  Workgroup = (image n, 64-pixel tile, deformable group g);
+// groups == 1.  gOut tile [Co][64] is staged in LDS once; per (tap k, <=32-channel chunk)
+// colg = W^T gOut is formed by MFMA into LDS (the reference's `columns` never touches HBM),
+// then each thread (pixel, channel subset) accumulates grad_mask / grad_offset partials
+// (kernel.cu:695-767) and scatters grad_x to the 4 bilinear corners (kernel.cu:635-693,
+// float atomics like the reference).
+__global__ __launch_bounds__(NT) void mdcn_bwd_data_kernel(MdcnArgs a, const float *__restrict__ gout,
+                                                           float *__restrict__ gx,
+                                                           float *__restrict__ goff,
+                                                           float *__restrict__ gmask, int GP,
+                                                           int WTP) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int Co = a.Co;
+  float *sG = sm;                       // [Co][GP]      gOut tile
+  float *sWt = sG + Co * GP;            // [KC][WTP]     W^T chunk
+  float *sCg = sWt + KC * WTP;          // [KC][CP]      colg chunk
+  float *sRed = sCg + KC * CP;          // [3][4][64]    cross-wave reduction
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long P = (long)a.Ho * a.Wo;
+  const int ntiles = (int)((P + PT - 1) / PT);
+  const int n = blockIdx.x / ntiles, tile = blockIdx.x % ntiles, g = blockIdx.y;
+  const int K = a.kh * a.kw, cpg = a.C / a.dg, C = a.C;
+  const long p = (long)tile * PT + lane;
+  const bool pvalid = p < P;
+  const int ho = pvalid ? (int)(p / a.Wo) : 0, wo = pvalid ? (int)(p % a.Wo) : 0;
+  const long HW = (long)a.H * a.W;
+  const float *xn = a.x + (long)n * C * HW;
+  float *gxn = gx + (long)n * C * HW;
+
+  for (int e = tid; e < Co * PT; e += NT) {
+    const int co = e / PT, pl = e % PT;
+    const long pp = (long)tile * PT + pl;
+    sG[co * GP + pl] = pp < P ? gout[((long)n * Co + co) * P + pp] : 0.f;
+  }
+
+  const int kr = lane >> 4, jj = lane & 15;
+  for (int k = 0; k < K; ++k) {
+    Samp s;
+    pixel_samp(s, a, n, g, k, pvalid ? p : 0, ho, wo);
+    float gm = 0.f, goh = 0.f, gow = 0.f;
+    for (int c0 = g * cpg; c0 < (g + 1) * cpg; c0 += KC) {
+      const int rows = min(KC, (g + 1) * cpg - c0);
+      __syncthreads();  // previous chunk's sCg / sWt readers are done
+      for (int e = tid; e < KC * Co; e += NT) {
+        const int cl = e % KC, co = e / KC;
+        sWt[cl * WTP + co] = cl < rows ? a.weight[((long)co * C + c0 + cl) * K + k] : 0.f;
+      }
+      __syncthreads();
+      // colg[c][px] = sum_co W[co][c][k] gOut[co][px]: 2 channel blocks x this wave's 16 px.
+      f32x4 cacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      for (int ks = 0; ks < Co / 4; ++ks) {
+        const float bv = sG[(4 * ks + kr) * GP + 16 * wave + jj];
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const float av = sWt[(16 * cb + jj) * WTP + 4 * ks + kr];
+          cacc[cb] = mfma16x16x4(av, bv, cacc[cb]);
+        }
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sCg[(16 * cb + 4 * kr + r) * CP + 16 * wave + jj] = cacc[cb][r];
+      __syncthreads();
+      if (pvalid && s.valid) {
+#pragma unroll 2
+        for (int ii = 0; ii < KC / 4; ++ii) {
+          const int cl = wave + 4 * ii;
+          if (cl >= rows) break;
+          const int c = c0 + cl;
+          const float cg = sCg[cl * CP + lane];
+          const float *im = xn + (long)c * HW;
+          const float v1 = (s.ok & 1) ? im[s.i1] : 0.f, v2 = (s.ok & 2) ? im[s.i2] : 0.f;
+          const float v3 = (s.ok & 4) ? im[s.i3] : 0.f, v4 = (s.ok & 8) ? im[s.i4] : 0.f;
+          const float hh = 1.f - s.lh, hw = 1.f - s.lw;
+          const float val = hh * hw * v1 + hh * s.lw * v2 + s.lh * hw * v3 + s.lh * s.lw * v4;
+          gm += cg * val;
+          const float wh = -hw * v1 - s.lw * v2 + hw * v3 + s.lw * v4;
+          const float ww = -hh * v1 + hh * v2 - s.lh * v3 + s.lh * v4;
+          const float top = cg * s.m;
+          goh += wh * top;
+          gow += ww * top;
+          float *gim = gxn + (long)c * HW;
+          if (s.ok & 1) atomicAdd(gim + s.i1, hh * hw * top);
+          if (s.ok & 2) atomicAdd(gim + s.i2, hh * s.lw * top);
+          if (s.ok & 4) atomicAdd(gim + s.i3, s.lh * hw * top);
+          if (s.ok & 8) atomicAdd(gim + s.i4, s.lh * s.lw * top);
+        }
+      }
+    }
+    // reduce the 4 waves' channel partials for each pixel
+    sRed[(0 * 4 + wave) * 64 + lane] = gm;
+    sRed[(1 * 4 + wave) * 64 + lane] = goh;
+    sRed[(2 * 4 + wave) * 64 + lane] = gow;
+    __syncthreads();
+    if (wave == 0 && pvalid) {
+      float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        t0 += sRed[(0 * 4 + q) * 64 + lane];
+        t1 += sRed[(1 * 4 + q) * 64 + lane];
+        t2 += sRed[(2 * 4 + q) * 64 + lane];
+      }
+      const long ob = (long)n * a.dg * 2 * K * P + (long)g * 2 * K * P;
+      goff[ob + (long)(2 * k) * P + p] = t1;
+      goff[ob + (long)(2 * k + 1) * P + p] = t2;
+      gmask[(long)n * a.dg * K * P + ((long)g * K + k) * P + p] = t0;
+    }
+  }
+}
+
+// (2) weight gradient: gW[co][c][k] += sum_{n,p} gOut[n][co][p] * col[c*K+k][n,p].
+// Workgroup = one K chunk (tap k, <=32 channels of group g) x one range of pixels (all
+// images flattened) x one 64-wide output-channel tile.  The col chunk is re-sampled into LDS
+// per 64-pixel sub-tile, the [co][c] tile accumulates in MFMA registers across the whole
+// pixel range, then one float atomic per element (grad accumulates, cpp:660-669).
+__global__ __launch_bounds__(NT) void mdcn_bwd_weight_kernel(MdcnArgs a, const float *__restrict__ gout,
+                                                             float *__restrict__ gw, int npieces,
+                                                             long range) {
+  constexpr int GP2 = PT + 2;  // A/B reads (16 rows x 4 cols per 16 lanes) conflict-free
+  __shared__ __attribute__((aligned(16))) float sG[64 * GP2];
+  __shared__ __attribute__((aligned(16))) float sC[KC * GP2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long P = (long)a.Ho * a.Wo, T = (long)a.N * P;
+  const int K = a.kh * a.kw, cpg = a.C / a.dg, C = a.C, Co = a.Co;
+  const int chunk = blockIdx.x;
+  const int k = chunk / (a.dg * npieces), rem = chunk % (a.dg * npieces);
+  const int g = rem / npieces, piece = rem % npieces;
+  const int c0 = g * cpg + piece * KC, rows = min(KC, (g + 1) * cpg - c0);
+  const int co0 = blockIdx.z * 64;
+  const long r0 = (long)blockIdx.y * range, r1 = min(r0 + range, T);
+  const long HW = (long)a.H * a.W;
+  const int kr = lane >> 4, jj = lane & 15;
+  // wave w: output-channel block w (16 co), both 16-channel blocks of the chunk
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  for (long t0 = r0; t0 < r1; t0 += PT) {
+    const long t = t0 + lane;
+    const bool tv = t < r1;
+    const int n = tv ? (int)(t / P) : 0;
+    const long p = tv ? t % P : 0;
+    Samp s;
+    pixel_samp(s, a, n, g, k, p, (int)(p / a.Wo), (int)(p % a.Wo));
+    const float *xn = a.x + (long)n * C * HW;
+#pragma unroll
+    for (int ii = 0; ii < KC / 4; ++ii) {
+      const int cl = wave + 4 * ii;
+      float v = 0.f;
+      if (cl < rows && tv) v = samp_val(xn + (long)(c0 + cl) * HW, s);
+      sC[cl * GP2 + lane] = v;
+    }
+    for (int e = tid; e < 64 * PT; e += NT) {
+      const int col = e / PT, pl = e % PT;
+      const long tt = t0 + pl;
+      const int co = co0 + col;
+      float v = 0.f;
+      if (tt < r1 && co < Co) v = gout[((long)(tt / P) * Co + co) * P + tt % P];
+      sG[col * GP2 + pl] = v;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int ks = 0; ks < PT / 4; ++ks) {
+      const float av = sG[(16 * wave + jj) * GP2 + 4 * ks + kr];
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const float bv = sC[(16 * cb + jj) * GP2 + 4 * ks + kr];
+        acc[cb] = mfma16x16x4(av, bv, acc[cb]);
+      }
+    }
+    __syncthreads();
+  }
+  // D[i = co (4kr + r)][jj = channel]
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + 16 * wave + 4 * kr + r, cl = 16 * cb + jj;
+      if (co < Co && cl < rows) atomicAdd(gw + ((long)co * C + c0 + cl) * K + k, acc[cb][r]);
+    }
+}
+
+__global__ __launch_bounds__(256) void bias_grad_kernel(const float *__restrict__ gout,
+                                                        float *__restrict__ gb, int N, int Co,
+                                                        long P) {
+  const int co = blockIdx.x;
+  float s = 0.f;
+  for (int n = 0; n < N; ++n)
+    for (long p = threadIdx.x; p < P; p += 256) s += gout[((long)n * Co + co) * P + p];
+  __shared__ float red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) gb[co] += red[0];
+}
+
+int check_shapes(const MdcnArgs &a) {
+  if (a.N <= 0 || a.C <= 0 || a.H <= 0 || a.W <= 0 || a.Co <= 0 || a.kh <= 0 || a.kw <= 0 ||
+      a.stride <= 0 || a.pad < 0 || a.dil <= 0 || a.groups <= 0 || a.dg <= 0)
+    return AANET_EINVAL;
+  if (a.C % a.groups || a.Co % a.groups || a.C % a.dg) return AANET_EINVAL;
+  if (a.Ho <= 0 || a.Wo <= 0) return AANET_EINVAL;
+  return AANET_OK;
+}
+
+MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float *mask,
+                   long mask_bs, int mask_logits, float mask_scale, const float *weight,
+                   const float *bias, const float *ps, const float *psh, int act, float *out,
+                   int n, int c, int h, int w, int co, int kh, int kw, int stride, int pad,
+                   int dil, int groups, int dg) {
+  MdcnArgs a;
+  a.x = x;
+  a.offset = offset;
+  a.mask = mask;
+  a.mask_logits = mask_logits;
+  a.mask_scale = mask_scale;
+  a.weight = weight;
+  a.bias = bias;
+  a.post_scale = ps;
+  a.post_shift = psh;
+  a.act = act;
+  a.out = out;
+  a.N = n;
+  a.C = c;
+  a.H = h;
+  a.W = w;
+  a.Co = co;
+  a.kh = kh;
+  a.kw = kw;
+  a.stride = stride;
+  a.pad = pad;
+  a.dil = dil;
+  a.groups = groups;
+  a.dg = dg;
+  a.Ho = conv_out_size(h, kh, stride, pad, dil);
+  a.Wo = conv_out_size(w, kw, stride, pad, dil);
+  const long P = (long)a.Ho * a.Wo, K = (long)kh * kw;
+  a.off_bs = off_bs >= 0 ? off_bs : (long)dg * 2 * K * P;
+  a.mask_bs = mask_bs >= 0 ? mask_bs : (long)dg * K * P;
+  return a;
+}
+
+int launch_fwd(const MdcnArgs &a, hipStream_t st) {
+  const int rc = check_shapes(a);
+  if (rc) return rc;
+  if (!a.x || !a.offset || !a.mask || !a.weight || !a.out) return AANET_EINVAL;
+  if (a.post_scale && !a.post_shift) return AANET_EINVAL;
+  const long P = (long)a.Ho * a.Wo;
+  const int Cog = a.Co / a.groups;
+  const int co_t = Cog <= 16 ? 16 : (Cog <= 32 ? 32 : 64);
+  const int ncot = host_div_up(Cog, co_t);
+  dim3 grid((unsigned)(a.N * host_div_up(P, PT)), (unsigned)(a.groups * ncot));
+  switch (co_t) {
+    case 16: hipLaunchKernelGGL(mdcn_fwd_kernel<16>, grid, dim3(NT), 0, st, a); break;
+    case 32: hipLaunchKernelGGL(mdcn_fwd_kernel<32>, grid, dim3(NT), 0, st, a); break;
+    default: hipLaunchKernelGGL(mdcn_fwd_kernel<64>, grid, dim3(NT), 0, st, a); break;
+  }
+  return aanet_launch_status();
+}
+
+int round_pitch(int v, int mod32) {  // smallest p >= v with p % 32 == mod32
+  int p = v;
+  while (p % 32 != mod32) ++p;
+  return p;
+}
+
+}  // namespace
+
+extern "C" int aanet_mdcn_fwd_f32(const float *x, const float *offset, const float *mask,
+                                  const float *weight, const float *bias, float *out, int n, int c,
+                                  int h, int w, int co, int kh, int kw, int stride, int pad,
+                                  int dil, int groups, int dg, aanet_stream_t stream) {
+  MdcnArgs a = make_args(x, offset, -1, mask, -1, 0, 1.f, weight, bias, nullptr, nullptr, 0, out,
+                         n, c, h, w, co, kh, kw, stride, pad, dil, groups, dg);
+  return launch_fwd(a, as_hip(stream));
+}
+
+extern "C" int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset,
+                                        long offset_batch_stride, const float *mask,
+                                        long mask_batch_stride, int mask_logits, float mask_scale,
+                                        const float *weight, const float *bias,
+                                        const float *post_scale, const float *post_shift, int act,
+                                        float *out, int n, int c, int h, int w, int co, int kh,
+                                        int kw, int stride, int pad, int dil, int groups, int dg,
+                                        aanet_stream_t stream) {
+  if (act < 0 || act > 2) return AANET_EINVAL;
+  MdcnArgs a = make_args(x, offset, offset_batch_stride, mask, mask_batch_stride, mask_logits,
+                         mask_scale, weight, bias, post_scale, post_shift, act, out, n, c, h, w,
+                         co, kh, kw, stride, pad, dil, groups, dg);
+  return launch_fwd(a, as_hip(stream));
+}
+
+extern "C" int aanet_mdcn_im2col_f32(const float *x, const float *offset, const float *mask,
+                                     float *col, int c, int h, int w, int kh, int kw, int stride,
+                                     int pad, int dil, int dg, aanet_stream_t stream) {
+  MdcnArgs a = make_args(x, offset, -1, mask, -1, 0, 1.f, nullptr, nullptr, nullptr, nullptr, 0,
+                         nullptr, 1, c, h, w, 1, kh, kw, stride, pad, dil, 1, dg);
+  const int rc = check_shapes(a);
+  if (rc) return rc;
+  if (!x || !offset || !mask || !col) return AANET_EINVAL;
+  const long total = (long)c * kh * kw * a.Ho * a.Wo;
+  hipLaunchKernelGGL(mdcn_im2col_kernel, dim3(host_div_up(total, 256) > 8192 ? 8192 : host_div_up(total, 256)),
+                     dim3(256), 0, as_hip(stream), a, col);
+  return aanet_launch_status();
+}
+
+extern "C" int aanet_mdcn_sample_index(const float *offset, int *h_low, int *w_low, int *valid,
+                                       int n, int h, int w, int kh, int kw, int stride, int pad,
+                                       int dil, int dg, aanet_stream_t stream) {
+  MdcnArgs a = make_args(nullptr, offset, -1, nullptr, -1, 0, 1.f, nullptr, nullptr, nullptr,
+                         nullptr, 0, nullptr, n, dg, h, w, 1, kh, kw, stride, pad, dil, 1, dg);
+  const int rc = check_shapes(a);
+  if (rc) return rc;
+  if (!offset || !h_low || !w_low || !valid) return AANET_EINVAL;
+  const long total = (long)n * dg * kh * kw * a.Ho * a.Wo;
+  hipLaunchKernelGGL(mdcn_sample_index_kernel,
+                     dim3(host_div_up(total, 256) > 8192 ? 8192 : host_div_up(total, 256)), dim3(256),
+                     0, as_hip(stream), a, h_low, w_low, valid);
+  return aanet_launch_status();
+}
+
+extern "C" int aanet_mdcn_bwd_f32(const float *x, const float *offset, const float *mask,
+                                  const float *weight, const float *grad_out, float *grad_x,
+                                  float *grad_offset, float *grad_mask, float *grad_weight,
+                                  float *grad_bias, int n, int c, int h, int w, int co, int kh,
+                                  int kw, int stride, int pad, int dil, int groups, int dg,
+                                  aanet_stream_t stream) {
+  MdcnArgs a = make_args(x, offset, -1, mask, -1, 0, 1.f, weight, nullptr, nullptr, nullptr, 0,
+                         nullptr, n, c, h, w, co, kh, kw, stride, pad, dil, groups, dg);
+  int rc = check_shapes(a);
+  if (rc) return rc;
+  if (!x || !offset || !mask || !weight || !grad_out || !grad_x || !grad_offset || !grad_mask ||
+      !grad_weight)
+    return AANET_EINVAL;
+  if (groups != 1) return AANET_EUNSUPPORTED;  // AANet uses groups=1 (nets/deform.py:25)
+  if (co % 4 || co > 256) return AANET_EUNSUPPORTED;
+  hipStream_t st = as_hip(stream);
+  const long P = (long)a.Ho * a.Wo;
+  const int K = kh * kw, cpg = c / dg;
+  hipError_t e = hipMemsetAsync(grad_x, 0, sizeof(float) * (size_t)n * c * h * w, st);
+  if (e != hipSuccess) return (int)e;
+  const int GP = round_pitch(PT, 16), WTP = round_pitch(co, 2);
+  const size_t smem = sizeof(float) * ((size_t)co * GP + (size_t)KC * WTP + (size_t)KC * CP + 3 * 4 * 64);
+  if (smem > 64 * 1024) return AANET_EUNSUPPORTED;
+  hipLaunchKernelGGL(mdcn_bwd_data_kernel, dim3((unsigned)(n * host_div_up(P, PT)), (unsigned)dg),
+                     dim3(NT), smem, st, a, grad_out, grad_x, grad_offset, grad_mask, GP, WTP);
+  rc = aanet_launch_status();
+  if (rc) return rc;
+  const int npieces = host_div_up(cpg, KC);
+  const long T = (long)n * P;
+  const int nchunks = K * dg * npieces;
+  // ~2048 workgroups in total; each covers `range` flattened pixels
+  long nsplit = 2048 / nchunks;
+  if (nsplit < 1) nsplit = 1;
+  long range = (T + nsplit - 1) / nsplit;
+  range = ((range + PT - 1) / PT) * PT;
+  nsplit = (T + range - 1) / range;
+  hipLaunchKernelGGL(mdcn_bwd_weight_kernel, dim3(nchunks, (unsigned)nsplit, host_div_up(co, 64)),
+                     dim3(NT), 0, st, a, grad_out, grad_weight, npieces, range);
+  rc = aanet_launch_status();
+  if (rc) return rc;
+  if (grad_bias) {
+    hipLaunchKernelGGL(bias_grad_kernel, dim3(co), dim3(256), 0, st, grad_out, grad_bias, n, co, P);
+    rc = aanet_launch_status();
+  }
+  return rc;
+}

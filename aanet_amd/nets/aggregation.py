@@ -1,0 +1,155 @@
+"""Drop-in for the adaptive aggregation of nets/aggregation.py (ISA + CSA).
+
+AdaptiveAggregationModule (aggregation.py:313-402) and AdaptiveAggregation (406-464) with the
+reference's constructor signatures, module tree (state-dict keys `fusions.{f}.branches.{s}.0.*`,
+`fusions.{f}.fuse_layers.{i}.{j}.*`, `final_conv.{i}.*`) and forward semantics, including the
+in-place mutation of the caller's list (`x[i] = dconv(x[i])`, aggregation.py:382).
+ISA bottlenecks run the HIP DCN; in eval mode BN is folded into the CSA convs.
+The 3D-conv aggregators (StereoNet/PSMNet/GCNet) are out of scope.
+"""
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ._fuse import conv_bn_act, use_fused
+from .deform import DeformSimpleBottleneck, SimpleBottleneck
+
+
+class AdaptiveAggregationModule(nn.Module):
+    def __init__(self, num_scales, num_output_branches, max_disp, num_blocks=1,
+                 simple_bottleneck=False, deformable_groups=2, mdconv_dilation=2):
+        super(AdaptiveAggregationModule, self).__init__()
+        self.num_scales = num_scales
+        self.num_output_branches = num_output_branches
+        self.max_disp = max_disp
+        self.num_blocks = num_blocks
+
+        self.branches = nn.ModuleList()
+        # Adaptive intra-scale aggregation (aggregation.py:328-340)
+        for i in range(self.num_scales):
+            num_candidates = max_disp // (2 ** i)
+            branch = nn.ModuleList()
+            for j in range(num_blocks):
+                if simple_bottleneck:
+                    branch.append(SimpleBottleneck(num_candidates, num_candidates))
+                else:
+                    branch.append(DeformSimpleBottleneck(num_candidates, num_candidates,
+                                                         modulation=True,
+                                                         mdconv_dilation=mdconv_dilation,
+                                                         deformable_groups=deformable_groups))
+            self.branches.append(nn.Sequential(*branch))
+
+        # Adaptive cross-scale aggregation (aggregation.py:342-371)
+        self.fuse_layers = nn.ModuleList()
+        for i in range(self.num_output_branches):
+            self.fuse_layers.append(nn.ModuleList())
+            for j in range(self.num_scales):
+                if i == j:
+                    self.fuse_layers[-1].append(nn.Identity())
+                elif i < j:
+                    self.fuse_layers[-1].append(
+                        nn.Sequential(nn.Conv2d(max_disp // (2 ** j), max_disp // (2 ** i),
+                                                kernel_size=1, bias=False),
+                                      nn.BatchNorm2d(max_disp // (2 ** i))))
+                else:
+                    layers = nn.ModuleList()
+                    for k in range(i - j - 1):
+                        layers.append(nn.Sequential(
+                            nn.Conv2d(max_disp // (2 ** j), max_disp // (2 ** j), kernel_size=3,
+                                      stride=2, padding=1, bias=False),
+                            nn.BatchNorm2d(max_disp // (2 ** j)),
+                            nn.LeakyReLU(0.2, inplace=True)))
+                    layers.append(nn.Sequential(
+                        nn.Conv2d(max_disp // (2 ** j), max_disp // (2 ** i), kernel_size=3,
+                                  stride=2, padding=1, bias=False),
+                        nn.BatchNorm2d(max_disp // (2 ** i))))
+                    self.fuse_layers[-1].append(nn.Sequential(*layers))
+
+        self.relu = nn.LeakyReLU(0.2, inplace=True)
+
+    def _exchange(self, i, j, xj, fused):
+        layer = self.fuse_layers[i][j]
+        if not fused or i == j:
+            return layer(xj)
+        if i < j:
+            return conv_bn_act(xj, layer[0], layer[1], None)
+        y = xj
+        for k, seq in enumerate(layer):
+            last = k == len(layer) - 1
+            y = conv_bn_act(y, seq[0], seq[1], None if last else "leaky")
+        return y
+
+    def forward(self, x):
+        """aggregation.py:375-402."""
+        assert len(self.branches) == len(x)
+        for i in range(len(self.branches)):
+            branch = self.branches[i]
+            for j in range(self.num_blocks):
+                dconv = branch[j]
+                x[i] = dconv(x[i])
+
+        if self.num_scales == 1:  # without fusions
+            return x
+
+        fused = use_fused(self, x[0])
+        x_fused = []
+        for i in range(len(self.fuse_layers)):
+            for j in range(len(self.branches)):
+                if j == 0:
+                    x_fused.append(self._exchange(i, 0, x[0], fused))
+                else:
+                    exchange = self._exchange(i, j, x[j], fused)
+                    if exchange.size()[2:] != x_fused[i].size()[2:]:
+                        exchange = F.interpolate(exchange, size=x_fused[i].size()[2:],
+                                                 mode='bilinear', align_corners=False)
+                    x_fused[i] = x_fused[i] + exchange
+
+        for i in range(len(x_fused)):
+            x_fused[i] = self.relu(x_fused[i])
+        return x_fused
+
+
+class AdaptiveAggregation(nn.Module):
+    """Stacked AAModules (aggregation.py:406-464)."""
+
+    def __init__(self, max_disp, num_scales=3, num_fusions=6, num_stage_blocks=1,
+                 num_deform_blocks=2, intermediate_supervision=True, deformable_groups=2,
+                 mdconv_dilation=2):
+        super(AdaptiveAggregation, self).__init__()
+        self.max_disp = max_disp
+        self.num_scales = num_scales
+        self.num_fusions = num_fusions
+        self.intermediate_supervision = intermediate_supervision
+
+        fusions = nn.ModuleList()
+        for i in range(num_fusions):
+            if self.intermediate_supervision:
+                num_out_branches = self.num_scales
+            else:
+                num_out_branches = 1 if i == num_fusions - 1 else self.num_scales
+            simple_bottleneck_module = not (i >= num_fusions - num_deform_blocks)
+            fusions.append(AdaptiveAggregationModule(num_scales=self.num_scales,
+                                                     num_output_branches=num_out_branches,
+                                                     max_disp=max_disp,
+                                                     num_blocks=num_stage_blocks,
+                                                     mdconv_dilation=mdconv_dilation,
+                                                     deformable_groups=deformable_groups,
+                                                     simple_bottleneck=simple_bottleneck_module))
+        self.fusions = nn.Sequential(*fusions)
+
+        self.final_conv = nn.ModuleList()
+        for i in range(self.num_scales):
+            in_channels = max_disp // (2 ** i)
+            self.final_conv.append(nn.Conv2d(in_channels, max_disp // (2 ** i), kernel_size=1))
+            if not self.intermediate_supervision:
+                break
+
+    def forward(self, cost_volume):
+        """aggregation.py:452-464."""
+        assert isinstance(cost_volume, list)
+        for i in range(self.num_fusions):
+            fusion = self.fusions[i]
+            cost_volume = fusion(cost_volume)
+        out = []  # 1/3, 1/6, 1/12
+        for i in range(len(self.final_conv)):
+            out = out + [self.final_conv[i](cost_volume[i])]
+        return out

@@ -1,0 +1,195 @@
+"""Drop-in for nets/deform.py (DeformConv2d and the ISA bottlenecks).
+
+Module trees and parameter names are the reference's, so state dicts load unchanged:
+  DeformConv2d          nets/deform.py:17-97  (offset_conv + deform_conv)
+  DeformBottleneck      nets/deform.py:100-141
+  SimpleBottleneck      nets/deform.py:144-184
+  DeformSimpleBottleneck nets/deform.py:187-236
+Training mode runs the reference op order with autograd (the DCN through the HIP
+ModulatedDeformConvFunction).  Eval mode without autograd takes the fused path: BN folded
+into the 1x1/3x3 convs, and the deformable conv2 -> bn2 -> ReLU done by ONE kernel that reads
+the offset_conv output in place (offset slice + 2*sigmoid(mask logits)) and applies BN+ReLU
+in its epilogue.
+"""
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from ._fuse import bn_affine, conv_bn_act, use_fused
+from .deform_conv import DeformConv, ModulatedDeformConv
+
+
+def conv3x3(in_planes, out_planes, stride=1, groups=1, dilation=1):
+    """3x3 convolution with padding (nets/deform.py:6-9)."""
+    return nn.Conv2d(in_planes, out_planes, kernel_size=3, stride=stride, padding=dilation,
+                     groups=groups, bias=False, dilation=dilation)
+
+
+def conv1x1(in_planes, out_planes, stride=1):
+    """1x1 convolution (nets/deform.py:12-14)."""
+    return nn.Conv2d(in_planes, out_planes, kernel_size=1, stride=stride, bias=False)
+
+
+class DeformConv2d(nn.Module):
+    """A single (modulated) deformable conv layer (nets/deform.py:17-97)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, stride=1, dilation=2, groups=1,
+                 deformable_groups=2, modulation=True, double_mask=True, bias=False):
+        super(DeformConv2d, self).__init__()
+        self.modulation = modulation
+        self.deformable_groups = deformable_groups
+        self.kernel_size = kernel_size
+        self.double_mask = double_mask
+        if self.modulation:
+            self.deform_conv = ModulatedDeformConv(in_channels, out_channels,
+                                                   kernel_size=kernel_size, stride=stride,
+                                                   padding=dilation, dilation=dilation,
+                                                   groups=groups,
+                                                   deformable_groups=deformable_groups, bias=bias)
+        else:
+            self.deform_conv = DeformConv(in_channels, out_channels, kernel_size=kernel_size,
+                                          stride=stride, padding=dilation, dilation=dilation,
+                                          groups=groups, deformable_groups=deformable_groups,
+                                          bias=bias)
+        k = 3 if self.modulation else 2
+        offset_out_channels = deformable_groups * k * kernel_size * kernel_size
+        # Group-wise offset learning (deform.py:69-72); zero init (deform.py:74-76)
+        self.offset_conv = nn.Conv2d(in_channels, offset_out_channels, kernel_size=kernel_size,
+                                     stride=stride, padding=dilation, dilation=dilation,
+                                     groups=deformable_groups, bias=True)
+        nn.init.constant_(self.offset_conv.weight, 0.)
+        nn.init.constant_(self.offset_conv.bias, 0.)
+
+    def forward(self, x):
+        if self.modulation:
+            offset_mask = self.offset_conv(x)
+            offset_channel = self.deformable_groups * 2 * self.kernel_size * self.kernel_size
+            offset = offset_mask[:, :offset_channel, :, :]
+            mask = offset_mask[:, offset_channel:, :, :]
+            mask = mask.sigmoid()
+            if self.double_mask:
+                mask = mask * 2
+            return self.deform_conv(x, offset, mask)
+        offset = self.offset_conv(x)
+        return self.deform_conv(x, offset)
+
+    def forward_fused(self, x, bn=None, act=0):
+        """Eval path: offset_conv (MIOpen) -> one HIP kernel for DCN (+BN, +act)."""
+        dc = self.deform_conv
+        offset_mask = self.offset_conv(x)
+        ps, psh = bn_affine(bn) if bn is not None else (None, None)
+        return ops.mdcn_forward_fused(x.contiguous(), offset_mask.contiguous(), dc.weight,
+                                      dc.bias, ps, psh, act, dc.stride, dc.padding, dc.dilation,
+                                      self.deformable_groups,
+                                      2.0 if self.double_mask else 1.0)
+
+
+class _BottleneckBase(nn.Module):
+    def _forward_ref(self, x):
+        identity = x
+        out = self.conv1(x)
+        out = self.bn1(out)
+        out = self.relu(out)
+        out = self.conv2(out)
+        out = self.bn2(out)
+        out = self.relu(out)
+        out = self.conv3(out)
+        out = self.bn3(out)
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        out += identity
+        out = self.relu(out)
+        return out
+
+    def _forward_fused(self, x, deform):
+        out = conv_bn_act(x, self.conv1, self.bn1, "relu")
+        if deform and self.conv2.modulation:
+            out = self.conv2.forward_fused(out, self.bn2, act=1)
+        else:
+            if deform:
+                out = self.bn2(self.conv2(out))
+                out = F.relu_(out)
+            else:
+                out = conv_bn_act(out, self.conv2, self.bn2, "relu")
+        out = conv_bn_act(out, self.conv3, self.bn3, None)
+        identity = self.downsample(x) if self.downsample is not None else x
+        out += identity
+        return F.relu_(out)
+
+
+class DeformBottleneck(_BottleneckBase):
+    """nets/deform.py:100-141 (feature-extractor block; reuses the HIP DCN)."""
+    expansion = 4
+    __constants__ = ['downsample']
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64,
+                 dilation=1, norm_layer=None):
+        super(DeformBottleneck, self).__init__()
+        if norm_layer is None:
+            norm_layer = nn.BatchNorm2d
+        width = int(planes * (base_width / 64.)) * groups
+        self.conv1 = conv1x1(inplanes, width)
+        self.bn1 = norm_layer(width)
+        self.conv2 = DeformConv2d(width, width, stride=stride)
+        self.bn2 = norm_layer(width)
+        self.conv3 = conv1x1(width, planes * self.expansion)
+        self.bn3 = norm_layer(planes * self.expansion)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        return self._forward_ref(x)
+
+
+class SimpleBottleneck(_BottleneckBase):
+    """Simple bottleneck block without channel expansion (nets/deform.py:144-184)."""
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64,
+                 dilation=1, norm_layer=None):
+        super(SimpleBottleneck, self).__init__()
+        if norm_layer is None:
+            norm_layer = nn.BatchNorm2d
+        width = int(planes * (base_width / 64.)) * groups
+        self.conv1 = conv1x1(inplanes, width)
+        self.bn1 = norm_layer(width)
+        self.conv2 = conv3x3(width, width, stride, groups, dilation)
+        self.bn2 = norm_layer(width)
+        self.conv3 = conv1x1(width, planes)
+        self.bn3 = norm_layer(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        if use_fused(self, x):
+            return self._forward_fused(x, deform=False)
+        return self._forward_ref(x)
+
+
+class DeformSimpleBottleneck(_BottleneckBase):
+    """Used for cost aggregation (nets/deform.py:187-236)."""
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64,
+                 norm_layer=None, mdconv_dilation=2, deformable_groups=2, modulation=True,
+                 double_mask=True):
+        super(DeformSimpleBottleneck, self).__init__()
+        if norm_layer is None:
+            norm_layer = nn.BatchNorm2d
+        width = int(planes * (base_width / 64.)) * groups
+        self.conv1 = conv1x1(inplanes, width)
+        self.bn1 = norm_layer(width)
+        self.conv2 = DeformConv2d(width, width, stride=stride, dilation=mdconv_dilation,
+                                  deformable_groups=deformable_groups, modulation=modulation,
+                                  double_mask=double_mask)
+        self.bn2 = norm_layer(width)
+        self.conv3 = conv1x1(width, planes)
+        self.bn3 = norm_layer(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        if use_fused(self, x):
+            return self._forward_fused(x, deform=True)
+        return self._forward_ref(x)

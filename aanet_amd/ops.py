@@ -1,0 +1,228 @@
+"""Torch-facing ops over the C ABI (autograd Functions + functional forms).
+
+Each op allocates its outputs with torch (caching allocator, device memory) and launches on
+torch's current HIP stream through ``_lib.call`` -- capturable into a HIP graph.
+"""
+import torch
+from torch.autograd import Function
+from torch.autograd.function import once_differentiable
+
+from . import _lib
+from ._lib import call, ptr, require_gpu, stream_of
+
+
+def _out_size(n, k, s, p, d):
+    return (n + 2 * p - (d * (k - 1) + 1)) // s + 1
+
+
+# ------------------------------------------------------------------ cost volumes --------
+def corr_volume(left, right, max_disp, out=None):
+    """nets/cost.py:40-48 -> [B, D, H, W]."""
+    require_gpu(left, right, names=("left", "right"))
+    B, C, H, W = left.shape
+    if right.shape != left.shape:
+        raise ValueError("left/right feature shapes differ")
+    if out is None:
+        out = torch.empty((B, max_disp, H, W), device=left.device, dtype=left.dtype)
+    call("aanet_corr_volume_f32", ptr(left), ptr(right), ptr(out), B, C, H, W, max_disp,
+         stream_of(left))
+    return out
+
+
+def shift_volume(left, right, max_disp, concat):
+    """nets/cost.py:22-38 (difference / concat) -> [B, C', D, H, W]."""
+    require_gpu(left, right, names=("left", "right"))
+    B, C, H, W = left.shape
+    oc = 2 * C if concat else C
+    out = torch.empty((B, oc, max_disp, H, W), device=left.device, dtype=left.dtype)
+    name = "aanet_concat_volume_f32" if concat else "aanet_diff_volume_f32"
+    call(name, ptr(left), ptr(right), ptr(out), B, C, H, W, max_disp, stream_of(left))
+    return out
+
+
+class CorrelationVolumeFunction(Function):
+    @staticmethod
+    def forward(ctx, left, right, max_disp):
+        left, right = left.contiguous(), right.contiguous()
+        ctx.save_for_backward(left, right)
+        ctx.max_disp = max_disp
+        return corr_volume(left, right, max_disp)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_out):
+        left, right = ctx.saved_tensors
+        grad_out = grad_out.contiguous()
+        require_gpu(grad_out, names=("grad_out",))
+        gl, gr = torch.empty_like(left), torch.empty_like(right)
+        B, C, H, W = left.shape
+        call("aanet_corr_volume_bwd_f32", ptr(left), ptr(right), ptr(grad_out), ptr(gl), ptr(gr),
+             B, C, H, W, ctx.max_disp, stream_of(left))
+        return gl, gr, None
+
+
+class ShiftVolumeFunction(Function):
+    @staticmethod
+    def forward(ctx, left, right, max_disp, concat):
+        left, right = left.contiguous(), right.contiguous()
+        ctx.shape, ctx.max_disp, ctx.concat = left.shape, max_disp, concat
+        return shift_volume(left, right, max_disp, concat)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_out):
+        grad_out = grad_out.contiguous()
+        require_gpu(grad_out, names=("grad_out",))
+        B, C, H, W = ctx.shape
+        gl = grad_out.new_empty((B, C, H, W))
+        gr = grad_out.new_empty((B, C, H, W))
+        name = "aanet_concat_volume_bwd_f32" if ctx.concat else "aanet_diff_volume_bwd_f32"
+        call(name, ptr(grad_out), ptr(gl), ptr(gr), B, C, H, W, ctx.max_disp, stream_of(grad_out))
+        return gl, gr, None, None
+
+
+# ------------------------------------------------------------ disparity regression ------
+def disp_regress(cost, negate=False, out=None):
+    """nets/estimation.py:13-30 -> [B, H, W]."""
+    require_gpu(cost, names=("cost",))
+    B, D, H, W = cost.shape
+    if out is None:
+        out = torch.empty((B, H, W), device=cost.device, dtype=cost.dtype)
+    call("aanet_disp_regress_f32", ptr(cost), ptr(out), B, D, H, W, int(bool(negate)),
+         stream_of(cost))
+    return out
+
+
+class DisparityRegressionFunction(Function):
+    @staticmethod
+    def forward(ctx, cost, negate):
+        cost = cost.contiguous()
+        ctx.save_for_backward(cost)
+        ctx.negate = negate
+        return disp_regress(cost, negate)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_disp):
+        (cost,) = ctx.saved_tensors
+        grad_disp = grad_disp.contiguous()
+        require_gpu(grad_disp, names=("grad_disp",))
+        gc = torch.empty_like(cost)
+        B, D, H, W = cost.shape
+        call("aanet_disp_regress_bwd_f32", ptr(cost), ptr(grad_disp), ptr(gc), B, D, H, W,
+             int(bool(ctx.negate)), stream_of(cost))
+        return gc, None
+
+
+# ------------------------------------------------------- modulated deformable conv ------
+def mdcn_forward(x, offset, mask, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
+                 deformable_groups=1, out=None):
+    """deform_conv_cuda.cpp:490-569 -> [N, Co, Ho, Wo]."""
+    require_gpu(x, offset, mask, weight, bias, names=("input", "offset", "mask", "weight", "bias"))
+    N, C, H, W = x.shape
+    Co, _, kh, kw = weight.shape
+    Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
+    if out is None:
+        out = torch.empty((N, Co, Ho, Wo), device=x.device, dtype=x.dtype)
+    call("aanet_mdcn_fwd_f32", ptr(x), ptr(offset), ptr(mask), ptr(weight), ptr(bias), ptr(out),
+         N, C, H, W, Co, kh, kw, stride, padding, dilation, groups, deformable_groups, stream_of(x))
+    return out
+
+
+def mdcn_forward_fused(x, offset_mask, weight, bias=None, post_scale=None, post_shift=None, act=0,
+                       stride=1, padding=0, dilation=1, deformable_groups=1, mask_scale=2.0):
+    """Eval fast path of DeformConv2d (nets/deform.py:78-97) + BN + activation.
+
+    offset_mask is the raw offset_conv output [N, dg*3*K, Ho, Wo]: channels [0, 2*dg*K) are
+    offsets, the rest mask logits (m = mask_scale * sigmoid), read in place (no slicing copies).
+    """
+    require_gpu(x, offset_mask, weight, bias, post_scale, post_shift,
+                names=("input", "offset_mask", "weight", "bias", "post_scale", "post_shift"))
+    N, C, H, W = x.shape
+    Co, _, kh, kw = weight.shape
+    K = kh * kw
+    Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
+    if offset_mask.shape != (N, deformable_groups * 3 * K, Ho, Wo):
+        raise ValueError(f"offset_mask shape {tuple(offset_mask.shape)} unexpected")
+    out = torch.empty((N, Co, Ho, Wo), device=x.device, dtype=x.dtype)
+    bs = offset_mask.stride(0)
+    mask_ptr = offset_mask.data_ptr() + 4 * deformable_groups * 2 * K * Ho * Wo
+    call("aanet_mdcn_fwd_fused_f32", ptr(x), ptr(offset_mask), bs, _lib.ctypes.c_void_p(mask_ptr),
+         bs, 1, float(mask_scale), ptr(weight), ptr(bias), ptr(post_scale), ptr(post_shift),
+         int(act), ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation, 1,
+         deformable_groups, stream_of(x))
+    return out
+
+
+def mdcn_backward(x, offset, mask, weight, grad_out, with_bias, stride, padding, dilation, groups,
+                  deformable_groups):
+    """deform_conv_cuda.cpp:571-685 -> (gX, gOffset, gMask, gW, gB or None)."""
+    require_gpu(x, offset, mask, weight, grad_out,
+                names=("input", "offset", "mask", "weight", "grad_output"))
+    N, C, H, W = x.shape
+    Co, _, kh, kw = weight.shape
+    gx, goff, gm = torch.empty_like(x), torch.empty_like(offset), torch.empty_like(mask)
+    gw = torch.zeros_like(weight)
+    gb = x.new_zeros((Co,)) if with_bias else None
+    call("aanet_mdcn_bwd_f32", ptr(x), ptr(offset), ptr(mask), ptr(weight), ptr(grad_out), ptr(gx),
+         ptr(goff), ptr(gm), ptr(gw), ptr(gb), N, C, H, W, Co, kh, kw, stride, padding, dilation,
+         groups, deformable_groups, stream_of(x))
+    return gx, goff, gm, gw, gb
+
+
+def mdcn_im2col(x, offset, mask, kh, kw, stride, padding, dilation, deformable_groups):
+    """Debug export (one image): col [C*K, Ho*Wo], kernel.cu:570-633."""
+    require_gpu(x, offset, mask, names=("input", "offset", "mask"))
+    C, H, W = x.shape
+    Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
+    col = torch.empty((C * kh * kw, Ho * Wo), device=x.device, dtype=x.dtype)
+    call("aanet_mdcn_im2col_f32", ptr(x), ptr(offset), ptr(mask), ptr(col), C, H, W, kh, kw,
+         stride, padding, dilation, deformable_groups, stream_of(x))
+    return col
+
+
+def mdcn_sample_index(offset, H, W, kh, kw, stride, padding, dilation, deformable_groups):
+    """Debug export: (h_low, w_low, valid) int32 [N, dg, K, Ho*Wo]."""
+    require_gpu(offset, names=("offset",))
+    N = offset.shape[0]
+    Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
+    shp = (N, deformable_groups, kh * kw, Ho * Wo)
+    hl, wl, vd = (torch.empty(shp, device=offset.device, dtype=torch.int32) for _ in range(3))
+    call("aanet_mdcn_sample_index", ptr(offset), ptr(hl), ptr(wl), ptr(vd), N, H, W, kh, kw, stride,
+         padding, dilation, deformable_groups, stream_of(offset))
+    return hl, wl, vd
+
+
+class ModulatedDeformConvFunction(Function):
+    """Same argument order / returns as nets/deform_conv/deform_conv.py:113-171."""
+
+    @staticmethod
+    def forward(ctx, input, offset, mask, weight, bias=None, stride=1, padding=0, dilation=1,
+                groups=1, deformable_groups=1):
+        if input is not None and input.dim() != 4:
+            raise ValueError(f"Expected 4D tensor as input, got {input.dim()}D tensor instead.")
+        if not input.is_cuda:
+            raise NotImplementedError  # as the reference (deform_conv.py:135-136)
+        ctx.stride, ctx.padding, ctx.dilation = stride, padding, dilation
+        ctx.groups, ctx.deformable_groups = groups, deformable_groups
+        ctx.with_bias = bias is not None
+        input, offset, mask = input.contiguous(), offset.contiguous(), mask.contiguous()
+        weight = weight.contiguous()
+        if weight.requires_grad or mask.requires_grad or offset.requires_grad or input.requires_grad:
+            ctx.save_for_backward(input, offset, mask, weight)
+        return mdcn_forward(input, offset, mask, weight, bias, stride, padding, dilation, groups,
+                            deformable_groups)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_output):
+        if not grad_output.is_cuda:
+            raise NotImplementedError
+        input, offset, mask, weight = ctx.saved_tensors
+        gx, goff, gm, gw, gb = mdcn_backward(input, offset, mask, weight, grad_output.contiguous(),
+                                             ctx.with_bias, ctx.stride, ctx.padding, ctx.dilation,
+                                             ctx.groups, ctx.deformable_groups)
+        return gx, goff, gm, gw, gb, None, None, None, None, None
+
+
+modulated_deform_conv = ModulatedDeformConvFunction.apply

@@ -1,0 +1,291 @@
+#!/usr/bin/env python3
+"""bench.py -- AANet cost-volume hot path on MI355X: stereo-pairs/s @384x1248, D=64, fp32.
+
+One step = the north-star path over one batch of B=8 synthetic stereo pairs per GPU, inputs
+resident in HBM: CostVolumePyramid (correlation, D=64/32/16) -> AdaptiveAggregation
+(6 fusions, 3 deformable, eval, no intermediate supervision) -> DisparityEstimation.
+Features are the 1/3, 1/6, 1/12 pyramids of a 384x1248 pair: [8,128,128,416], [8,128,64,208],
+[8,128,32,104] (BASELINE.json configs[1]).  Random-init weights of that architecture
+(offset_conv nonzero), synthetic N(0,1) features: there is no network for data/checkpoints.
+
+Launch: `python bench.py [--gpus 1 --steps K --warmup W]`; for N>1 under torch.distributed.run
+(one process per GPU, RCCL).  Pairs are sharded across ranks with no data-path collective
+(weak scaling); one all_gather of a per-rank metrics record at the end.  Rank 0 prints ONE
+JSON line.  `roofline` is measured live (HIP events on the launch stream) for the dominant
+HIP kernel; `cpu_baseline` times the CPU oracle (port of the reference path) on one pair.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "stereo-pairs/s @384x1248 D=64 fp32, 1/2/4/8 MI355X; EPE vs ref"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 = f32 vector rate
+H_IMG, W_IMG, MAXD_IMG = 384, 1248, 192
+MAXD = MAXD_IMG // 3       # cost-volume disparities at 1/3 resolution (nets/aanet.py:56-59)
+FEAT_C = 128
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8, help="stereo pairs per GPU")
+    ap.add_argument("--no-graph", action="store_true", help="time eager launches, not a HIP graph")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-iters", type=int, default=20)
+    ap.add_argument("--only", default=None,
+                    help="profiling mode: run only one kernel family (corr|mdcn|regress|step)")
+    return ap.parse_args()
+
+
+def build_model(device):
+    from aanet_amd.nets import AANetHotPath
+    torch.manual_seed(0)  # identical weights on every rank
+    m = AANetHotPath(MAXD, feature_similarity="correlation", num_scales=3, num_fusions=6,
+                     deformable_groups=2, mdconv_dilation=2, no_intermediate_supervision=True,
+                     num_stage_blocks=1, num_deform_blocks=3)
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for name, mod in m.named_modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.running_mean.copy_(0.05 * torch.randn(mod.num_features, generator=g))
+                mod.running_var.copy_(0.8 + 0.4 * torch.rand(mod.num_features, generator=g))
+            if name.endswith("offset_conv"):
+                mod.weight.normal_(0.0, 0.01, generator=g)   # nonzero, std 0.01
+                mod.bias.normal_(0.0, 0.5, generator=g)
+    return m.to(device).eval()
+
+
+def make_features(batch, rank, device):
+    gen = torch.Generator(device=device).manual_seed(1234 + rank)
+    shapes = [(batch, FEAT_C, (H_IMG // 3) >> s, (W_IMG // 3) >> s) for s in range(3)]
+    left = [torch.randn(s, device=device, generator=gen) for s in shapes]
+    right = [torch.randn(s, device=device, generator=gen) for s in shapes]
+    return left, right
+
+
+def time_events(fn, iters, stream):
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    start.record(stream)
+    for _ in range(iters):
+        fn()
+    end.record(stream)
+    torch.cuda.synchronize()
+    return start.elapsed_time(end) / iters  # ms
+
+
+def kernel_rooflines(model, left, right, batch, iters):
+    """Per-kernel average duration (HIP events on the launch stream) and roofline fractions."""
+    from aanet_amd import ops
+    from aanet_amd.nets._fuse import bn_affine, conv_bn_act
+    stream = torch.cuda.current_stream()
+    res = {}
+    # correlation, scale 0 (one launch): algorithmic bytes = read L,R once + write volume
+    B, C, H, W = left[0].shape
+    corr_bytes = 4 * (2 * B * C * H * W + B * MAXD * H * W)
+    ms = time_events(lambda: ops.corr_volume(left[0], right[0], MAXD), iters, stream)
+    res["corr_volume_s0"] = dict(bound="hbm", ms=ms, algo=corr_bytes, unit="GB/s",
+                                 achieved=corr_bytes / ms / 1e6, peak=HBM_PEAK_GBS)
+    # regression, scale 0
+    vol = ops.corr_volume(left[0], right[0], MAXD)
+    reg_bytes = 4 * (B * MAXD * H * W + B * H * W)
+    ms = time_events(lambda: ops.disp_regress(vol), iters, stream)
+    res["disp_regress_s0"] = dict(bound="hbm", ms=ms, algo=reg_bytes, unit="GB/s",
+                                  achieved=reg_bytes / ms / 1e6, peak=HBM_PEAK_GBS)
+    # modulated DCN (fused eval form: + BN + ReLU), scale 0 of the last fusion
+    blk = model.aggregation.fusions[5].branches[0][0]
+    with torch.no_grad():
+        x1 = conv_bn_act(vol, blk.conv1, blk.bn1, "relu")
+        om = blk.conv2.offset_conv(x1)
+        ps, psh = bn_affine(blk.bn2)
+        w = blk.conv2.deform_conv.weight
+        fn = lambda: ops.mdcn_forward_fused(x1, om, w, None, ps, psh, 1, 1, 2, 2, 2, 2.0)  # noqa: E731
+        ms = time_events(fn, iters, stream)
+    Co, Ci = w.shape[:2]
+    flops = 2.0 * B * H * W * Co * Ci * 9
+    res["mdcn_fwd_s0"] = dict(bound="mfma", ms=ms, algo=flops, unit="TFLOP/s",
+                              achieved=flops / ms / 1e9, peak=FP32_MFMA_PEAK_TF)
+    for v in res.values():
+        v["frac"] = v["achieved"] / v["peak"]
+    return res
+
+
+def cpu_baseline(model, left, right, gpu_disp):
+    """Time the CPU oracle (restated reference path) on ONE pair; also EPE vs the GPU output."""
+    from oracle import aggregation as oagg
+    threads = torch.get_num_threads()
+    sd = {k: v.detach().cpu().numpy() for k, v in model.aggregation.state_dict().items()}
+    lp = [t[:1].cpu().numpy() for t in left]
+    rp = [t[:1].cpu().numpy() for t in right]
+    t0 = time.perf_counter()
+    ref = oagg.hot_path(lp, rp, sd, MAXD, intermediate_supervision=False)[0]
+    dt = time.perf_counter() - t0
+    ours = gpu_disp[:1].cpu().numpy()
+    diff = np.abs(ours.astype(np.float64) - ref.astype(np.float64))
+    return dict(value=1.0 / dt, unit="stereo-pairs/s", cores=threads, kind="port",
+                sample="1 pair of the C2 workload (features 128x128x416 pyramid, D=64): "
+                       "oracle/ C restatement (cost volume, DCN, regression) + torch-CPU convs",
+                seconds=dt), float(diff.mean()), float(diff.max())
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    model = build_model(device)
+    left, right = make_features(args.batch, rank, device)
+
+    def step():
+        with torch.no_grad():
+            return model(left, right)[0]
+
+    if args.only:
+        profile_only(args, model, left, right, step)
+        return
+
+    for _ in range(args.warmup):
+        out = step()
+    torch.cuda.synchronize()
+
+    graph = None
+    if not args.no_graph:
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    out = step()
+            torch.cuda.current_stream().wait_stream(s)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                out = step()
+            torch.cuda.synchronize()
+        except Exception as e:  # capture unsupported by some library op: time eager launches
+            print(f"hip graph capture failed ({e}); timing eager launches", file=sys.stderr)
+            graph = None
+            torch.cuda.synchronize()
+
+    run = graph.replay if graph is not None else step
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    disp = out  # graph output buffer (or last eager output)
+
+    record = torch.tensor([args.batch * args.steps, elapsed, float(disp.min()), float(disp.max())],
+                          dtype=torch.float64, device=device)
+    if world > 1:
+        gathered = [torch.empty_like(record) for _ in range(world)]
+        dist.all_gather(gathered, record)
+        recs = torch.stack(gathered).cpu()
+    else:
+        recs = record.cpu().view(1, -1)
+    total_pairs = float(recs[:, 0].sum())
+    t_max = float(recs[:, 1].max())
+
+    if rank == 0:
+        roof = kernel_rooflines(model, left, right, args.batch, args.kernel_iters)
+        dom_name = max(roof, key=lambda k: roof[k]["ms"])
+        dom = roof[dom_name]
+        traffic = load_traffic(dom_name)
+        line = {
+            "metric": METRIC,
+            "value": total_pairs / t_max,
+            "unit": "stereo-pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1000.0 * t_max / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (N(0,1) feature pyramids on device, seeded per rank; random-init weights)",
+            "config": {
+                "workload": "C2: KITTI 384x1248 stereo pairs, features 128ch at 1/3,1/6,1/12, "
+                            "correlation volume D=64/32/16 -> AdaptiveAggregation (6 fusions, 3 "
+                            "deformable, eval) -> soft-argmin",
+                "batch_per_gpu": args.batch,
+                "global_batch": args.batch * world,
+                "parallelism": f"dp{world} (pairs sharded, no data-path collective)",
+                "hip_graph": graph is not None,
+            },
+            "roofline": {"kernel": dom_name, "bound": dom["bound"], "achieved": dom["achieved"],
+                         "peak": dom["peak"], "unit": dom["unit"], "frac": dom["frac"],
+                         "traffic": traffic, "ms_per_launch": dom["ms"],
+                         "algorithmic_per_launch": dom["algo"]},
+            "kernels": {k: {kk: v[kk] for kk in ("bound", "ms", "achieved", "unit", "frac")}
+                        for k, v in roof.items()},
+        }
+        if not args.no_cpu_baseline:
+            cb, epe, mx = cpu_baseline(model, left, right, disp)
+            line["cpu_baseline"] = cb
+            line["epe_vs_ref"] = epe
+            line["max_abs_disp_err_vs_ref"] = mx
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def load_traffic(kernel):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/pmc_*.json)."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get(kernel)
+
+
+def profile_only(args, model, left, right, step):
+    """Profiling helper: run one kernel family args.steps times (for rocprofv3 passes)."""
+    from aanet_amd import ops
+    if args.only == "step":
+        fn = step
+    elif args.only == "corr":
+        fn = lambda: ops.corr_volume(left[0], right[0], MAXD)  # noqa: E731
+    elif args.only == "regress":
+        vol = ops.corr_volume(left[0], right[0], MAXD)
+        fn = lambda: ops.disp_regress(vol)  # noqa: E731
+    elif args.only == "mdcn":
+        roof_iters = args.steps
+        kernel_rooflines(model, left, right, args.batch, roof_iters)
+        torch.cuda.synchronize()
+        return
+    else:
+        raise SystemExit(f"unknown --only {args.only}")
+    for _ in range(args.warmup + args.steps):
+        fn()
+    torch.cuda.synchronize()
+    print(json.dumps({"only": args.only, "steps": args.steps}))
+
+
+if __name__ == "__main__":
+    main()

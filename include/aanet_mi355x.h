@@ -1,0 +1,125 @@
+/*
+ * aanet_mi355x.h -- C ABI of the MI355X (gfx950) AANet cost-volume hot path.
+ *
+ * Every entry point:
+ *   - takes plain device pointers (fp32, NCHW / NCDHW contiguous unless a stride is given),
+ *     sizes as int, and an explicit HIP stream (hipStream_t, passed as aanet_stream_t);
+ *   - allocates nothing and never synchronises (graph-capturable); the caller owns buffers;
+ *   - returns 0 on success, a negative AANET_E* code for an invalid argument, or a positive
+ *     hipError_t for a launch failure.  Nothing is swallowed or only printed.
+ *
+ * Each function names the reference interface (wuzhongwulidong/aanet, file:line) it replaces.
+ */
+#ifndef AANET_MI355X_H
+#define AANET_MI355X_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t *aanet_stream_t; /* identical to hipStream_t */
+
+enum {
+  AANET_OK = 0,
+  AANET_EINVAL = -1,      /* bad size / null pointer / inconsistent shape */
+  AANET_EUNSUPPORTED = -2 /* valid for the reference but outside what this build implements */
+};
+
+int aanet_version(void);
+const char *aanet_status_string(int status);
+
+/* ------------------------------------------------------------------ cost volumes ------- */
+
+/* nets/cost.py:40-48 (CostVolume, feature_similarity='correlation').
+ * left, right [n, c, h, w] -> out [n, max_disp, h, w];
+ * out[b,d,y,x] = (1/c) * sum_c left[b,c,y,x] * right[b,c,y,x-d] for x >= d, else 0. */
+int aanet_corr_volume_f32(const float *left, const float *right, float *out, int n, int c, int h,
+                          int w, int max_disp, aanet_stream_t stream);
+
+/* Autograd of nets/cost.py:40-48: grad_left / grad_right [n,c,h,w] are OVERWRITTEN. */
+int aanet_corr_volume_bwd_f32(const float *left, const float *right, const float *grad_out,
+                              float *grad_left, float *grad_right, int n, int c, int h, int w,
+                              int max_disp, aanet_stream_t stream);
+
+/* nets/cost.py:31-38 (concat): out [n, 2c, max_disp, h, w]. */
+int aanet_concat_volume_f32(const float *left, const float *right, float *out, int n, int c, int h,
+                            int w, int max_disp, aanet_stream_t stream);
+
+/* nets/cost.py:22-29 (difference): out [n, c, max_disp, h, w]. */
+int aanet_diff_volume_f32(const float *left, const float *right, float *out, int n, int c, int h,
+                          int w, int max_disp, aanet_stream_t stream);
+
+/* Autograd of concat / difference: grad_left / grad_right [n,c,h,w] OVERWRITTEN. */
+int aanet_concat_volume_bwd_f32(const float *grad_out, float *grad_left, float *grad_right, int n,
+                                int c, int h, int w, int max_disp, aanet_stream_t stream);
+int aanet_diff_volume_bwd_f32(const float *grad_out, float *grad_left, float *grad_right, int n,
+                              int c, int h, int w, int max_disp, aanet_stream_t stream);
+
+/* nets/cost.py:58-76 (CostVolumePyramid, correlation): scale s uses max_disp >> s.
+ * Arrays of num_scales device pointers / sizes (host arrays); all scales are enqueued by one
+ * call. */
+int aanet_corr_pyramid_f32(int num_scales, const float *const *left, const float *const *right,
+                           float *const *out, const int *c, const int *h, const int *w, int n,
+                           int max_disp, aanet_stream_t stream);
+
+/* ------------------------------------------------------------ disparity regression ----- */
+
+/* nets/estimation.py:13-30 (DisparityEstimation): cost [n, d, h, w] -> disp [n, h, w];
+ * disp = sum_i i * softmax_i(negate ? -cost : cost).  d = cost.size(1). */
+int aanet_disp_regress_f32(const float *cost, float *disp, int n, int d, int h, int w, int negate,
+                           aanet_stream_t stream);
+
+/* Autograd of the above: grad_cost [n, d, h, w] OVERWRITTEN. */
+int aanet_disp_regress_bwd_f32(const float *cost, const float *grad_disp, float *grad_cost, int n,
+                               int d, int h, int w, int negate, aanet_stream_t stream);
+
+/* ------------------------------------------------------ modulated deformable conv ------ */
+
+/* deform_conv_cuda.cpp:490-569 (modulated_deform_conv_cuda_forward) + kernel.cu:570-633.
+ * x [n,c,h,w]; offset [n, dg*2*kh*kw, ho, wo]; mask [n, dg*kh*kw, ho, wo];
+ * weight [co, c/groups, kh, kw]; bias [co] or NULL; out [n, co, ho, wo] OVERWRITTEN.
+ * ho = (h + 2*pad - (dil*(kh-1)+1)) / stride + 1 (deform_conv.py:174-183). */
+int aanet_mdcn_fwd_f32(const float *x, const float *offset, const float *mask, const float *weight,
+                       const float *bias, float *out, int n, int c, int h, int w, int co, int kh,
+                       int kw, int stride, int pad, int dil, int groups, int dg,
+                       aanet_stream_t stream);
+
+/* Eval-mode fused form used by DeformSimpleBottleneck (nets/deform.py:78-97, 216-226):
+ *   - offset and mask may be channel slices of one tensor: per-image strides in elements;
+ *   - mask_logits != 0: the mask pointer holds pre-sigmoid logits, m = mask_scale*sigmoid(l)
+ *     (deform.py:86-89 with double_mask => mask_scale = 2);
+ *   - epilogue: y = act(post_scale[co] * (conv + bias[co]) + post_shift[co]); act 0 none,
+ *     1 ReLU, 2 LeakyReLU(0.2).  post_scale / post_shift may be NULL (identity). */
+int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset, long offset_batch_stride,
+                             const float *mask, long mask_batch_stride, int mask_logits,
+                             float mask_scale, const float *weight, const float *bias,
+                             const float *post_scale, const float *post_shift, int act, float *out,
+                             int n, int c, int h, int w, int co, int kh, int kw, int stride,
+                             int pad, int dil, int groups, int dg, aanet_stream_t stream);
+
+/* deform_conv_cuda.cpp:571-685 (modulated_deform_conv_cuda_backward) + kernel.cu:635-767.
+ * grad_x, grad_offset, grad_mask are OVERWRITTEN; grad_weight and grad_bias (may be NULL)
+ * ACCUMULATE, as in the reference (cpp:660-671). */
+int aanet_mdcn_bwd_f32(const float *x, const float *offset, const float *mask, const float *weight,
+                       const float *grad_out, float *grad_x, float *grad_offset, float *grad_mask,
+                       float *grad_weight, float *grad_bias, int n, int c, int h, int w, int co,
+                       int kh, int kw, int stride, int pad, int dil, int groups, int dg,
+                       aanet_stream_t stream);
+
+/* Debug exports for bit-exact checks (SURVEY.md §8c pin 6):
+ * im2col of ONE image, kernel.cu:570-633: col [c*kh*kw, ho*wo]. */
+int aanet_mdcn_im2col_f32(const float *x, const float *offset, const float *mask, float *col,
+                          int c, int h, int w, int kh, int kw, int stride, int pad, int dil,
+                          int dg, aanet_stream_t stream);
+/* sampling indices (floor of the fp32 coordinates) and the kernel.cu:618 validity flag,
+ * [n, dg, kh*kw, ho*wo] int32 each. */
+int aanet_mdcn_sample_index(const float *offset, int *h_low, int *w_low, int *valid, int n, int h,
+                            int w, int kh, int kw, int stride, int pad, int dil, int dg,
+                            aanet_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AANET_MI355X_H */

@@ -17,15 +17,43 @@ import torch.nn.functional as F
 from . import oracle
 
 BN_EPS = 1e-5
+TRAINING = False  # batch statistics in BN (module-level switch used by training-mode tests)
 
 
 def _t(a):
-    return torch.from_numpy(np.ascontiguousarray(a))
+    return a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))
 
 
 def _bn(x, sd, p):
+    if TRAINING:
+        return F.batch_norm(x, None, None, _t(sd[p + ".weight"]), _t(sd[p + ".bias"]), True, 0.0,
+                            BN_EPS)
     return F.batch_norm(x, _t(sd[p + ".running_mean"]), _t(sd[p + ".running_var"]),
                         _t(sd[p + ".weight"]), _t(sd[p + ".bias"]), False, 0.0, BN_EPS)
+
+
+class OracleMDCN(torch.autograd.Function):
+    """CPU autograd wrapper of the C oracle (forward cpp:490-569, backward cpp:571-685)."""
+
+    @staticmethod
+    def forward(ctx, x, offset, mask, weight, bias, dilation, dg):
+        ctx.save_for_backward(x, offset, mask, weight)
+        ctx.dilation, ctx.dg, ctx.with_bias = dilation, dg, bias is not None
+        out = oracle.mdcn_forward(x.detach().numpy(), offset.detach().numpy(),
+                                  mask.detach().numpy(), weight.detach().numpy(),
+                                  None if bias is None else bias.detach().numpy(), 1, dilation,
+                                  dilation, 1, dg)
+        return torch.from_numpy(out)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, offset, mask, weight = ctx.saved_tensors
+        gx, go, gm, gw, gb = oracle.mdcn_backward(x.numpy(), offset.numpy(), mask.numpy(),
+                                                  weight.numpy(), g.contiguous().numpy(),
+                                                  ctx.with_bias, 1, ctx.dilation, ctx.dilation,
+                                                  1, ctx.dg)
+        t = torch.from_numpy
+        return t(gx), t(go), t(gm), t(gw), (t(gb) if gb is not None else None), None, None
 
 
 def _conv(x, sd, p, stride=1, padding=0, dilation=1, groups=1):
@@ -40,10 +68,10 @@ def deform_conv2d(x, sd, p, dilation, dg):
     k2 = 9
     offset = om[:, :dg * 2 * k2]
     mask = torch.sigmoid(om[:, dg * 2 * k2:]) * 2
-    out = oracle.mdcn_forward(x.numpy(), offset.contiguous().numpy(), mask.contiguous().numpy(),
-                              sd[p + ".deform_conv.weight"], sd.get(p + ".deform_conv.bias"),
-                              1, dilation, dilation, 1, dg)
-    return _t(out)
+    b = sd.get(p + ".deform_conv.bias")
+    return OracleMDCN.apply(x.contiguous(), offset.contiguous(), mask.contiguous(),
+                            _t(sd[p + ".deform_conv.weight"]), None if b is None else _t(b),
+                            dilation, dg)
 
 
 def bottleneck(x, sd, p, deform, dilation=2, dg=2):
@@ -98,11 +126,11 @@ def adaptive_aggregation(volumes, sd, num_scales=3, num_fusions=6, num_deform_bl
         deform = f >= num_fusions - num_deform_blocks
         x = aa_module(x, sd, f"fusions.{f}", num_scales, num_out, deform, dilation, dg)
     n_final = num_scales if intermediate_supervision else 1
-    return [_conv(x[i], sd, f"final_conv.{i}").numpy() for i in range(n_final)]
+    return [_conv(x[i], sd, f"final_conv.{i}") for i in range(n_final)]
 
 
 def hot_path(left_pyr, right_pyr, sd, max_disp, **kw):
     """cost volume pyramid -> AdaptiveAggregation -> regression in reverse order (aanet.py:146-167)."""
     vols = oracle.cost_volume_pyramid(left_pyr, right_pyr, max_disp)
-    aggs = adaptive_aggregation(vols, sd, **kw)
+    aggs = [a.detach().numpy() for a in adaptive_aggregation(vols, sd, **kw)]
     return [oracle.disp_regress(aggs[len(aggs) - 1 - i]) for i in range(len(aggs))]

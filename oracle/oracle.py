@@ -106,6 +106,25 @@ def cost_volume_pyramid(left_pyr, right_pyr, max_disp, feature_similarity="corre
             for s, (l, r) in enumerate(zip(left_pyr, right_pyr))]
 
 
+def corr_volume_bwd(left, right, grad_out, dtype=np.float32):
+    """Autograd of nets/cost.py:40-48 -> (grad_left, grad_right)."""
+    L, R, g = _c(left, dtype), _c(right, dtype), _c(grad_out, dtype)
+    B, C, H, W = L.shape
+    gl, gr = np.empty_like(L), np.empty_like(R)
+    _fn("orc_corr_volume_bwd", dtype)(_ptr(L), _ptr(R), _ptr(g), _ptr(gl), _ptr(gr), B, C, H, W,
+                                      g.shape[1])
+    return gl, gr
+
+
+def shift_volume_bwd(grad_out, C, concat, dtype=np.float32):
+    """Autograd of nets/cost.py:22-38 -> (grad_left, grad_right)."""
+    g = _c(grad_out, dtype)
+    B, _, D, H, W = g.shape
+    gl, gr = np.empty((B, C, H, W), dtype), np.empty((B, C, H, W), dtype)
+    _fn("orc_shift_volume_bwd", dtype)(_ptr(g), _ptr(gl), _ptr(gr), B, C, H, W, D, int(concat))
+    return gl, gr
+
+
 # ------------------------------------------------------------ disparity regression -------
 def disp_regress(cost, match_similarity=True, dtype=np.float32):
     """nets/estimation.py:13-30 -> [B, H, W]."""

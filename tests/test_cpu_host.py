@@ -1,0 +1,92 @@
+"""CPU-side checks of the host layer: C-ABI library exports, drop-in module API / state-dict keys,
+and loud failure (no silent CPU fallback)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import aanet_amd
+from aanet_amd import _lib, nets, ops
+from tests.golden_io import golden, state_dict_of
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    txt = open(os.path.join(REPO, "include", "aanet_mi355x.h")).read()
+    return sorted(set(re.findall(r"\b(aanet_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    fns = header_functions()
+    assert len(fns) >= 15
+    for f in fns:
+        assert hasattr(L, f), f"{f} declared in include/aanet_mi355x.h but not exported"
+    assert set(fns) == set(_lib.exported_symbols())
+
+
+def test_library_version_and_status_strings():
+    L = _lib.lib()
+    assert L.aanet_version() == 1
+    assert L.aanet_status_string(0) == b"ok"
+    assert L.aanet_status_string(-1) == b"invalid argument"
+    assert L.aanet_status_string(-2) == b"unsupported configuration"
+
+
+def test_invalid_arguments_are_rejected_without_a_gpu():
+    """Argument validation runs on the host before any launch: bad sizes return AANET_EINVAL."""
+    L = _lib.lib()
+    assert L.aanet_corr_volume_f32(None, None, None, 1, 1, 1, 1, 1, None) == -1
+    assert L.aanet_disp_regress_f32(None, None, 0, 1, 1, 1, 0, None) == -1
+    # C not divisible by groups
+    args = [None] * 6 + [1, 3, 4, 4, 4, 3, 3, 1, 1, 1, 2, 1, None]
+    assert L.aanet_mdcn_fwd_f32(*args) == -1
+    with pytest.raises(_lib.AanetError):
+        _lib.call("aanet_corr_volume_f32", None, None, None, 0, 1, 1, 1, 1, None)
+
+
+def test_ops_fail_loudly_on_cpu_tensors():
+    x = torch.zeros(1, 4, 3, 5)
+    with pytest.raises(NotImplementedError):
+        ops.corr_volume(x, x, 2)
+    with pytest.raises(NotImplementedError):
+        nets.DisparityEstimation(4)(torch.zeros(1, 4, 3, 5))
+    with pytest.raises(NotImplementedError):
+        nets.ModulatedDeformConv(4, 4, 3, padding=1)(x, torch.zeros(1, 18, 3, 5), torch.ones(1, 9, 3, 5))
+
+
+@pytest.mark.parametrize("inter", [True, False])
+def test_state_dict_keys_match_reference(inter):
+    g = golden("aggregation_inter" if inter else "aggregation_final")
+    ref = state_dict_of(g)
+    m = nets.AdaptiveAggregation(16, num_scales=3, num_fusions=6, num_stage_blocks=1,
+                                 num_deform_blocks=3, intermediate_supervision=inter)
+    ours = m.state_dict()
+    assert set(ours) == set(ref)
+    for k, v in ref.items():
+        assert tuple(ours[k].shape) == v.shape, k
+
+
+def test_hot_path_module_api_mirrors_aanet():
+    m = nets.AANetHotPath(64, no_intermediate_supervision=True)
+    # AANet eval config (max_disp=192 -> 64): final fusion has one output branch, one final conv
+    assert len(m.aggregation.final_conv) == 1
+    assert len(m.aggregation.fusions[-1].fuse_layers) == 1
+    assert isinstance(m.cost_volume, nets.CostVolumePyramid)
+    # the DCN-bearing keys the training LR grouping relies on (utils/utils.py:156-169)
+    keys = list(m.state_dict())
+    assert any(k.endswith("conv2.offset_conv.weight") for k in keys)
+    assert any(k.endswith("conv2.deform_conv.weight") for k in keys)
+    w = m.state_dict()["aggregation.fusions.5.branches.0.0.conv2.offset_conv.weight"]
+    assert tuple(w.shape) == (54, 32, 3, 3)
+    # offset_conv is zero-initialised like the reference (deform.py:74-76)
+    assert float(w.abs().sum()) == 0.0
+
+
+def test_package_exposes_native_library_path():
+    assert aanet_amd.native_library_path().endswith("libaanet_mi355x.so")
+    assert os.path.exists(aanet_amd.native_library_path())

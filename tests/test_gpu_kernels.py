@@ -1,0 +1,179 @@
+"""GPU parity: HIP kernels (through the C ABI) vs the CPU oracle and the reference's golden vectors.
+
+Tolerances (fp32 throughout):
+  * concat / difference volumes, DCN im2col values, DCN sampling indices: bit-exact.
+  * correlation volume: |err| <= 1e-5 * (1 + |ref|)   (channel sum order differs: fma chain)
+  * regression: |err| <= 1e-4 px                      (north star: 1e-3 max abs disparity)
+  * DCN forward: |err| <= 2e-5 * scale               (GEMM order differs from the oracle's)
+  * DCN backward: rtol 1e-4 with atol scaled to the gradient magnitude (float atomics).
+"""
+import numpy as np
+import pytest
+import torch
+
+from aanet_amd import ops
+from oracle import oracle
+from tests.golden_io import golden, golden_names
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    torch.manual_seed(0)
+
+
+def g2t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def t2n(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def close(a, b, rtol, atol, what=""):
+    err = np.abs(a.astype(np.float64) - b.astype(np.float64))
+    tol = atol + rtol * np.abs(b.astype(np.float64))
+    bad = err > tol
+    assert not bad.any(), f"{what}: {bad.sum()} / {bad.size} mismatches, max err {err.max():.3g}"
+
+
+# -------------------------------------------------------------- correlation volume -------
+@pytest.mark.parametrize("name", golden_names("corr_"))
+def test_corr_volume_vs_reference_golden(name):
+    g = golden(name)
+    out = t2n(ops.corr_volume(g2t(g["left"]), g2t(g["right"]), int(g["max_disp"])))
+    close(out, g["out"], 1e-5, 1e-5, name)
+    D = int(g["max_disp"])
+    for d in range(D):
+        assert np.all(out[:, d, :, :d] == 0), "x < d must be exactly zero (cost.py:41)"
+
+
+@pytest.mark.parametrize("B,C,H,W,D", [(2, 128, 5, 200, 64), (1, 128, 3, 416, 64), (1, 128, 4, 208, 32),
+                                       (2, 128, 3, 104, 16), (1, 32, 3, 130, 192), (1, 7, 2, 65, 24),
+                                       (1, 3, 2, 5, 1), (1, 64, 2, 70, 100)])
+def test_corr_volume_vs_oracle(B, C, H, W, D):
+    rng = np.random.default_rng(B * 1000 + C + D)
+    L = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    R = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    out = t2n(ops.corr_volume(g2t(L), g2t(R), D))
+    close(out, oracle.corr_volume(L, R, D), 1e-5, 1e-5, "corr")
+
+
+def test_corr_pyramid_vs_reference_golden():
+    from aanet_amd.nets import CostVolumePyramid
+    g = golden("pyramid")
+    outs = CostVolumePyramid(int(g["max_disp"]))([g2t(g[f"left{s}"]) for s in range(3)],
+                                                 [g2t(g[f"right{s}"]) for s in range(3)])
+    for s in range(3):
+        close(t2n(outs[s]), g[f"out{s}"], 1e-5, 1e-5, f"scale{s}")
+
+
+def test_corr_volume_full_size_properties():
+    """BASELINE config C2 scale 0 ([8,128,128,416], D=64): sampled entries against a float64
+    dot product, exact zero fill for x < d, and rows of identical features."""
+    B, C, H, W, D = 8, 128, 128, 416, 64
+    gen = torch.Generator(device=DEV).manual_seed(1234)
+    L = torch.randn(B, C, H, W, device=DEV, generator=gen)
+    R = torch.randn(B, C, H, W, device=DEV, generator=gen)
+    out = ops.corr_volume(L, R, D)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(0)
+    idx = [(rng.integers(B), rng.integers(D), rng.integers(H), rng.integers(W)) for _ in range(400)]
+    Lc, Rc, oc = L.cpu().double(), R.cpu().double(), out.cpu()
+    for b, d, y, x in idx:
+        ref = 0.0 if x < d else float((Lc[b, :, y, x] * Rc[b, :, y, x - d]).mean())
+        assert abs(float(oc[b, d, y, x]) - ref) <= 1e-5 * (1 + abs(ref))
+    for d in range(D):
+        assert torch.all(oc[:, d, :, :d] == 0)
+    # identical left/right and d=0 => mean of squares >= 0 everywhere
+    same = ops.corr_volume(L, L, D)
+    assert torch.all(same[:, 0] >= 0)
+
+
+@pytest.mark.parametrize("B,C,H,W,D", [(2, 8, 3, 40, 16), (1, 128, 2, 100, 64), (1, 5, 2, 17, 9)])
+def test_corr_volume_backward_vs_oracle(B, C, H, W, D):
+    rng = np.random.default_rng(7)
+    L = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    R = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    G = rng.standard_normal((B, D, H, W)).astype(np.float32)
+    Lt, Rt = g2t(L).requires_grad_(), g2t(R).requires_grad_()
+    out = ops.CorrelationVolumeFunction.apply(Lt, Rt, D)
+    out.backward(g2t(G))
+    gl, gr = oracle.corr_volume_bwd(L, R, G)
+    close(t2n(Lt.grad), gl, 1e-5, 1e-5, "grad_left")
+    close(t2n(Rt.grad), gr, 1e-5, 1e-5, "grad_right")
+
+
+# --------------------------------------------------------------- concat / difference -----
+@pytest.mark.parametrize("name", golden_names("concat_") + golden_names("diff_"))
+def test_shift_volume_bit_exact_vs_reference_golden(name):
+    g = golden(name)
+    out = t2n(ops.shift_volume(g2t(g["left"]), g2t(g["right"]), int(g["max_disp"]),
+                               name.startswith("concat")))
+    assert np.array_equal(out, g["out"])
+
+
+@pytest.mark.parametrize("concat", [True, False])
+def test_shift_volume_c5_shape_and_backward(concat):
+    """Config C5-like (PSMNet feature [B,32,H/4,W/4], D=48) at reduced H; bit-exact + grads."""
+    rng = np.random.default_rng(5)
+    B, C, H, W, D = 1, 32, 8, 312, 48
+    L = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    R = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    Lt, Rt = g2t(L).requires_grad_(), g2t(R).requires_grad_()
+    out = ops.ShiftVolumeFunction.apply(Lt, Rt, D, concat)
+    ref = (oracle.concat_volume if concat else oracle.diff_volume)(L, R, D)
+    assert np.array_equal(t2n(out), ref)
+    G = rng.standard_normal(ref.shape).astype(np.float32)
+    out.backward(g2t(G))
+    gl, gr = oracle.shift_volume_bwd(G, C, concat)
+    close(t2n(Lt.grad), gl, 1e-5, 1e-5, "grad_left")
+    close(t2n(Rt.grad), gr, 1e-5, 1e-5, "grad_right")
+
+
+# --------------------------------------------------------------------- regression --------
+@pytest.mark.parametrize("name", golden_names("regress_"))
+def test_regression_vs_reference_golden(name):
+    from aanet_amd.nets import DisparityEstimation
+    g = golden(name)
+    est = DisparityEstimation(int(g["max_disp"]), bool(g["match_similarity"]))
+    out = t2n(est(g2t(g["cost"])))
+    close(out, g["out"], 0, 1e-4, name)
+
+
+@pytest.mark.parametrize("negate", [False, True])
+def test_regression_vs_oracle_and_backward(negate):
+    rng = np.random.default_rng(11)
+    cost = (rng.standard_normal((2, 64, 16, 130)) * 4).astype(np.float32)
+    ct = g2t(cost).requires_grad_()
+    disp = ops.DisparityRegressionFunction.apply(ct, negate)
+    close(t2n(disp), oracle.disp_regress(cost, not negate), 0, 1e-4, "disp")
+    G = rng.standard_normal((2, 16, 130)).astype(np.float32)
+    disp.backward(g2t(G))
+    close(t2n(ct.grad), oracle.disp_regress_bwd(cost, G, not negate), 1e-4, 1e-5, "grad")
+
+
+def test_regression_full_size_properties():
+    """C2 scale 0 [8,64,128,416]: disparity within [0, D-1]; a dominant candidate wins."""
+    B, D, H, W = 8, 64, 128, 416
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    cost = torch.randn(B, D, H, W, device=DEV, generator=gen)
+    disp = ops.disp_regress(cost)
+    assert float(disp.min()) >= 0 and float(disp.max()) <= D - 1
+    target = torch.randint(0, D, (B, H, W), device=DEV, generator=gen)
+    spike = cost.scatter(1, target.unsqueeze(1), 200.0)
+    d2 = ops.disp_regress(spike)
+    assert torch.equal(d2, target.float())
+    # sampled pixels against float64
+    rng = np.random.default_rng(1)
+    cc, dd = cost.cpu().double(), disp.cpu().double()
+    for _ in range(200):
+        b, y, x = rng.integers(B), rng.integers(H), rng.integers(W)
+        p = torch.softmax(cc[b, :, y, x], 0)
+        ref = float((p * torch.arange(D, dtype=torch.float64)).sum())
+        assert abs(float(dd[b, y, x]) - ref) <= 1e-4

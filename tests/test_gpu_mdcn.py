@@ -1,0 +1,138 @@
+"""GPU parity of the modulated deformable conv (HIP, through the C ABI) vs the CPU oracle.
+
+* sampling indices (h_low, w_low, validity) and im2col values: BIT-EXACT (SURVEY §8c pin 6);
+* forward: |err| <= 2e-5 * (1 + |ref|) (GEMM summation order differs);
+* backward: grad_offset / grad_mask / grad_weight / grad_bias rtol 1e-4 + atol scaled to the
+  tensor's magnitude; grad_x uses float atomics like the reference (order-dependent rounding).
+"""
+import numpy as np
+import pytest
+import torch
+
+from aanet_amd import ops
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def g2t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def t2n(t):
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def make_case(seed, N, C, H, W, Co, k=3, stride=1, pad=2, dil=2, dg=2, groups=1, off_scale=2.0,
+              integer_heavy=False):
+    rng = np.random.default_rng(seed)
+    Ho = oracle.out_size(H, k, stride, pad, dil)
+    Wo = oracle.out_size(W, k, stride, pad, dil)
+    x = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    off = (rng.standard_normal((N, dg * 2 * k * k, Ho, Wo)) * off_scale).astype(np.float32)
+    if integer_heavy:  # exact integers / halves stress floor() and the strict range checks
+        off = np.round(off * 2) / 2
+        off[..., ::3] = -1.0 - rng.integers(0, 3, off[..., ::3].shape)
+    msk = rng.uniform(0, 2, (N, dg * k * k, Ho, Wo)).astype(np.float32)
+    w = (rng.standard_normal((Co, C // groups, k, k)) / np.sqrt(C * k * k)).astype(np.float32)
+    b = rng.standard_normal(Co).astype(np.float32)
+    return x, off, msk, w, b
+
+
+CASES = [
+    # N, C, H, W, Co, k, stride, pad, dil, dg, groups
+    (2, 64, 16, 52, 64, 3, 1, 2, 2, 2, 1),     # aggregation scale-0 shape family
+    (2, 32, 9, 26, 32, 3, 1, 2, 2, 2, 1),      # scale 1
+    (2, 16, 5, 13, 16, 3, 1, 2, 2, 2, 1),      # scale 2 (cpg = 8)
+    (1, 128, 8, 26, 128, 3, 1, 1, 1, 2, 1),    # feature-extractor DCN (C=128, dil 1)
+    (1, 128, 16, 52, 128, 3, 2, 1, 1, 2, 1),   # stride 2
+    (1, 24, 7, 11, 40, 3, 1, 1, 1, 3, 2),      # groups=2, dg=3, Co not a tile multiple
+    (2, 6, 5, 7, 5, 1, 1, 0, 1, 1, 1),         # 1x1 kernel, tiny
+    (1, 8, 6, 9, 12, 3, 2, 2, 2, 4, 1),        # dg=4, cpg=2
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("integer_heavy", [False, True])
+def test_mdcn_sample_index_and_im2col_bit_exact(case, integer_heavy):
+    N, C, H, W, Co, k, s, p, d, dg, groups = case
+    x, off, msk, w, b = make_case(1, N, C, H, W, Co, k, s, p, d, dg, groups,
+                                  integer_heavy=integer_heavy)
+    hl, wl, vd = ops.mdcn_sample_index(g2t(off), H, W, k, k, s, p, d, dg)
+    ohl, owl, ovd = oracle.mdcn_sample_index(off, H, W, k, k, s, p, d, dg)
+    assert np.array_equal(t2n(hl), ohl) and np.array_equal(t2n(wl), owl)
+    assert np.array_equal(t2n(vd), ovd)
+    for n in range(N):
+        col = ops.mdcn_im2col(g2t(x[n]), g2t(off[n]), g2t(msk[n]), k, k, s, p, d, dg)
+        assert np.array_equal(t2n(col), oracle.mdcn_im2col(x[n], off[n], msk[n], k, k, s, p, d, dg))
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("with_bias", [False, True])
+def test_mdcn_forward_vs_oracle(case, with_bias):
+    N, C, H, W, Co, k, s, p, d, dg, groups = case
+    x, off, msk, w, b = make_case(2, N, C, H, W, Co, k, s, p, d, dg, groups)
+    bias = b if with_bias else None
+    out = ops.mdcn_forward(g2t(x), g2t(off), g2t(msk), g2t(w), g2t(bias) if with_bias else None,
+                           s, p, d, groups, dg)
+    ref = oracle.mdcn_forward(x, off, msk, w, bias, s, p, d, groups, dg)
+    got = t2n(out)
+    err = np.abs(got - ref)
+    assert err.max() <= 2e-5 * (1 + np.abs(ref).max()), err.max()
+
+
+def test_mdcn_forward_zero_offset_equals_conv2d():
+    """KAT 1 on the GPU: offsets 0, mask 1 => torch conv2d (MIOpen)."""
+    x, off, msk, w, b = make_case(3, 2, 64, 20, 40, 64)
+    off[:] = 0
+    msk[:] = 1
+    out = ops.mdcn_forward(g2t(x), g2t(off), g2t(msk), g2t(w), None, 1, 2, 2, 1, 2)
+    ref = torch.nn.functional.conv2d(g2t(x), g2t(w), None, 1, 2, 2)
+    assert torch.allclose(out, ref, rtol=1e-4, atol=1e-4)
+
+
+def test_mdcn_fused_eval_path_vs_oracle():
+    """Fused path: offset/mask read in place from the offset_conv output, 2*sigmoid, BN, ReLU."""
+    rng = np.random.default_rng(4)
+    N, C, H, W, dg = 2, 64, 12, 40, 2
+    x = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    om = rng.standard_normal((N, dg * 27, H, W)).astype(np.float32)
+    w = (rng.standard_normal((C, C, 3, 3)) / 24).astype(np.float32)
+    sc = rng.uniform(0.5, 1.5, C).astype(np.float32)
+    sh = rng.standard_normal(C).astype(np.float32)
+    out = ops.mdcn_forward_fused(g2t(x), g2t(om), g2t(w), None, g2t(sc), g2t(sh), 1, 1, 2, 2, dg, 2.0)
+    mask = 2.0 / (1.0 + np.exp(-om[:, dg * 18:].astype(np.float64)))
+    ref = oracle.mdcn_forward(x, om[:, :dg * 18], mask.astype(np.float32), w, None, 1, 2, 2, 1, dg)
+    ref = np.maximum(ref * sc[None, :, None, None] + sh[None, :, None, None], 0)
+    got = t2n(out)
+    assert np.abs(got - ref).max() <= 1e-4 * (1 + np.abs(ref).max())
+
+
+BWD_CASES = [
+    (2, 64, 12, 30, 64, 3, 1, 2, 2, 2),
+    (2, 32, 9, 26, 32, 3, 1, 2, 2, 2),
+    (1, 16, 5, 13, 16, 3, 1, 2, 2, 2),
+    (1, 48, 10, 21, 36, 3, 2, 1, 1, 3),
+]
+
+
+@pytest.mark.parametrize("case", BWD_CASES)
+def test_mdcn_backward_vs_oracle(case):
+    N, C, H, W, Co, k, s, p, d, dg = case
+    x, off, msk, w, b = make_case(5, N, C, H, W, Co, k, s, p, d, dg)
+    Ho, Wo = off.shape[2:]
+    go = np.random.default_rng(6).standard_normal((N, Co, Ho, Wo)).astype(np.float32)
+    xt, ot, mt = g2t(x).requires_grad_(), g2t(off).requires_grad_(), g2t(msk).requires_grad_()
+    wt, bt = g2t(w).requires_grad_(), g2t(b).requires_grad_()
+    out = ops.modulated_deform_conv(xt, ot, mt, wt, bt, s, p, d, 1, dg)
+    out.backward(g2t(go))
+    gx, goff, gm, gw, gb = oracle.mdcn_backward(x, off, msk, w, go, True, s, p, d, 1, dg)
+    for name, got, ref in (("grad_input", xt.grad, gx), ("grad_offset", ot.grad, goff),
+                           ("grad_mask", mt.grad, gm), ("grad_weight", wt.grad, gw),
+                           ("grad_bias", bt.grad, gb)):
+        got = t2n(got)
+        scale = np.abs(ref).max() + 1e-12
+        err = np.abs(got - ref)
+        assert err.max() <= 1e-4 * scale + 1e-6, f"{name}: max err {err.max():.3g} (scale {scale:.3g})"

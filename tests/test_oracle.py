@@ -77,7 +77,7 @@ def test_aggregation_oracle_matches_reference(tag):
                                      intermediate_supervision=inter)
     assert len(aggs) == (3 if inter else 1)
     for i, a in enumerate(aggs):
-        np.testing.assert_allclose(a, g[f"agg{i}"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(a.detach().numpy(), g[f"agg{i}"], rtol=1e-5, atol=1e-5)
     disps = oagg.hot_path([g[f"feat_left{s}"] for s in range(3)],
                           [g[f"feat_right{s}"] for s in range(3)], sd, 16,
                           intermediate_supervision=inter)
@@ -196,3 +196,34 @@ def test_dcn_backward_matches_finite_difference_f64():
             flat[idx] = old
             np.testing.assert_allclose(grad.reshape(-1)[idx], (fp - fm) / (2 * eps), rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(gb, go.sum(axis=(0, 2, 3)), rtol=1e-12)
+
+
+def test_cost_volume_backward_matches_torch_autograd_of_reference_formula():
+    """Pin the cost-volume backward restatement against torch autograd of cost.py:22-48's ops."""
+    rng = np.random.default_rng(4)
+    B, C, H, W, D = 2, 3, 4, 9, 5
+    Lf, Rf = rng.standard_normal((B, C, H, W)), rng.standard_normal((B, C, H, W))
+    L = torch.tensor(Lf, requires_grad=True)
+    R = torch.tensor(Rf, requires_grad=True)
+    corr = L.new_zeros(B, D, H, W)
+    for i in range(D):
+        corr[:, i, :, i:] = (L[:, :, :, i:] * R[:, :, :, :W - i]).mean(dim=1)
+    g = torch.tensor(rng.standard_normal((B, D, H, W)))
+    gl, gr = torch.autograd.grad(corr, (L, R), g)
+    ol, or_ = oracle.corr_volume_bwd(Lf, Rf, g.numpy(), dtype=np.float64)
+    np.testing.assert_allclose(ol, gl.numpy(), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(or_, gr.numpy(), rtol=1e-12, atol=1e-12)
+    for concat in (True, False):
+        L.grad = R.grad = None
+        OC = 2 * C if concat else C
+        vol = L.new_zeros(B, OC, D, H, W)
+        for i in range(D):
+            if concat:
+                vol[:, :, i, :, i:] = torch.cat((L[:, :, :, i:], R[:, :, :, :W - i]), dim=1)
+            else:
+                vol[:, :, i, :, i:] = L[:, :, :, i:] - R[:, :, :, :W - i]
+        g = torch.tensor(rng.standard_normal((B, OC, D, H, W)))
+        gl, gr = torch.autograd.grad(vol, (L, R), g)
+        ol, or_ = oracle.shift_volume_bwd(g.numpy(), C, concat, dtype=np.float64)
+        np.testing.assert_allclose(ol, gl.numpy(), rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(or_, gr.numpy(), rtol=1e-12, atol=1e-12)
