@@ -54,14 +54,14 @@ __global__ __launch_bounds__(RB) void disp_regress_bwd_kernel(const float *__res
   for (int d = 0; d < D; ++d) m = fmaxf(m, sign * c[(long)d * HW]);
   float z = 0.f, acc = 0.f;
   for (int d = 0; d < D; ++d) {
-    const float ev = __expf(sign * c[(long)d * HW] - m);
+    const float ev = expf(sign * c[(long)d * HW] - m);
     z += ev;
     acc += ev * (float)d;
   }
   const float inv = 1.f / z, mu = acc * inv, g = gdisp[e];
   float *gc = gcost + b * D * HW + p;
   for (int d = 0; d < D; ++d) {
-    const float pr = __expf(sign * c[(long)d * HW] - m) * inv;
+    const float pr = expf(sign * c[(long)d * HW] - m) * inv;
     gc[(long)d * HW] = sign * g * pr * ((float)d - mu);
   }
 }

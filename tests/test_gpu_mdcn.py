@@ -111,6 +111,9 @@ def test_mdcn_fused_eval_path_vs_oracle():
 
 
 BWD_CASES = [
+    (2, 16, 24, 48, 16, 3, 1, 2, 2, 2),   # golden-model layer shapes (max_disp=16)
+    (2, 8, 12, 24, 8, 3, 1, 2, 2, 2),
+    (2, 4, 6, 12, 4, 3, 1, 2, 2, 2),
     (2, 64, 12, 30, 64, 3, 1, 2, 2, 2),
     (2, 32, 9, 26, 32, 3, 1, 2, 2, 2),
     (1, 16, 5, 13, 16, 3, 1, 2, 2, 2),
@@ -119,9 +122,10 @@ BWD_CASES = [
 
 
 @pytest.mark.parametrize("case", BWD_CASES)
-def test_mdcn_backward_vs_oracle(case):
+@pytest.mark.parametrize("off_scale", [0.7, 2.0])
+def test_mdcn_backward_vs_oracle(case, off_scale):
     N, C, H, W, Co, k, s, p, d, dg = case
-    x, off, msk, w, b = make_case(5, N, C, H, W, Co, k, s, p, d, dg)
+    x, off, msk, w, b = make_case(5, N, C, H, W, Co, k, s, p, d, dg, off_scale=off_scale)
     Ho, Wo = off.shape[2:]
     go = np.random.default_rng(6).standard_normal((N, Co, Ho, Wo)).astype(np.float32)
     xt, ot, mt = g2t(x).requires_grad_(), g2t(off).requires_grad_(), g2t(msk).requires_grad_()

@@ -64,53 +64,82 @@ def test_hot_path_disparity_vs_reference_golden(tag):
         assert err <= 2e-4, f"disp{i}: max abs {err:.3g} px"
 
 
-def test_training_step_gradients_vs_oracle():
-    """Train-mode forward+backward of the whole path (BN batch stats, HIP DCN backward) against
-    the CPU oracle graph with torch autograd + the C oracle DCN backward."""
+def _grads_vs_oracle(sd_np, train_bn):
+    """Forward+backward of the whole path on the GPU (HIP DCN / cost / regression backward) and
+    of the oracle graph on the CPU (torch autograd for stock ops + the C oracle DCN backward).
+    Returns (our loss, oracle loss, [(name, ours, oracle)])."""
     g = golden("aggregation_inter")
-    sd_np = state_dict_of(g)
     m = nets.AANetHotPath(16, no_intermediate_supervision=False, num_deform_blocks=3)
     m.load_state_dict({"aggregation." + k: torch.from_numpy(v) for k, v in sd_np.items()})
-    m = m.to(DEV).train()
+    m = m.to(DEV)
+    m.train(train_bn)
     fl = [g2t(g[f"feat_left{s}"]).requires_grad_() for s in range(3)]
     fr = [g2t(g[f"feat_right{s}"]).requires_grad_() for s in range(3)]
     disps = m(fl, fr)
     loss = sum((d * (i + 1)).mean() for i, d in enumerate(disps))
     loss.backward()
 
-    # oracle: same math on CPU (torch autograd for stock ops, oracle C for DCN + cost + regression)
-    params = {k: torch.from_numpy(v.copy()).requires_grad_(v.dtype == np.float32 and "running" not in k
-                                                            and "num_batches" not in k)
+    params = {k: torch.from_numpy(v.copy()).requires_grad_("running" not in k and "num_batches" not in k)
               for k, v in sd_np.items()}
-    vols = [torch.tensor(g[f"volume{s}"]) for s in range(3)]
-    for v in vols:
-        v.requires_grad_()
-    oagg.TRAINING = True
+    with torch.no_grad():
+        vols = [torch.from_numpy(v) for v in
+                oagg.oracle.cost_volume_pyramid([g[f"feat_left{s}"] for s in range(3)],
+                                                [g[f"feat_right{s}"] for s in range(3)], 16)]
+    oagg.TRAINING = train_bn
     try:
         aggs = oagg.adaptive_aggregation(vols, params, intermediate_supervision=True)
     finally:
         oagg.TRAINING = False
-    # regression as torch ops (estimation.py:19-28) for autograd
     ref_loss = 0
-    for i in range(3):
+    for i in range(3):  # estimation.py:19-28 as torch ops, reverse scale order (aanet.py:161)
         a = aggs[2 - i]
         p = torch.softmax(a, 1)
         d = (p * torch.arange(a.shape[1], dtype=a.dtype).view(1, -1, 1, 1)).sum(1)
         ref_loss = ref_loss + (d * (i + 1)).mean()
     ref_loss.backward()
-    assert abs(float(loss) - float(ref_loss)) <= 1e-4 * max(1.0, abs(float(ref_loss)))
     named = dict(m.aggregation.named_parameters())
-    checked = 0
-    for k, p in params.items():
-        if p.grad is None:
-            continue
-        got = named[k].grad.cpu().numpy()
-        ref = p.grad.numpy()
+    pairs = [(k, named[k].grad.cpu().numpy(), p.grad.numpy()) for k, p in params.items()
+             if p.grad is not None]
+    return float(loss.detach()), float(ref_loss.detach()), pairs
+
+
+def test_training_gradients_vs_oracle_strict():
+    """Eval-mode BN (linear) and offsets that are exact fractional constants (offset_conv weight 0,
+    random bias): CPU and GPU forwards then take identical floor() branches, so every gradient
+    must agree to rounding.  Checks the autograd wiring of all HIP backward kernels."""
+    sd = dict(state_dict_of(golden("aggregation_inter")))
+    rng = np.random.default_rng(9)
+    for k in list(sd):
+        if k.endswith("offset_conv.weight"):
+            sd[k] = np.zeros_like(sd[k])
+        if k.endswith("offset_conv.bias"):
+            b = rng.uniform(0.1, 0.9, sd[k].shape) * rng.choice([-1, 1], sd[k].shape)
+            sd[k] = b.astype(np.float32)
+    loss, ref_loss, pairs = _grads_vs_oracle(sd, train_bn=False)
+    assert abs(loss - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
+    bad = []
+    for k, got, ref in pairs:
         scale = np.abs(ref).max() + 1e-8
         err = np.abs(got - ref).max()
-        assert err <= 2e-3 * scale + 1e-6, f"{k}: err {err:.3g} scale {scale:.3g}"
-        checked += 1
-    assert checked > 100
-    # cost-volume gradient w.r.t. the features: compare through the volume gradient
-    for s in range(3):
-        assert fl[s].grad is not None and torch.isfinite(fl[s].grad).all()
+        if err > 1e-3 * scale + 1e-6:
+            bad.append(f"{k}: err {err:.3g} scale {scale:.3g}")
+    assert len(pairs) > 100
+    assert not bad, f"{len(bad)}/{len(pairs)} params off:\n" + "\n".join(bad[:40])
+
+
+def test_training_gradients_vs_oracle_train_bn_random_offsets():
+    """Train-mode BN (batch statistics) with learned-like random offsets.  The bilinear sampler's
+    derivative jumps where a sample crosses an integer grid line, and CPU/GPU offsets differ in
+    the last bits, so a handful of samples may take different branches: the gradients are
+    compared by direction (cosine similarity) rather than element-wise."""
+    sd = state_dict_of(golden("aggregation_inter"))
+    loss, ref_loss, pairs = _grads_vs_oracle(sd, train_bn=True)
+    assert abs(loss - ref_loss) <= 1e-4 * max(1.0, abs(ref_loss))
+    allg = np.concatenate([g.ravel() for _, g, _ in pairs])
+    allr = np.concatenate([r.ravel() for _, _, r in pairs])
+    cos = float(allg @ allr / (np.linalg.norm(allg) * np.linalg.norm(allr)))
+    assert cos > 0.999, cos
+    for k, got, ref in pairs:
+        n = np.linalg.norm(ref)
+        if n > 1e-6:
+            assert float(got.ravel() @ ref.ravel()) / (np.linalg.norm(got) * n) > 0.99, k
