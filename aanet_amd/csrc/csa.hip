@@ -1,0 +1,91 @@
+// csa.hip -- cross-scale aggregation sum for gfx950 (replaces nets/aggregation.py:387-400 in the
+// eval path): out = act(e_0 + up(e_1) + ... ), where every e_j whose spatial size differs from
+// the output is bilinearly resized with PyTorch's align_corners=False rule
+// (F.interpolate(..., mode='bilinear', align_corners=False), aggregation.py:395-396).
+// One pass: each output element reads its same-size term once and 4 taps of each resized term,
+// instead of the reference's separate interpolate / add / add / LeakyReLU kernels.
+#include "common.h"
+
+namespace {
+
+constexpr int MAXIN = 4;
+
+struct CsaArgs {
+  const float *in[MAXIN];
+  int ih[MAXIN], iw[MAXIN];
+  float sh[MAXIN], sw[MAXIN];  // input/output size ratios (area_pixel_compute_scale)
+  int num;
+  float *out;
+  int N, C, H, W, act;
+};
+
+// PyTorch upsample_bilinear2d, align_corners=False: src = scale*(dst+0.5)-0.5, clamped at 0;
+// i1 = (int)src; i1p = i1 < in-1; lambda = src - i1.
+__device__ __forceinline__ float bilinear_resize(const float *__restrict__ im, int ih, int iw,
+                                                 float sh, float sw, int y, int x) {
+  float hr = sh * ((float)y + 0.5f) - 0.5f;
+  hr = hr < 0.f ? 0.f : hr;
+  float wr = sw * ((float)x + 0.5f) - 0.5f;
+  wr = wr < 0.f ? 0.f : wr;
+  const int h1 = (int)hr, w1 = (int)wr;
+  const int h1p = h1 < ih - 1 ? 1 : 0, w1p = w1 < iw - 1 ? 1 : 0;
+  const float h1l = hr - (float)h1, h0l = 1.f - h1l;
+  const float w1l = wr - (float)w1, w0l = 1.f - w1l;
+  const float *r0 = im + (long)h1 * iw, *r1 = im + (long)(h1 + h1p) * iw;
+  return h0l * (w0l * r0[w1] + w1l * r0[w1 + w1p]) + h1l * (w0l * r1[w1] + w1l * r1[w1 + w1p]);
+}
+
+__global__ __launch_bounds__(256) void csa_sum_kernel(CsaArgs a) {
+  const long HW = (long)a.H * a.W;
+  const long total = (long)a.N * a.C * HW;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long plane = e / HW;
+    const int q = (int)(e % HW), y = q / a.W, x = q % a.W;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXIN; ++j) {
+      if (j >= a.num) break;
+      float v;
+      if (a.ih[j] == a.H && a.iw[j] == a.W) {
+        v = a.in[j][e];
+      } else {
+        v = bilinear_resize(a.in[j] + plane * a.ih[j] * a.iw[j], a.ih[j], a.iw[j], a.sh[j],
+                            a.sw[j], y, x);
+      }
+      acc = j == 0 ? v : acc + v;
+    }
+    if (a.act == 1) acc = acc > 0.f ? acc : 0.f;
+    if (a.act == 2) acc = acc > 0.f ? acc : 0.2f * acc;
+    a.out[e] = acc;
+  }
+}
+
+}  // namespace
+
+extern "C" int aanet_csa_sum_f32(float *out, int n, int c, int h, int w, int num_inputs,
+                                 const float *const *inputs, const int *in_h, const int *in_w,
+                                 int act, aanet_stream_t stream) {
+  AANET_HOST_CHECK(out && inputs && in_h && in_w && n > 0 && c > 0 && h > 0 && w > 0);
+  AANET_HOST_CHECK(num_inputs >= 1 && num_inputs <= MAXIN && act >= 0 && act <= 2);
+  CsaArgs a;
+  for (int j = 0; j < MAXIN; ++j) {
+    a.in[j] = j < num_inputs ? inputs[j] : nullptr;
+    a.ih[j] = j < num_inputs ? in_h[j] : 1;
+    a.iw[j] = j < num_inputs ? in_w[j] : 1;
+    if (j < num_inputs && (!inputs[j] || in_h[j] <= 0 || in_w[j] <= 0)) return AANET_EINVAL;
+    a.sh[j] = (float)a.ih[j] / (float)h;
+    a.sw[j] = (float)a.iw[j] / (float)w;
+  }
+  a.num = num_inputs;
+  a.out = out;
+  a.N = n;
+  a.C = c;
+  a.H = h;
+  a.W = w;
+  a.act = act;
+  const long total = (long)n * c * h * w;
+  long g = (total + 255) / 256;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(csa_sum_kernel, dim3((unsigned)g), dim3(256), 0, as_hip(stream), a);
+  return aanet_launch_status();
+}

@@ -34,6 +34,7 @@ struct MdcnArgs {
   const float *bias;
   const float *post_scale;
   const float *post_shift;
+  const float *residual;  // added before the activation (same shape as out) or NULL
   int act;
   float *out;
   int N, C, H, W, Co, kh, kw, stride, pad, dil, groups, dg, Ho, Wo;
@@ -83,6 +84,49 @@ __device__ __forceinline__ float samp_val(const float *__restrict__ im, const Sa
   return v * s.m;
 }
 
+// Forward form of the sampler: the two horizontal corners of a row are read with ONE 8-byte
+// load (dword aligned) at a column base clamped into [0, W-2]; invalid corners carry weight 0
+// so the clamped read never changes the value.  Same products and sum order as samp_val.
+typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+struct Samp2 {
+  int itop, ibot;   // element offsets of the 2-wide column pair in rows hl and hl+1
+  int swap;         // 1 when the pair base is wl+1 (wl == -1) -> corners swapped
+  float w1, w2, w3, w4, m;
+};
+
+__device__ __forceinline__ void make_samp2(Samp2 &s, float h, float w, int H, int W, float m) {
+#pragma clang fp contract(off)
+  const bool valid = h > -1.f && w > -1.f && h < (float)H && w < (float)W;
+  const int hl = (int)floorf(h), wl = (int)floorf(w);
+  const float lh = h - (float)hl, lw = w - (float)wl;
+  const float hh = 1.f - lh, hw = 1.f - lw;
+  const bool ok1 = valid && hl >= 0 && wl >= 0;
+  const bool ok2 = valid && hl >= 0 && wl + 1 <= W - 1;
+  const bool ok3 = valid && hl + 1 <= H - 1 && wl >= 0;
+  const bool ok4 = valid && hl + 1 <= H - 1 && wl + 1 <= W - 1;
+  s.w1 = ok1 ? hh * hw : 0.f;
+  s.w2 = ok2 ? hh * lw : 0.f;
+  s.w3 = ok3 ? lh * hw : 0.f;
+  s.w4 = ok4 ? lh * lw : 0.f;
+  const int pb = valid ? min(max(wl, 0), W - 2) : 0;
+  const int rt = valid ? min(max(hl, 0), H - 1) : 0;
+  const int rb = valid ? min(max(hl + 1, 0), H - 1) : 0;
+  s.itop = rt * W + pb;
+  s.ibot = rb * W + pb;
+  s.swap = (valid && pb != wl) ? 1 : 0;
+  s.m = m;
+}
+
+__device__ __forceinline__ float samp_val2(const float *__restrict__ im, const Samp2 &s) {
+#pragma clang fp contract(off)
+  const f2u t = *reinterpret_cast<const f2u *>(im + s.itop);
+  const f2u b = *reinterpret_cast<const f2u *>(im + s.ibot);
+  const float v1 = s.swap ? t.y : t.x, v2 = s.swap ? t.x : t.y;
+  const float v3 = s.swap ? b.y : b.x, v4 = s.swap ? b.x : b.y;
+  const float v = s.w1 * v1 + s.w2 * v2 + s.w3 * v3 + s.w4 * v4;
+  return v * s.m;
+}
+
 __device__ __forceinline__ float load_mask(const MdcnArgs &a, int n, int g, int k, int K, long P,
                                            long p) {
   const float v = a.mask[(long)n * a.mask_bs + ((long)g * K + k) * P + p];
@@ -105,6 +149,26 @@ __device__ __forceinline__ void pixel_samp(Samp &s, const MdcnArgs &a, int n, in
   make_samp(s, h, w, a.H, a.W, m);
 }
 
+__device__ __forceinline__ void pixel_samp2(Samp2 &s, const MdcnArgs &a, int n, int g, int k,
+                                            long p, int ho, int wo) {
+#pragma clang fp contract(off)
+  const int K = a.kh * a.kw;
+  const long P = (long)a.Ho * a.Wo;
+  const int i = k / a.kw, j = k % a.kw;
+  const float *off = a.offset + (long)n * a.off_bs + (long)g * 2 * K * P;
+  const float oh = off[(long)(2 * k) * P + p], ow = off[(long)(2 * k + 1) * P + p];
+  const float m = load_mask(a, n, g, k, K, P, p);
+  const float h = (float)(ho * a.stride - a.pad + i * a.dil) + oh;
+  const float w = (float)(wo * a.stride - a.pad + j * a.dil) + ow;
+  make_samp2(s, h, w, a.H, a.W, m);
+}
+
+// Plain convolution tap: one in-bounds element or zero.
+struct SampP {
+  int idx;
+  int ok;
+};
+
 __device__ __forceinline__ float apply_act(float v, int act) {
   if (act == 1) return v > 0.f ? v : 0.f;
   if (act == 2) return v > 0.f ? v : 0.2f * v;
@@ -112,9 +176,13 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 }
 
 // ------------------------------------------------------------------------ forward -------
+// Implicit-GEMM convolution engine.  MODE 1: modulated deformable (bilinear sampler, used by
+// the DCN); MODE 0: plain convolution (one tap per input element; used by the eval fast path
+// for every other conv of the ISA/CSA blocks: 1x1, 3x3, dilated, grouped, strided).
+// Epilogue: y = act(post_scale*(acc + bias) + post_shift + residual).
 // grid: x = N * ceil(P/64), y = groups * ceil(Cog/CO_T).
-template <int CO_T>
-__global__ __launch_bounds__(NT) void mdcn_fwd_kernel(MdcnArgs a) {
+template <int MODE, int CO_T>
+__global__ __launch_bounds__(NT) void conv_fwd_kernel(MdcnArgs a) {
   constexpr int NCB = CO_T / 16;  // 16-wide output-channel blocks per wave
   constexpr int WP = 34;          // sW pitch: conflict-free A reads (2*i + kr distinct)
   __shared__ __attribute__((aligned(16))) float sCol[KC * CP];
@@ -141,18 +209,38 @@ __global__ __launch_bounds__(NT) void mdcn_fwd_kernel(MdcnArgs a) {
   const int kr = lane >> 4, jj = lane & 15;
   const int cbeg = gc * Cg, cend = (gc + 1) * Cg;
   for (int k = 0; k < K; ++k) {
+    SampP sp = {0, 0};
+    if (MODE == 0) {
+      const int hi = ho * a.stride - a.pad + (k / a.kw) * a.dil;
+      const int wi = wo * a.stride - a.pad + (k % a.kw) * a.dil;
+      sp.ok = pvalid && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+      sp.idx = sp.ok ? hi * a.W + wi : 0;
+    }
     for (int c0 = cbeg; c0 < cend;) {
-      const int g = c0 / cpg;
-      const int c1 = min(min(c0 + KC, (g + 1) * cpg), cend);
+      const int g = MODE ? c0 / cpg : 0;
+      const int c1 = MODE ? min(min(c0 + KC, (g + 1) * cpg), cend) : min(c0 + KC, cend);
       const int rows = c1 - c0;
-      Samp s;
-      pixel_samp(s, a, n, g, k, pvalid ? p : 0, ho, wo);
+      if (MODE) {
+        Samp2 s;
+        pixel_samp2(s, a, n, g, k, pvalid ? p : 0, ho, wo);
 #pragma unroll
-      for (int ii = 0; ii < KC / 4; ++ii) {
-        const int cl = wave + 4 * ii;
-        float v = 0.f;
-        if (cl < rows && pvalid) v = samp_val(xn + (long)(c0 + cl) * HW, s);
-        sCol[cl * CP + lane] = v;
+        for (int ii = 0; ii < KC / 4; ++ii) {
+          const int cl = wave + 4 * ii;
+          float v = 0.f;
+          if (cl < rows && pvalid) v = samp_val2(xn + (long)(c0 + cl) * HW, s);
+          sCol[cl * CP + lane] = v;
+        }
+      } else {
+#pragma unroll
+        for (int ii = 0; ii < KC / 4; ++ii) {
+          const int cl = wave + 4 * ii;
+          float v = 0.f;
+          if (cl < rows) {
+            const float t = xn[(long)(c0 + cl) * HW + sp.idx];
+            v = sp.ok ? t : 0.f;
+          }
+          sCol[cl * CP + lane] = v;
+        }
       }
       for (int e = tid; e < KC * CO_T; e += NT) {
         const int cl = e % KC, col = e / KC;
@@ -188,7 +276,9 @@ __global__ __launch_bounds__(NT) void mdcn_fwd_kernel(MdcnArgs a) {
           float v = acc[m][r];
           if (a.bias) v += a.bias[co];
           if (a.post_scale) v = v * a.post_scale[co] + a.post_shift[co];
-          a.out[((long)n * a.Co + co) * P + pe] = apply_act(v, a.act);
+          const long o = ((long)n * a.Co + co) * P + pe;
+          if (a.residual) v += a.residual[o];
+          a.out[o] = apply_act(v, a.act);
         }
       }
   }
@@ -204,9 +294,9 @@ __global__ void mdcn_im2col_kernel(MdcnArgs a, float *__restrict__ col) {
        e += (long)gridDim.x * blockDim.x) {
     const long p = e % P;
     const int ck = (int)(e / P), c = ck / K, k = ck % K;
-    Samp s;
-    pixel_samp(s, a, 0, c / cpg, k, p, (int)(p / a.Wo), (int)(p % a.Wo));
-    col[e] = samp_val(a.x + (long)c * HW, s);
+    Samp2 s;
+    pixel_samp2(s, a, 0, c / cpg, k, p, (int)(p / a.Wo), (int)(p % a.Wo));
+    col[e] = samp_val2(a.x + (long)c * HW, s);
   }
 }
 
@@ -455,6 +545,7 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
   a.bias = bias;
   a.post_scale = ps;
   a.post_shift = psh;
+  a.residual = nullptr;
   a.act = act;
   a.out = out;
   a.N = n;
@@ -477,10 +568,13 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
   return a;
 }
 
+template <int MODE>
 int launch_fwd(const MdcnArgs &a, hipStream_t st) {
   const int rc = check_shapes(a);
   if (rc) return rc;
-  if (!a.x || !a.offset || !a.mask || !a.weight || !a.out) return AANET_EINVAL;
+  if (!a.x || !a.weight || !a.out) return AANET_EINVAL;
+  if (MODE && (!a.offset || !a.mask)) return AANET_EINVAL;
+  if (MODE && a.W < 2) return AANET_EUNSUPPORTED;  // pair-gather sampler needs 2 columns
   if (a.post_scale && !a.post_shift) return AANET_EINVAL;
   const long P = (long)a.Ho * a.Wo;
   const int Cog = a.Co / a.groups;
@@ -488,9 +582,9 @@ int launch_fwd(const MdcnArgs &a, hipStream_t st) {
   const int ncot = host_div_up(Cog, co_t);
   dim3 grid((unsigned)(a.N * host_div_up(P, PT)), (unsigned)(a.groups * ncot));
   switch (co_t) {
-    case 16: hipLaunchKernelGGL(mdcn_fwd_kernel<16>, grid, dim3(NT), 0, st, a); break;
-    case 32: hipLaunchKernelGGL(mdcn_fwd_kernel<32>, grid, dim3(NT), 0, st, a); break;
-    default: hipLaunchKernelGGL(mdcn_fwd_kernel<64>, grid, dim3(NT), 0, st, a); break;
+    case 16: hipLaunchKernelGGL((conv_fwd_kernel<MODE, 16>), grid, dim3(NT), 0, st, a); break;
+    case 32: hipLaunchKernelGGL((conv_fwd_kernel<MODE, 32>), grid, dim3(NT), 0, st, a); break;
+    default: hipLaunchKernelGGL((conv_fwd_kernel<MODE, 64>), grid, dim3(NT), 0, st, a); break;
   }
   return aanet_launch_status();
 }
@@ -509,7 +603,19 @@ extern "C" int aanet_mdcn_fwd_f32(const float *x, const float *offset, const flo
                                   int dil, int groups, int dg, aanet_stream_t stream) {
   MdcnArgs a = make_args(x, offset, -1, mask, -1, 0, 1.f, weight, bias, nullptr, nullptr, 0, out,
                          n, c, h, w, co, kh, kw, stride, pad, dil, groups, dg);
-  return launch_fwd(a, as_hip(stream));
+  return launch_fwd<1>(a, as_hip(stream));
+}
+
+extern "C" int aanet_conv2d_fused_f32(const float *x, const float *weight, const float *bias,
+                                      const float *post_scale, const float *post_shift,
+                                      const float *residual, int act, float *out, int n, int c,
+                                      int h, int w, int co, int kh, int kw, int stride, int pad,
+                                      int dil, int groups, aanet_stream_t stream) {
+  if (act < 0 || act > 2) return AANET_EINVAL;
+  MdcnArgs a = make_args(x, nullptr, 0, nullptr, 0, 0, 1.f, weight, bias, post_scale, post_shift,
+                         act, out, n, c, h, w, co, kh, kw, stride, pad, dil, groups, 1);
+  a.residual = residual;
+  return launch_fwd<0>(a, as_hip(stream));
 }
 
 extern "C" int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset,
@@ -524,7 +630,7 @@ extern "C" int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset,
   MdcnArgs a = make_args(x, offset, offset_batch_stride, mask, mask_batch_stride, mask_logits,
                          mask_scale, weight, bias, post_scale, post_shift, act, out, n, c, h, w,
                          co, kh, kw, stride, pad, dil, groups, dg);
-  return launch_fwd(a, as_hip(stream));
+  return launch_fwd<1>(a, as_hip(stream));
 }
 
 extern "C" int aanet_mdcn_im2col_f32(const float *x, const float *offset, const float *mask,
@@ -535,6 +641,7 @@ extern "C" int aanet_mdcn_im2col_f32(const float *x, const float *offset, const 
   const int rc = check_shapes(a);
   if (rc) return rc;
   if (!x || !offset || !mask || !col) return AANET_EINVAL;
+  if (w < 2) return AANET_EUNSUPPORTED;
   const long total = (long)c * kh * kw * a.Ho * a.Wo;
   hipLaunchKernelGGL(mdcn_im2col_kernel, dim3(host_div_up(total, 256) > 8192 ? 8192 : host_div_up(total, 256)),
                      dim3(256), 0, as_hip(stream), a, col);

@@ -1,10 +1,12 @@
-"""Eval-mode fusion helpers: fold BatchNorm into the preceding conv (cached per parameter
-version) so the inference graph runs conv+BN(+activation) as one op.
-
-Training mode never uses these: modules then run the reference op sequence with autograd.
+"""Eval-mode fusion helpers.  In eval mode without autograd every conv of the ISA/CSA blocks runs
+on the HIP implicit-GEMM engine (aanet_conv2d_fused_f32) with the following BatchNorm folded
+into its weights/bias (cached per parameter version), the activation and the bottleneck's
+residual add in its epilogue.  Training mode never uses these: modules then run the reference
+op sequence with autograd.
 """
 import torch
-import torch.nn.functional as F
+
+from .. import ops
 
 
 def bn_scale_shift(bn):
@@ -19,16 +21,22 @@ def _key(*tensors):
 
 
 def folded(conv, bn):
-    """(weight, bias) of conv followed by eval BN, cached on the conv module."""
-    key = _key(conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var)
+    """(weight, bias) of conv followed by eval BN (bn may be None), cached on the conv module."""
+    tensors = (conv.weight, conv.bias) + ((bn.weight, bn.bias, bn.running_mean, bn.running_var)
+                                          if bn is not None else ())
+    key = _key(*tensors)
     cache = getattr(conv, "_aanet_fold", None)
     if cache is not None and cache[0] == key:
         return cache[1], cache[2]
     with torch.no_grad():
-        scale, shift = bn_scale_shift(bn)
-        w = (conv.weight * scale.view(-1, 1, 1, 1)).contiguous()
-        b = shift if conv.bias is None else conv.bias * scale + shift
-        b = b.contiguous()
+        if bn is None:
+            w = conv.weight.contiguous()
+            b = None if conv.bias is None else conv.bias.contiguous()
+        else:
+            scale, shift = bn_scale_shift(bn)
+            w = (conv.weight * scale.view(-1, 1, 1, 1)).contiguous()
+            b = shift if conv.bias is None else conv.bias * scale + shift
+            b = b.contiguous()
     conv._aanet_fold = (key, w, b)
     return w, b
 
@@ -46,15 +54,18 @@ def bn_affine(bn):
     return scale, shift
 
 
-def conv_bn_act(x, conv, bn, act=None, inplace_ok=True):
-    """conv -> eval BN -> act ('relu' | 'leaky' | None) with BN folded into the conv."""
+def _int(v):
+    return v[0] if isinstance(v, (tuple, list)) else v
+
+
+def conv_bn_act(x, conv, bn=None, act=None, residual=None):
+    """act(BN(conv(x)) [+ residual]) as ONE HIP kernel (BN folded into the conv)."""
     w, b = folded(conv, bn)
-    y = F.conv2d(x, w, b, conv.stride, conv.padding, conv.dilation, conv.groups)
-    if act == "relu":
-        y = F.relu_(y) if inplace_ok else F.relu(y)
-    elif act == "leaky":
-        y = F.leaky_relu_(y, 0.2) if inplace_ok else F.leaky_relu(y, 0.2)
-    return y
+    for v in (conv.stride, conv.padding, conv.dilation):
+        if isinstance(v, (tuple, list)) and v[0] != v[1]:
+            raise NotImplementedError("asymmetric conv parameters")
+    return ops.conv2d_fused(x.contiguous(), w, b, _int(conv.stride), _int(conv.padding),
+                            _int(conv.dilation), conv.groups, act, residual)
 
 
 def use_fused(module, x):

@@ -4,12 +4,15 @@ AdaptiveAggregationModule (aggregation.py:313-402) and AdaptiveAggregation (406-
 reference's constructor signatures, module tree (state-dict keys `fusions.{f}.branches.{s}.0.*`,
 `fusions.{f}.fuse_layers.{i}.{j}.*`, `final_conv.{i}.*`) and forward semantics, including the
 in-place mutation of the caller's list (`x[i] = dconv(x[i])`, aggregation.py:382).
-ISA bottlenecks run the HIP DCN; in eval mode BN is folded into the CSA convs.
+ISA bottlenecks run the HIP DCN.  In eval mode without autograd every conv is a HIP
+implicit-GEMM kernel (BN folded) and each CSA output branch is one fused resize+sum+LeakyReLU
+kernel; training mode runs the reference op sequence with autograd.
 The 3D-conv aggregators (StereoNet/PSMNet/GCNet) are out of scope.
 """
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import ops
 from ._fuse import conv_bn_act, use_fused
 from .deform import DeformSimpleBottleneck, SimpleBottleneck
 
@@ -66,17 +69,26 @@ class AdaptiveAggregationModule(nn.Module):
 
         self.relu = nn.LeakyReLU(0.2, inplace=True)
 
-    def _exchange(self, i, j, xj, fused):
-        layer = self.fuse_layers[i][j]
-        if not fused or i == j:
-            return layer(xj)
-        if i < j:
-            return conv_bn_act(xj, layer[0], layer[1], None)
-        y = xj
-        for k, seq in enumerate(layer):
-            last = k == len(layer) - 1
-            y = conv_bn_act(y, seq[0], seq[1], None if last else "leaky")
-        return y
+    def _fuse_eval(self, x):
+        """Eval CSA: each exchange conv (+BN folded, +LeakyReLU inside strided chains) is one HIP
+        conv kernel at its own resolution; the resize + sum + LeakyReLU of every output branch is
+        one aanet_csa_sum_f32 kernel (same term order as aggregation.py:388-400)."""
+        x_fused = []
+        for i in range(len(self.fuse_layers)):
+            terms = []
+            for j in range(len(self.branches)):
+                layer = self.fuse_layers[i][j]
+                if i == j:
+                    terms.append(x[j])
+                elif i < j:
+                    terms.append(conv_bn_act(x[j], layer[0], layer[1], None))
+                else:
+                    y = x[j]
+                    for k, seq in enumerate(layer):
+                        y = conv_bn_act(y, seq[0], seq[1], None if k == len(layer) - 1 else "leaky")
+                    terms.append(y)
+            x_fused.append(ops.csa_sum([t.contiguous() for t in terms], act="leaky"))
+        return x_fused
 
     def forward(self, x):
         """aggregation.py:375-402."""
@@ -90,14 +102,15 @@ class AdaptiveAggregationModule(nn.Module):
         if self.num_scales == 1:  # without fusions
             return x
 
-        fused = use_fused(self, x[0])
+        if use_fused(self, x[0]):
+            return self._fuse_eval(x)
         x_fused = []
         for i in range(len(self.fuse_layers)):
             for j in range(len(self.branches)):
                 if j == 0:
-                    x_fused.append(self._exchange(i, 0, x[0], fused))
+                    x_fused.append(self.fuse_layers[i][0](x[0]))
                 else:
-                    exchange = self._exchange(i, j, x[j], fused)
+                    exchange = self.fuse_layers[i][j](x[j])
                     if exchange.size()[2:] != x_fused[i].size()[2:]:
                         exchange = F.interpolate(exchange, size=x_fused[i].size()[2:],
                                                  mode='bilinear', align_corners=False)
@@ -144,12 +157,16 @@ class AdaptiveAggregation(nn.Module):
                 break
 
     def forward(self, cost_volume):
-        """aggregation.py:452-464."""
+        """aggregation.py:452-464 (final 1x1 conv with bias on the HIP conv engine in eval)."""
         assert isinstance(cost_volume, list)
         for i in range(self.num_fusions):
             fusion = self.fusions[i]
             cost_volume = fusion(cost_volume)
         out = []  # 1/3, 1/6, 1/12
+        fused = use_fused(self, cost_volume[0])
         for i in range(len(self.final_conv)):
-            out = out + [self.final_conv[i](cost_volume[i])]
+            if fused:
+                out = out + [conv_bn_act(cost_volume[i], self.final_conv[i])]
+            else:
+                out = out + [self.final_conv[i](cost_volume[i])]
         return out

@@ -73,10 +73,10 @@ class DeformConv2d(nn.Module):
         offset = self.offset_conv(x)
         return self.deform_conv(x, offset)
 
-    def forward_fused(self, x, bn=None, act=0):
-        """Eval path: offset_conv (MIOpen) -> one HIP kernel for DCN (+BN, +act)."""
+    def forward_fused(self, x, bn=None, act=None):
+        """Eval path: offset_conv (HIP conv engine) -> one HIP kernel for DCN (+BN, +act)."""
         dc = self.deform_conv
-        offset_mask = self.offset_conv(x)
+        offset_mask = conv_bn_act(x, self.offset_conv)
         ps, psh = bn_affine(bn) if bn is not None else (None, None)
         return ops.mdcn_forward_fused(x.contiguous(), offset_mask.contiguous(), dc.weight,
                                       dc.bias, ps, psh, act, dc.stride, dc.padding, dc.dilation,
@@ -102,19 +102,16 @@ class _BottleneckBase(nn.Module):
         return out
 
     def _forward_fused(self, x, deform):
+        """conv1+bn1+relu -> conv2(+bn2+relu) -> conv3+bn3+identity+relu: 3-4 HIP kernels."""
         out = conv_bn_act(x, self.conv1, self.bn1, "relu")
         if deform and self.conv2.modulation:
-            out = self.conv2.forward_fused(out, self.bn2, act=1)
+            out = self.conv2.forward_fused(out, self.bn2, act="relu")
+        elif deform:
+            out = F.relu_(self.bn2(self.conv2(out)))
         else:
-            if deform:
-                out = self.bn2(self.conv2(out))
-                out = F.relu_(out)
-            else:
-                out = conv_bn_act(out, self.conv2, self.bn2, "relu")
-        out = conv_bn_act(out, self.conv3, self.bn3, None)
+            out = conv_bn_act(out, self.conv2, self.bn2, "relu")
         identity = self.downsample(x) if self.downsample is not None else x
-        out += identity
-        return F.relu_(out)
+        return conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity.contiguous())
 
 
 class DeformBottleneck(_BottleneckBase):

@@ -129,7 +129,7 @@ def mdcn_forward(x, offset, mask, weight, bias=None, stride=1, padding=0, dilati
     return out
 
 
-def mdcn_forward_fused(x, offset_mask, weight, bias=None, post_scale=None, post_shift=None, act=0,
+def mdcn_forward_fused(x, offset_mask, weight, bias=None, post_scale=None, post_shift=None, act=None,
                        stride=1, padding=0, dilation=1, deformable_groups=1, mask_scale=2.0):
     """Eval fast path of DeformConv2d (nets/deform.py:78-97) + BN + activation.
 
@@ -149,8 +149,44 @@ def mdcn_forward_fused(x, offset_mask, weight, bias=None, post_scale=None, post_
     mask_ptr = offset_mask.data_ptr() + 4 * deformable_groups * 2 * K * Ho * Wo
     call("aanet_mdcn_fwd_fused_f32", ptr(x), ptr(offset_mask), bs, _lib.ctypes.c_void_p(mask_ptr),
          bs, 1, float(mask_scale), ptr(weight), ptr(bias), ptr(post_scale), ptr(post_shift),
-         int(act), ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation, 1,
+         ACT[act] if not isinstance(act, int) else act, ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation, 1,
          deformable_groups, stream_of(x))
+    return out
+
+
+ACT = {None: 0, "relu": 1, "leaky": 2}
+
+
+def conv2d_fused(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None,
+                 residual=None, post_scale=None, post_shift=None):
+    """Plain conv on the HIP implicit-GEMM engine: act(post_scale*(conv+bias)+post_shift+residual)."""
+    require_gpu(x, weight, bias, residual, post_scale, post_shift,
+                names=("input", "weight", "bias", "residual", "post_scale", "post_shift"))
+    N, C, H, W = x.shape
+    Co, _, kh, kw = weight.shape
+    Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
+    if residual is not None and tuple(residual.shape) != (N, Co, Ho, Wo):
+        raise ValueError("residual shape must match the output")
+    out = torch.empty((N, Co, Ho, Wo), device=x.device, dtype=x.dtype)
+    call("aanet_conv2d_fused_f32", ptr(x), ptr(weight), ptr(bias), ptr(post_scale), ptr(post_shift),
+         ptr(residual), ACT[act], ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation,
+         groups, stream_of(x))
+    return out
+
+
+def csa_sum(inputs, act="leaky"):
+    """act(inputs[0] + resize(inputs[1]) + ...) at inputs[0]'s size (aggregation.py:387-400)."""
+    require_gpu(*inputs)
+    N, C, H, W = inputs[0].shape
+    for t in inputs:
+        if t.shape[:2] != (N, C):
+            raise ValueError("csa_sum inputs must share batch and channels")
+    out = torch.empty_like(inputs[0])
+    k = len(inputs)
+    ptrs = (_lib.ctypes.c_void_p * k)(*[t.data_ptr() for t in inputs])
+    hs = (_lib.ctypes.c_int * k)(*[t.shape[2] for t in inputs])
+    ws = (_lib.ctypes.c_int * k)(*[t.shape[3] for t in inputs])
+    call("aanet_csa_sum_f32", ptr(out), N, C, H, W, k, ptrs, hs, ws, ACT[act], stream_of(out))
     return out
 
 

@@ -99,6 +99,25 @@ int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset, long offset_ba
                              int n, int c, int h, int w, int co, int kh, int kw, int stride,
                              int pad, int dil, int groups, int dg, aanet_stream_t stream);
 
+/* Plain convolution on the same implicit-GEMM engine, for the eval fast path of every other
+ * conv in the ISA/CSA blocks (nets/deform.py:6-14 conv1x1/conv3x3, nets/deform.py:70-72
+ * offset_conv, nets/aggregation.py:354-370 fuse layers, :447 final_conv), which the reference
+ * runs through cuDNN.  BN is folded by the caller into weight/bias (or passed as post_scale /
+ * post_shift).  y = act(post_scale*(conv(x) + bias) + post_shift + residual); act 0 none,
+ * 1 ReLU, 2 LeakyReLU(0.2).  bias / post_* / residual may be NULL; residual has out's shape. */
+int aanet_conv2d_fused_f32(const float *x, const float *weight, const float *bias,
+                           const float *post_scale, const float *post_shift, const float *residual,
+                           int act, float *out, int n, int c, int h, int w, int co, int kh, int kw,
+                           int stride, int pad, int dil, int groups, aanet_stream_t stream);
+
+/* Cross-scale fusion sum (nets/aggregation.py:387-400): out[n,c,h,w] =
+ * act(sum_j resize(inputs[j])), j in input order; inputs whose (in_h, in_w) differ from
+ * (h, w) are resized bilinearly with align_corners=False (aggregation.py:395-396).
+ * Up to 4 inputs, each [n, c, in_h[j], in_w[j]]. */
+int aanet_csa_sum_f32(float *out, int n, int c, int h, int w, int num_inputs,
+                      const float *const *inputs, const int *in_h, const int *in_w, int act,
+                      aanet_stream_t stream);
+
 /* deform_conv_cuda.cpp:571-685 (modulated_deform_conv_cuda_backward) + kernel.cu:635-767.
  * grad_x, grad_offset, grad_mask are OVERWRITTEN; grad_weight and grad_bias (may be NULL)
  * ACCUMULATE, as in the reference (cpp:660-671). */
