@@ -176,104 +176,235 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 }
 
 // ------------------------------------------------------------------------ forward -------
-// Implicit-GEMM convolution engine.  MODE 1: modulated deformable (bilinear sampler, used by
-// the DCN); MODE 0: plain convolution (one tap per input element; used by the eval fast path
-// for every other conv of the ISA/CSA blocks: 1x1, 3x3, dilated, grouped, strided).
+// Implicit-GEMM convolution engine.  MODE 1: modulated deformable (bilinear sampler, the DCN);
+// MODE 0: plain convolution (one tap per input element; every other conv of the ISA/CSA
+// blocks: 1x1, 3x3, dilated, grouped, strided).
+//
+// Workgroup = 256 threads, output tile CO_T channels x PTT pixels of one image.  The K
+// dimension is walked in chunks of (tap k, <= 32 input channels of one deformable group):
+//   stage   : each thread builds PTT*32/256 im2col values of the chunk for ONE pixel (sampling
+//             state computed once per (pixel, tap, group)) -> LDS [pixel][channel];
+//             the weight slice -> LDS [co][channel];
+//   contract: wave w owns CO_T x (PTT/4) outputs; per 16 channels it reads one ds_read_b128 per
+//             16-row operand block and issues 4 k-steps of v_mfma_f32_16x16x4_f32 -- the
+//             reduction index is permuted (lane group kr takes channels 4kr..4kr+3) identically
+//             for both operands, so the sum is unchanged.
+// Software pipeline: LDS is double buffered; while the MFMAs of chunk c run, the global loads
+// of chunk c+1 are in flight in registers and the offsets/mask of chunk c+2 are being fetched;
+// one barrier per chunk.
 // Epilogue: y = act(post_scale*(acc + bias) + post_shift + residual).
-// grid: x = N * ceil(P/64), y = groups * ceil(Cog/CO_T).
-template <int MODE, int CO_T>
-__global__ __launch_bounds__(NT) void conv_fwd_kernel(MdcnArgs a) {
-  constexpr int NCB = CO_T / 16;  // 16-wide output-channel blocks per wave
-  constexpr int WP = 34;          // sW pitch: conflict-free A reads (2*i + kr distinct)
-  __shared__ __attribute__((aligned(16))) float sCol[KC * CP];
-  __shared__ __attribute__((aligned(16))) float sW[CO_T * WP];
+// grid: x = N * ceil(P/PTT), y = groups * ceil(Cog/CO_T).
+constexpr int SP = 40;  // LDS row pitch (floats) of both tiles: conflict-free ds_read_b128
+
+struct ChunkIt {
+  int k, c0, c1;
+  __device__ __forceinline__ void first(int cbeg, int cend, int cpg, int mode) {
+    k = 0;
+    c0 = cbeg;
+    c1 = next_end(cbeg, cend, cpg, mode);
+  }
+  __device__ __forceinline__ static int next_end(int c0, int cend, int cpg, int mode) {
+    int e = min(c0 + KC, cend);
+    if (mode) e = min(e, (c0 / cpg + 1) * cpg);
+    return e;
+  }
+  __device__ __forceinline__ void advance(int cbeg, int cend, int cpg, int mode) {
+    c0 = c1;
+    if (c0 >= cend) {
+      c0 = cbeg;
+      ++k;
+    }
+    c1 = next_end(c0, cend, cpg, mode);
+  }
+};
+
+template <int MODE, int CO_T, int PTT, int PACKED>
+__global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
+  constexpr int NCB = CO_T / 16;         // 16-row output-channel blocks per wave
+  constexpr int NPB = PTT / 64;          // 16-col pixel blocks per wave
+  constexpr int CPT = KC * PTT / NT;     // im2col values staged per thread per chunk
+  constexpr int WPT = KC * CO_T / NT;    // weights staged per thread per chunk
+  constexpr int BUF = (PTT + CO_T) * SP; // floats per LDS buffer
+  __shared__ __attribute__((aligned(16))) float smem[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long P = (long)a.Ho * a.Wo;
-  const int ntiles = (int)((P + PT - 1) / PT);
+  const int ntiles = (int)((P + PTT - 1) / PTT);
   const int n = blockIdx.x / ntiles, tile = blockIdx.x % ntiles;
   const int Cg = a.C / a.groups, Cog = a.Co / a.groups, K = a.kh * a.kw, cpg = a.C / a.dg;
   const int ncot = (Cog + CO_T - 1) / CO_T;
   const int gc = blockIdx.y / ncot, cot = blockIdx.y % ncot;
   const int co0 = gc * Cog + cot * CO_T, co_end = min(co0 + CO_T, (gc + 1) * Cog);
-  const long p = (long)tile * PT + lane;
-  const bool pvalid = p < P;
-  const int ho = pvalid ? (int)(p / a.Wo) : 0, wo = pvalid ? (int)(p % a.Wo) : 0;
+  const int cbeg = gc * Cg, cend = (gc + 1) * Cg;
   const long HW = (long)a.H * a.W;
   const float *xn = a.x + (long)n * a.C * HW;
 
-  f32x4 acc[NCB];
+  // staging role: one pixel, CPT consecutive channels of the chunk
+  const int spx = tid % PTT, scb = (tid / PTT) * CPT;
+  const long p = (long)tile * PTT + spx;
+  const bool pvalid = p < P;
+  const int ho = pvalid ? (int)(p / a.Wo) : 0, wo = pvalid ? (int)(p % a.Wo) : 0;
+  const long psafe = pvalid ? p : 0;
+
+  const int nchunks = K * ((cend - cbeg) + 0);  // upper bound helper (not used directly)
+  (void)nchunks;
+
+  // ---- register staging buffers
+  float wreg[WPT];
+  float vraw[CPT];              // plain: loaded values
+  f2u traw[MODE ? CPT : 1], braw[MODE ? CPT : 1];
+  Samp2 snext;                  // sampling state of the chunk being loaded (MODE 1)
+  float off_h = 0.f, off_w = 0.f, mlog = 0.f;  // raw offsets/mask of the chunk after it
+  int sp_ok = 0, sp_idx = 0;
+
+  auto load_params_raw = [&](const ChunkIt &c) {  // MODE 1: issue offset / mask loads
+    const int g = c.c0 / cpg;
+    const float *off = a.offset + (long)n * a.off_bs + (long)g * 2 * K * P;
+    off_h = off[(long)(2 * c.k) * P + psafe];
+    off_w = off[(long)(2 * c.k + 1) * P + psafe];
+    mlog = a.mask[(long)n * a.mask_bs + ((long)g * K + c.k) * P + psafe];
+  };
+  auto finish_params = [&](const ChunkIt &c) {  // MODE 1: coordinates from the raw loads
+#pragma clang fp contract(off)
+    const int i = c.k / a.kw, j = c.k % a.kw;
+    const float m = a.mask_logits ? a.mask_scale * (1.f / (1.f + expf(-mlog))) : mlog;
+    const float h = (float)(ho * a.stride - a.pad + i * a.dil) + off_h;
+    const float w = (float)(wo * a.stride - a.pad + j * a.dil) + off_w;
+    make_samp2(snext, h, w, a.H, a.W, m);
+  };
+  auto issue_loads = [&](const ChunkIt &c) {
+    const int rows = c.c1 - c.c0;
 #pragma unroll
-  for (int m = 0; m < NCB; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < WPT; ++i) {
+      const int e = tid + NT * i, co = e / KC, cl = e % KC;
+      const int cog = co0 + co;
+      float v = 0.f;
+      if (cl < rows && cog < co_end) {
+        const int cc = c.c0 + cl - cbeg;
+        v = PACKED ? a.weight[((long)c.k * a.Co + cog) * Cg + cc]
+                   : a.weight[((long)cog * Cg + cc) * K + c.k];
+      }
+      wreg[i] = v;
+    }
+    if (MODE == 0) {
+      const int hi = ho * a.stride - a.pad + (c.k / a.kw) * a.dil;
+      const int wi = wo * a.stride - a.pad + (c.k % a.kw) * a.dil;
+      sp_ok = pvalid && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+      sp_idx = sp_ok ? hi * a.W + wi : 0;
+#pragma unroll
+      for (int e = 0; e < CPT; ++e) {
+        const int cl = scb + e;
+        vraw[e] = cl < rows ? xn[(long)(c.c0 + cl) * HW + sp_idx] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < CPT; ++e) {
+        const int cl = min(scb + e, rows - 1);
+        const float *im = xn + (long)(c.c0 + cl) * HW;
+        traw[e] = *reinterpret_cast<const f2u *>(im + snext.itop);
+        braw[e] = *reinterpret_cast<const f2u *>(im + snext.ibot);
+      }
+    }
+  };
+  auto store_stage = [&](const ChunkIt &c, int buf) {
+    float *sC = smem + buf * BUF, *sW = sC + PTT * SP;
+    const int rows = c.c1 - c.c0;
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      const int e = tid + NT * i;
+      sW[(e / KC) * SP + e % KC] = wreg[i];
+    }
+    float v[CPT];
+#pragma unroll
+    for (int e = 0; e < CPT; ++e) {
+      if (MODE == 0) {
+        v[e] = sp_ok ? vraw[e] : 0.f;
+      } else {
+#pragma clang fp contract(off)
+        const Samp2 &s = snext;
+        const float v1 = s.swap ? traw[e].y : traw[e].x, v2 = s.swap ? traw[e].x : traw[e].y;
+        const float v3 = s.swap ? braw[e].y : braw[e].x, v4 = s.swap ? braw[e].x : braw[e].y;
+        const float t = s.w1 * v1 + s.w2 * v2 + s.w3 * v3 + s.w4 * v4;
+        v[e] = (scb + e < rows && pvalid) ? t * s.m : 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < CPT / 4; ++q)
+      *reinterpret_cast<f32x4 *>(sC + spx * SP + scb + 4 * q) =
+          f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+  };
+
+  f32x4 acc[NCB][NPB];
+#pragma unroll
+  for (int m = 0; m < NCB; ++m)
+#pragma unroll
+    for (int b = 0; b < NPB; ++b) acc[m][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int kr = lane >> 4, jj = lane & 15;
-  const int cbeg = gc * Cg, cend = (gc + 1) * Cg;
-  for (int k = 0; k < K; ++k) {
-    SampP sp = {0, 0};
-    if (MODE == 0) {
-      const int hi = ho * a.stride - a.pad + (k / a.kw) * a.dil;
-      const int wi = wo * a.stride - a.pad + (k % a.kw) * a.dil;
-      sp.ok = pvalid && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
-      sp.idx = sp.ok ? hi * a.W + wi : 0;
+  ChunkIt cur, nxt, nn;
+  cur.first(cbeg, cend, cpg, MODE);
+  // prologue: chunk 0 -> LDS buffer 0; parameters of chunk 1 fetched
+  if (MODE) {
+    load_params_raw(cur);
+    finish_params(cur);
+  }
+  issue_loads(cur);
+  store_stage(cur, 0);
+  nxt = cur;
+  nxt.advance(cbeg, cend, cpg, MODE);
+  bool has_next = nxt.k < K;
+  if (MODE && has_next) {
+    load_params_raw(nxt);
+    finish_params(nxt);
+  }
+  __syncthreads();
+
+  for (int buf = 0;; buf ^= 1) {
+    nn = nxt;
+    nn.advance(cbeg, cend, cpg, MODE);
+    const bool has_nn = has_next && nn.k < K;
+    if (has_next) issue_loads(nxt);              // chunk c+1 loads in flight
+    if (MODE && has_nn) load_params_raw(nn);     // chunk c+2 offsets in flight
+    {
+      const float *sC = smem + buf * BUF, *sW = sC + PTT * SP;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4 A[NCB], B[NPB];
+#pragma unroll
+        for (int m = 0; m < NCB; ++m)
+          A[m] = *reinterpret_cast<const f32x4 *>(sW + (16 * m + jj) * SP + 16 * h + 4 * kr);
+#pragma unroll
+        for (int b = 0; b < NPB; ++b)
+          B[b] = *reinterpret_cast<const f32x4 *>(sC + (16 * NPB * wave + 16 * b + jj) * SP +
+                                                  16 * h + 4 * kr);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+          for (int m = 0; m < NCB; ++m)
+#pragma unroll
+            for (int b = 0; b < NPB; ++b) acc[m][b] = mfma16x16x4(A[m][s4], B[b][s4], acc[m][b]);
+      }
     }
-    for (int c0 = cbeg; c0 < cend;) {
-      const int g = MODE ? c0 / cpg : 0;
-      const int c1 = MODE ? min(min(c0 + KC, (g + 1) * cpg), cend) : min(c0 + KC, cend);
-      const int rows = c1 - c0;
-      if (MODE) {
-        Samp2 s;
-        pixel_samp2(s, a, n, g, k, pvalid ? p : 0, ho, wo);
-#pragma unroll
-        for (int ii = 0; ii < KC / 4; ++ii) {
-          const int cl = wave + 4 * ii;
-          float v = 0.f;
-          if (cl < rows && pvalid) v = samp_val2(xn + (long)(c0 + cl) * HW, s);
-          sCol[cl * CP + lane] = v;
-        }
-      } else {
-#pragma unroll
-        for (int ii = 0; ii < KC / 4; ++ii) {
-          const int cl = wave + 4 * ii;
-          float v = 0.f;
-          if (cl < rows) {
-            const float t = xn[(long)(c0 + cl) * HW + sp.idx];
-            v = sp.ok ? t : 0.f;
-          }
-          sCol[cl * CP + lane] = v;
-        }
-      }
-      for (int e = tid; e < KC * CO_T; e += NT) {
-        const int cl = e % KC, col = e / KC;
-        const int co = co0 + col;
-        float v = 0.f;
-        if (cl < rows && co < co_end) v = a.weight[((long)co * Cg + (c0 + cl - cbeg)) * K + k];
-        sW[col * WP + cl] = v;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int ks = 0; ks < KC / 4; ++ks) {
-        const float bv = sCol[(4 * ks + kr) * CP + 16 * wave + jj];
-#pragma unroll
-        for (int m = 0; m < NCB; ++m) {
-          const float av = sW[(16 * m + jj) * WP + 4 * ks + kr];
-          acc[m] = mfma16x16x4(av, bv, acc[m]);
-        }
-      }
-      __syncthreads();
-      c0 = c1;
-    }
+    if (!has_next) break;
+    store_stage(nxt, buf ^ 1);
+    if (MODE && has_nn) finish_params(nn);
+    __syncthreads();
+    nxt = nn;
+    has_next = has_nn;
   }
 
-  // Epilogue: lane holds pixel column jj, output channels 16m + 4kr + r.
-  const long pe = (long)tile * PT + 16 * wave + jj;
-  if (pe < P) {
+  // Epilogue: lane holds pixel column jj of block b, output channels 16m + 4kr + r.
+#pragma unroll
+  for (int b = 0; b < NPB; ++b) {
+    const long pe = (long)tile * PTT + 16 * NPB * wave + 16 * b + jj;
+    if (pe >= P) continue;
 #pragma unroll
     for (int m = 0; m < NCB; ++m)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + 16 * m + 4 * kr + r;
         if (co < co_end) {
-          float v = acc[m][r];
+          float v = acc[m][b][r];
           if (a.bias) v += a.bias[co];
           if (a.post_scale) v = v * a.post_scale[co] + a.post_shift[co];
           const long o = ((long)n * a.Co + co) * P + pe;
@@ -568,8 +699,16 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
   return a;
 }
 
+template <int MODE, int CO_T, int PTT>
+void launch_fwd_t(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
+  if (packed)
+    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1>), grid, dim3(NT), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 0>), grid, dim3(NT), 0, st, a);
+}
+
 template <int MODE>
-int launch_fwd(const MdcnArgs &a, hipStream_t st) {
+int launch_fwd(const MdcnArgs &a, int packed, hipStream_t st) {
   const int rc = check_shapes(a);
   if (rc) return rc;
   if (!a.x || !a.weight || !a.out) return AANET_EINVAL;
@@ -580,13 +719,35 @@ int launch_fwd(const MdcnArgs &a, hipStream_t st) {
   const int Cog = a.Co / a.groups;
   const int co_t = Cog <= 16 ? 16 : (Cog <= 32 ? 32 : 64);
   const int ncot = host_div_up(Cog, co_t);
-  dim3 grid((unsigned)(a.N * host_div_up(P, PT)), (unsigned)(a.groups * ncot));
-  switch (co_t) {
-    case 16: hipLaunchKernelGGL((conv_fwd_kernel<MODE, 16>), grid, dim3(NT), 0, st, a); break;
-    case 32: hipLaunchKernelGGL((conv_fwd_kernel<MODE, 32>), grid, dim3(NT), 0, st, a); break;
-    default: hipLaunchKernelGGL((conv_fwd_kernel<MODE, 64>), grid, dim3(NT), 0, st, a); break;
+  // 128-pixel tiles when they still give >= 4 workgroups per CU, else 64
+  const int ptt = (long)a.N * host_div_up(P, 128) * a.groups * ncot >= 1024 ? 128 : 64;
+  dim3 grid((unsigned)(a.N * host_div_up(P, ptt)), (unsigned)(a.groups * ncot));
+  if (ptt == 128) {
+    switch (co_t) {
+      case 16: launch_fwd_t<MODE, 16, 128>(a, packed, grid, st); break;
+      case 32: launch_fwd_t<MODE, 32, 128>(a, packed, grid, st); break;
+      default: launch_fwd_t<MODE, 64, 128>(a, packed, grid, st); break;
+    }
+  } else {
+    switch (co_t) {
+      case 16: launch_fwd_t<MODE, 16, 64>(a, packed, grid, st); break;
+      case 32: launch_fwd_t<MODE, 32, 64>(a, packed, grid, st); break;
+      default: launch_fwd_t<MODE, 64, 64>(a, packed, grid, st); break;
+    }
   }
   return aanet_launch_status();
+}
+
+__global__ void pack_weight_kernel(const float *__restrict__ w, float *__restrict__ wp, int Co,
+                                   int Cg, int K) {
+  const long total = (long)Co * Cg * K;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long)gridDim.x * blockDim.x) {
+    const int k = (int)(e % K);
+    const long t = e / K;
+    const int c = (int)(t % Cg), co = (int)(t / Cg);
+    wp[((long)k * Co + co) * Cg + c] = w[e];
+  }
 }
 
 int round_pitch(int v, int mod32) {  // smallest p >= v with p % 32 == mod32
@@ -603,25 +764,26 @@ extern "C" int aanet_mdcn_fwd_f32(const float *x, const float *offset, const flo
                                   int dil, int groups, int dg, aanet_stream_t stream) {
   MdcnArgs a = make_args(x, offset, -1, mask, -1, 0, 1.f, weight, bias, nullptr, nullptr, 0, out,
                          n, c, h, w, co, kh, kw, stride, pad, dil, groups, dg);
-  return launch_fwd<1>(a, as_hip(stream));
+  return launch_fwd<1>(a, 0, as_hip(stream));
 }
 
 extern "C" int aanet_conv2d_fused_f32(const float *x, const float *weight, const float *bias,
                                       const float *post_scale, const float *post_shift,
-                                      const float *residual, int act, float *out, int n, int c,
-                                      int h, int w, int co, int kh, int kw, int stride, int pad,
-                                      int dil, int groups, aanet_stream_t stream) {
+                                      const float *residual, int act, int weight_packed,
+                                      float *out, int n, int c, int h, int w, int co, int kh,
+                                      int kw, int stride, int pad, int dil, int groups,
+                                      aanet_stream_t stream) {
   if (act < 0 || act > 2) return AANET_EINVAL;
   MdcnArgs a = make_args(x, nullptr, 0, nullptr, 0, 0, 1.f, weight, bias, post_scale, post_shift,
                          act, out, n, c, h, w, co, kh, kw, stride, pad, dil, groups, 1);
   a.residual = residual;
-  return launch_fwd<0>(a, as_hip(stream));
+  return launch_fwd<0>(a, weight_packed, as_hip(stream));
 }
 
 extern "C" int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset,
                                         long offset_batch_stride, const float *mask,
                                         long mask_batch_stride, int mask_logits, float mask_scale,
-                                        const float *weight, const float *bias,
+                                        const float *weight, int weight_packed, const float *bias,
                                         const float *post_scale, const float *post_shift, int act,
                                         float *out, int n, int c, int h, int w, int co, int kh,
                                         int kw, int stride, int pad, int dil, int groups, int dg,
@@ -630,7 +792,16 @@ extern "C" int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset,
   MdcnArgs a = make_args(x, offset, offset_batch_stride, mask, mask_batch_stride, mask_logits,
                          mask_scale, weight, bias, post_scale, post_shift, act, out, n, c, h, w,
                          co, kh, kw, stride, pad, dil, groups, dg);
-  return launch_fwd<1>(a, as_hip(stream));
+  return launch_fwd<1>(a, weight_packed, as_hip(stream));
+}
+
+extern "C" int aanet_conv_weight_pack_f32(const float *weight, float *weight_packed, int co,
+                                          int cg, int kh, int kw, aanet_stream_t stream) {
+  AANET_HOST_CHECK(weight && weight_packed && co > 0 && cg > 0 && kh > 0 && kw > 0);
+  const long total = (long)co * cg * kh * kw;
+  hipLaunchKernelGGL(pack_weight_kernel, dim3(host_div_up(total, 256) > 4096 ? 4096 : host_div_up(total, 256)),
+                     dim3(256), 0, as_hip(stream), weight, weight_packed, co, cg, kh * kw);
+  return aanet_launch_status();
 }
 
 extern "C" int aanet_mdcn_im2col_f32(const float *x, const float *offset, const float *mask,

@@ -21,13 +21,14 @@ def _key(*tensors):
 
 
 def folded(conv, bn):
-    """(weight, bias) of conv followed by eval BN (bn may be None), cached on the conv module."""
+    """(weight, bias, packed weight) of conv followed by eval BN (bn may be None), cached on the
+    conv module; the packed copy is the [kh][kw][co][cg] layout the HIP engine streams."""
     tensors = (conv.weight, conv.bias) + ((bn.weight, bn.bias, bn.running_mean, bn.running_var)
                                           if bn is not None else ())
     key = _key(*tensors)
     cache = getattr(conv, "_aanet_fold", None)
     if cache is not None and cache[0] == key:
-        return cache[1], cache[2]
+        return cache[1], cache[2], cache[3]
     with torch.no_grad():
         if bn is None:
             w = conv.weight.contiguous()
@@ -37,8 +38,9 @@ def folded(conv, bn):
             w = (conv.weight * scale.view(-1, 1, 1, 1)).contiguous()
             b = shift if conv.bias is None else conv.bias * scale + shift
             b = b.contiguous()
-    conv._aanet_fold = (key, w, b)
-    return w, b
+    wp = ops.pack_weight(w) if w.is_cuda else None
+    conv._aanet_fold = (key, w, b, wp)
+    return w, b, wp
 
 
 def bn_affine(bn):
@@ -60,12 +62,12 @@ def _int(v):
 
 def conv_bn_act(x, conv, bn=None, act=None, residual=None):
     """act(BN(conv(x)) [+ residual]) as ONE HIP kernel (BN folded into the conv)."""
-    w, b = folded(conv, bn)
+    w, b, wp = folded(conv, bn)
     for v in (conv.stride, conv.padding, conv.dilation):
         if isinstance(v, (tuple, list)) and v[0] != v[1]:
             raise NotImplementedError("asymmetric conv parameters")
     return ops.conv2d_fused(x.contiguous(), w, b, _int(conv.stride), _int(conv.padding),
-                            _int(conv.dilation), conv.groups, act, residual)
+                            _int(conv.dilation), conv.groups, act, residual, packed_weight=wp)
 
 
 def use_fused(module, x):

@@ -15,7 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from ._fuse import bn_affine, conv_bn_act, use_fused
+from ._fuse import bn_affine, conv_bn_act, folded, use_fused
 from .deform_conv import DeformConv, ModulatedDeformConv
 
 
@@ -78,10 +78,11 @@ class DeformConv2d(nn.Module):
         dc = self.deform_conv
         offset_mask = conv_bn_act(x, self.offset_conv)
         ps, psh = bn_affine(bn) if bn is not None else (None, None)
+        _, _, wp = folded(dc, None)
         return ops.mdcn_forward_fused(x.contiguous(), offset_mask.contiguous(), dc.weight,
                                       dc.bias, ps, psh, act, dc.stride, dc.padding, dc.dilation,
                                       self.deformable_groups,
-                                      2.0 if self.double_mask else 1.0)
+                                      2.0 if self.double_mask else 1.0, packed_weight=wp)
 
 
 class _BottleneckBase(nn.Module):

@@ -130,14 +130,15 @@ def mdcn_forward(x, offset, mask, weight, bias=None, stride=1, padding=0, dilati
 
 
 def mdcn_forward_fused(x, offset_mask, weight, bias=None, post_scale=None, post_shift=None, act=None,
-                       stride=1, padding=0, dilation=1, deformable_groups=1, mask_scale=2.0):
+                       stride=1, padding=0, dilation=1, deformable_groups=1, mask_scale=2.0,
+                       packed_weight=None):
     """Eval fast path of DeformConv2d (nets/deform.py:78-97) + BN + activation.
 
     offset_mask is the raw offset_conv output [N, dg*3*K, Ho, Wo]: channels [0, 2*dg*K) are
     offsets, the rest mask logits (m = mask_scale * sigmoid), read in place (no slicing copies).
     """
-    require_gpu(x, offset_mask, weight, bias, post_scale, post_shift,
-                names=("input", "offset_mask", "weight", "bias", "post_scale", "post_shift"))
+    require_gpu(x, offset_mask, weight, bias, post_scale, post_shift, packed_weight,
+                names=("input", "offset_mask", "weight", "bias", "post_scale", "post_shift", "packed"))
     N, C, H, W = x.shape
     Co, _, kh, kw = weight.shape
     K = kh * kw
@@ -147,8 +148,10 @@ def mdcn_forward_fused(x, offset_mask, weight, bias=None, post_scale=None, post_
     out = torch.empty((N, Co, Ho, Wo), device=x.device, dtype=x.dtype)
     bs = offset_mask.stride(0)
     mask_ptr = offset_mask.data_ptr() + 4 * deformable_groups * 2 * K * Ho * Wo
+    wsrc = packed_weight if packed_weight is not None else weight
     call("aanet_mdcn_fwd_fused_f32", ptr(x), ptr(offset_mask), bs, _lib.ctypes.c_void_p(mask_ptr),
-         bs, 1, float(mask_scale), ptr(weight), ptr(bias), ptr(post_scale), ptr(post_shift),
+         bs, 1, float(mask_scale), ptr(wsrc), int(packed_weight is not None), ptr(bias),
+         ptr(post_scale), ptr(post_shift),
          ACT[act] if not isinstance(act, int) else act, ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation, 1,
          deformable_groups, stream_of(x))
     return out
@@ -157,20 +160,32 @@ def mdcn_forward_fused(x, offset_mask, weight, bias=None, post_scale=None, post_
 ACT = {None: 0, "relu": 1, "leaky": 2}
 
 
+def pack_weight(weight):
+    """[co][cg][kh][kw] -> [kh][kw][co][cg] (aanet_conv_weight_pack_f32)."""
+    require_gpu(weight, names=("weight",))
+    Co, Cg, kh, kw = weight.shape
+    out = torch.empty((kh, kw, Co, Cg), device=weight.device, dtype=weight.dtype)
+    call("aanet_conv_weight_pack_f32", ptr(weight), ptr(out), Co, Cg, kh, kw, stream_of(weight))
+    return out
+
+
 def conv2d_fused(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None,
-                 residual=None, post_scale=None, post_shift=None):
-    """Plain conv on the HIP implicit-GEMM engine: act(post_scale*(conv+bias)+post_shift+residual)."""
-    require_gpu(x, weight, bias, residual, post_scale, post_shift,
-                names=("input", "weight", "bias", "residual", "post_scale", "post_shift"))
+                 residual=None, post_scale=None, post_shift=None, packed_weight=None):
+    """Plain conv on the HIP implicit-GEMM engine: act(post_scale*(conv+bias)+post_shift+residual).
+    weight gives the shape ([co][cg][kh][kw]); packed_weight (pack_weight(weight)) if given is
+    what the kernel reads."""
+    require_gpu(x, weight, bias, residual, post_scale, post_shift, packed_weight,
+                names=("input", "weight", "bias", "residual", "post_scale", "post_shift", "packed"))
     N, C, H, W = x.shape
     Co, _, kh, kw = weight.shape
     Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
     if residual is not None and tuple(residual.shape) != (N, Co, Ho, Wo):
         raise ValueError("residual shape must match the output")
     out = torch.empty((N, Co, Ho, Wo), device=x.device, dtype=x.dtype)
-    call("aanet_conv2d_fused_f32", ptr(x), ptr(weight), ptr(bias), ptr(post_scale), ptr(post_shift),
-         ptr(residual), ACT[act], ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation,
-         groups, stream_of(x))
+    wsrc = packed_weight if packed_weight is not None else weight
+    call("aanet_conv2d_fused_f32", ptr(x), ptr(wsrc), ptr(bias), ptr(post_scale), ptr(post_shift),
+         ptr(residual), ACT[act], int(packed_weight is not None), ptr(out), N, C, H, W, Co, kh, kw,
+         stride, padding, dilation, groups, stream_of(x))
     return out
 
 

@@ -90,7 +90,7 @@ def time_events(fn, iters, stream):
 def kernel_rooflines(model, left, right, batch, iters):
     """Per-kernel average duration (HIP events on the launch stream) and roofline fractions."""
     from aanet_amd import ops
-    from aanet_amd.nets._fuse import bn_affine, conv_bn_act
+    from aanet_amd.nets._fuse import bn_affine, conv_bn_act, folded
     stream = torch.cuda.current_stream()
     res = {}
     # correlation, scale 0 (one launch): algorithmic bytes = read L,R once + write volume
@@ -112,7 +112,9 @@ def kernel_rooflines(model, left, right, batch, iters):
         om = blk.conv2.offset_conv(x1)
         ps, psh = bn_affine(blk.bn2)
         w = blk.conv2.deform_conv.weight
-        fn = lambda: ops.mdcn_forward_fused(x1, om, w, None, ps, psh, 1, 1, 2, 2, 2, 2.0)  # noqa: E731
+        wp = folded(blk.conv2.deform_conv, None)[2]
+        fn = lambda: ops.mdcn_forward_fused(x1, om, w, None, ps, psh, 1, 1, 2, 2, 2, 2.0,  # noqa: E731
+                                            packed_weight=wp)
         ms = time_events(fn, iters, stream)
     Co, Ci = w.shape[:2]
     flops = 2.0 * B * H * W * Co * Ci * 9

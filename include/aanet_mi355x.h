@@ -91,10 +91,13 @@ int aanet_mdcn_fwd_f32(const float *x, const float *offset, const float *mask, c
  *   - mask_logits != 0: the mask pointer holds pre-sigmoid logits, m = mask_scale*sigmoid(l)
  *     (deform.py:86-89 with double_mask => mask_scale = 2);
  *   - epilogue: y = act(post_scale[co] * (conv + bias[co]) + post_shift[co]); act 0 none,
- *     1 ReLU, 2 LeakyReLU(0.2).  post_scale / post_shift may be NULL (identity). */
+ *     1 ReLU, 2 LeakyReLU(0.2).  post_scale / post_shift may be NULL (identity);
+ *   - weight_packed != 0: weight is in the [kh][kw][co][c/groups] layout produced by
+ *     aanet_conv_weight_pack_f32 (coalesced K-chunk loads); 0: reference [co][c/groups][kh][kw]. */
 int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset, long offset_batch_stride,
                              const float *mask, long mask_batch_stride, int mask_logits,
-                             float mask_scale, const float *weight, const float *bias,
+                             float mask_scale, const float *weight, int weight_packed,
+                             const float *bias,
                              const float *post_scale, const float *post_shift, int act, float *out,
                              int n, int c, int h, int w, int co, int kh, int kw, int stride,
                              int pad, int dil, int groups, int dg, aanet_stream_t stream);
@@ -107,8 +110,14 @@ int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset, long offset_ba
  * 1 ReLU, 2 LeakyReLU(0.2).  bias / post_* / residual may be NULL; residual has out's shape. */
 int aanet_conv2d_fused_f32(const float *x, const float *weight, const float *bias,
                            const float *post_scale, const float *post_shift, const float *residual,
-                           int act, float *out, int n, int c, int h, int w, int co, int kh, int kw,
-                           int stride, int pad, int dil, int groups, aanet_stream_t stream);
+                           int act, int weight_packed, float *out, int n, int c, int h, int w,
+                           int co, int kh, int kw, int stride, int pad, int dil, int groups,
+                           aanet_stream_t stream);
+
+/* Weight repack for the conv engine: [co][cg][kh][kw] -> [kh][kw][co][cg].  Done once per
+ * weight version by the caller (the eval path caches it with the folded BN). */
+int aanet_conv_weight_pack_f32(const float *weight, float *weight_packed, int co, int cg, int kh,
+                               int kw, aanet_stream_t stream);
 
 /* Cross-scale fusion sum (nets/aggregation.py:387-400): out[n,c,h,w] =
  * act(sum_j resize(inputs[j])), j in input order; inputs whose (in_h, in_w) differ from

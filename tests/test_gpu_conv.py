@@ -27,7 +27,8 @@ CONV_CASES = [
 
 @pytest.mark.parametrize("case", CONV_CASES)
 @pytest.mark.parametrize("epi", ["plain", "bias_relu", "bn_leaky_res"])
-def test_conv2d_fused_vs_torch_cpu(case, epi):
+@pytest.mark.parametrize("packed", [False, True])
+def test_conv2d_fused_vs_torch_cpu(case, epi, packed):
     N, C, H, W, Co, k, s, p, d, g = case
     gen = torch.Generator().manual_seed(hash(case) % 1000)
     x = torch.randn(N, C, H, W, generator=gen)
@@ -43,10 +44,12 @@ def test_conv2d_fused_vs_torch_cpu(case, epi):
     elif epi == "bias_relu":
         ref = F.relu(ref)
     act = {"plain": None, "bias_relu": "relu", "bn_leaky_res": "leaky"}[epi]
-    got = ops.conv2d_fused(x.to(DEV), w.to(DEV), None if epi == "plain" else b.to(DEV), s, p, d, g,
+    wd = w.to(DEV)
+    got = ops.conv2d_fused(x.to(DEV), wd, None if epi == "plain" else b.to(DEV), s, p, d, g,
                            act, None if res is None else res.to(DEV),
                            sc.to(DEV) if epi == "bn_leaky_res" else None,
-                           sh.to(DEV) if epi == "bn_leaky_res" else None).cpu()
+                           sh.to(DEV) if epi == "bn_leaky_res" else None,
+                           packed_weight=ops.pack_weight(wd) if packed else None).cpu()
     err = (got - ref).abs().max().item()
     assert err <= 2e-5 * (1 + ref.abs().max().item()), err
 

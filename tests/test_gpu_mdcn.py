@@ -102,7 +102,9 @@ def test_mdcn_fused_eval_path_vs_oracle():
     w = (rng.standard_normal((C, C, 3, 3)) / 24).astype(np.float32)
     sc = rng.uniform(0.5, 1.5, C).astype(np.float32)
     sh = rng.standard_normal(C).astype(np.float32)
-    out = ops.mdcn_forward_fused(g2t(x), g2t(om), g2t(w), None, g2t(sc), g2t(sh), 1, 1, 2, 2, dg, 2.0)
+    wt = g2t(w)
+    out = ops.mdcn_forward_fused(g2t(x), g2t(om), wt, None, g2t(sc), g2t(sh), 1, 1, 2, 2, dg, 2.0,
+                                 packed_weight=ops.pack_weight(wt))
     mask = 2.0 / (1.0 + np.exp(-om[:, dg * 18:].astype(np.float64)))
     ref = oracle.mdcn_forward(x, om[:, :dg * 18], mask.astype(np.float32), w, None, 1, 2, 2, 1, dg)
     ref = np.maximum(ref * sc[None, :, None, None] + sh[None, :, None, None], 0)
