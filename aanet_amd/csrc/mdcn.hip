@@ -181,42 +181,82 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 // blocks: 1x1, 3x3, dilated, grouped, strided).
 //
 // Workgroup = 256 threads, output tile CO_T channels x PTT pixels of one image.  The K
-// dimension is walked in chunks of (tap k, <= 32 input channels of one deformable group):
-//   stage   : each thread builds PTT*32/256 im2col values of the chunk for ONE pixel (sampling
-//             state computed once per (pixel, tap, group)) -> LDS [pixel][channel];
-//             the weight slice -> LDS [co][channel];
-//   contract: wave w owns CO_T x (PTT/4) outputs; per 16 channels it reads one ds_read_b128 per
-//             16-row operand block and issues 4 k-steps of v_mfma_f32_16x16x4_f32 -- the
-//             reduction index is permuted (lane group kr takes channels 4kr..4kr+3) identically
-//             for both operands, so the sum is unchanged.
-// Software pipeline: LDS is double buffered; while the MFMAs of chunk c run, the global loads
-// of chunk c+1 are in flight in registers and the offsets/mask of chunk c+2 are being fetched;
-// one barrier per chunk.
-// Epilogue: y = act(post_scale*(acc + bias) + post_shift + residual).
+// dimension is walked in chunks of (<= 32 input channels of one deformable group, tap k),
+// taps innermost so a chunk's 32 channel planes stay L2-resident across its 9 taps:
+//   stage   : each thread builds PTT*32/256 im2col values of the chunk for ONE pixel -> LDS
+//             [pixel][channel]; the sampling state of a (pixel, tap, group) is computed once.
+//             Gathers are buffer loads: per-lane 32-bit offset (the tap position) + wave-uniform
+//             SGPR offset (the channel plane), so a gather costs no address VALU; the plain
+//             conv's zero padding comes from the buffer range check (offset past the image).
+//             The weight slice -> LDS [co][channel].
+//   contract: wave w owns CO_T x (PTT/4) outputs; per 16 channels one ds_read_b128 per 16-row
+//             operand block, then 4 k-steps of v_mfma_f32_16x16x4_f32 -- the reduction index
+//             is permuted (lane group kr takes channels 4kr..4kr+3) identically for both operands.
+// Software pipeline: LDS double buffer; while the MFMAs of chunk c run, the global loads of
+// chunk c+1 are in flight in registers and the offsets/mask of chunk c+2 are being fetched;
+// one barrier per chunk.  Blocks are remapped so each XCD gets a contiguous range of tiles
+// (neighbouring tiles share input rows -> same L2).
+// Epilogue: the tile is transposed through LDS and written as 16-byte row segments:
+// y = act(post_scale*(acc + bias) + post_shift + residual).
 // grid: x = N * ceil(P/PTT), y = groups * ceil(Cog/CO_T).
-constexpr int SP = 40;  // LDS row pitch (floats) of both tiles: conflict-free ds_read_b128
+constexpr int SP = 40;  // LDS row pitch (floats) of both staging tiles: conflict-free b128 reads
+
+typedef int i2v __attribute__((ext_vector_type(2)));
 
 struct ChunkIt {
   int k, c0, c1;
-  __device__ __forceinline__ void first(int cbeg, int cend, int cpg, int mode) {
-    k = 0;
-    c0 = cbeg;
-    c1 = next_end(cbeg, cend, cpg, mode);
-  }
   __device__ __forceinline__ static int next_end(int c0, int cend, int cpg, int mode) {
     int e = min(c0 + KC, cend);
     if (mode) e = min(e, (c0 / cpg + 1) * cpg);
     return e;
   }
-  __device__ __forceinline__ void advance(int cbeg, int cend, int cpg, int mode) {
-    c0 = c1;
-    if (c0 >= cend) {
-      c0 = cbeg;
-      ++k;
+  __device__ __forceinline__ void first(int cbeg, int cend, int cpg, int mode) {
+    k = 0;
+    c0 = cbeg;
+    c1 = next_end(cbeg, cend, cpg, mode);
+  }
+  __device__ __forceinline__ void advance(int K, int cend, int cpg, int mode) {
+    if (++k == K) {
+      k = 0;
+      c0 = c1;
+      c1 = next_end(c0, cend, cpg, mode);
     }
-    c1 = next_end(c0, cend, cpg, mode);
   }
 };
+
+// Pair-gather sampling state with the corner selection folded into the weights:
+// val = (wa_t*t.x + wb_t*t.y) + wa_b*b.x + wb_b*b.y equals kernel.cu:494-496 bit for bit
+// (terms that the reference adds as w*0 are exact zeros here too).
+struct SampW {
+  int ot, ob;  // byte offsets of the 2-wide pairs in rows hl, hl+1
+  float wat, wbt, wab, wbb, m;
+};
+
+__device__ __forceinline__ void make_sampw(SampW &s, float h, float w, int H, int W, float m) {
+#pragma clang fp contract(off)
+  const bool valid = h > -1.f && w > -1.f && h < (float)H && w < (float)W;
+  const int hl = (int)floorf(h), wl = (int)floorf(w);
+  const float lh = h - (float)hl, lw = w - (float)wl;
+  const float hh = 1.f - lh, hw = 1.f - lw;
+  const bool ok1 = valid && hl >= 0 && wl >= 0;
+  const bool ok2 = valid && hl >= 0 && wl + 1 <= W - 1;
+  const bool ok3 = valid && hl + 1 <= H - 1 && wl >= 0;
+  const bool ok4 = valid && hl + 1 <= H - 1 && wl + 1 <= W - 1;
+  const float w1 = ok1 ? hh * hw : 0.f, w2 = ok2 ? hh * lw : 0.f;
+  const float w3 = ok3 ? lh * hw : 0.f, w4 = ok4 ? lh * lw : 0.f;
+  const int pb = valid ? min(max(wl, 0), W - 2) : 0;
+  const int rt = valid ? min(max(hl, 0), H - 1) : 0;
+  const int rb = valid ? min(max(hl + 1, 0), H - 1) : 0;
+  s.ot = (rt * W + pb) * 4;
+  s.ob = (rb * W + pb) * 4;
+  const bool swap = valid && pb != wl;  // wl == -1: pair = (wl+1, wl+2); wl == W-1: (wl-1, wl)
+  const bool left = wl < pb;             // wl == -1
+  s.wat = swap ? (left ? w2 : 0.f) : w1;
+  s.wbt = swap ? (left ? 0.f : w1) : w2;
+  s.wab = swap ? (left ? w4 : 0.f) : w3;
+  s.wbb = swap ? (left ? 0.f : w3) : w4;
+  s.m = m;
+}
 
 template <int MODE, int CO_T, int PTT, int PACKED>
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
@@ -225,84 +265,104 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
   constexpr int CPT = KC * PTT / NT;     // im2col values staged per thread per chunk
   constexpr int WPT = KC * CO_T / NT;    // weights staged per thread per chunk
   constexpr int BUF = (PTT + CO_T) * SP; // floats per LDS buffer
+  constexpr int OP = PTT + 4;            // epilogue tile pitch
+  static_assert(CO_T * OP <= 2 * BUF, "epilogue tile must fit the staging buffers");
   __shared__ __attribute__((aligned(16))) float smem[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long P = (long)a.Ho * a.Wo;
   const int ntiles = (int)((P + PTT - 1) / PTT);
-  const int n = blockIdx.x / ntiles, tile = blockIdx.x % ntiles;
+  // XCD-aware remap of the pixel-tile index (bijective for any grid size)
+  const int nwg = gridDim.x, b0 = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b0 & 7;
+  const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b0 >> 3);
+  const int n = bid / ntiles, tile = bid % ntiles;
   const int Cg = a.C / a.groups, Cog = a.Co / a.groups, K = a.kh * a.kw, cpg = a.C / a.dg;
   const int ncot = (Cog + CO_T - 1) / CO_T;
   const int gc = blockIdx.y / ncot, cot = blockIdx.y % ncot;
   const int co0 = gc * Cog + cot * CO_T, co_end = min(co0 + CO_T, (gc + 1) * Cog);
   const int cbeg = gc * Cg, cend = (gc + 1) * Cg;
   const long HW = (long)a.H * a.W;
-  const float *xn = a.x + (long)n * a.C * HW;
+  const int img_bytes = (int)(a.C * HW * 4);
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void *)(a.x + (long)n * a.C * HW), (short)0,
+                                                     img_bytes, 0x00020000);
+  const int plane_bytes = (int)(HW * 4);
 
-  // staging role: one pixel, CPT consecutive channels of the chunk
-  const int spx = tid % PTT, scb = (tid / PTT) * CPT;
+  // staging role: one pixel, CPT consecutive channels of the chunk (wave-uniform base)
+  const int spx = tid % PTT;
+  const int scb = __builtin_amdgcn_readfirstlane((tid / PTT) * CPT);
   const long p = (long)tile * PTT + spx;
   const bool pvalid = p < P;
   const int ho = pvalid ? (int)(p / a.Wo) : 0, wo = pvalid ? (int)(p % a.Wo) : 0;
   const long psafe = pvalid ? p : 0;
 
-  const int nchunks = K * ((cend - cbeg) + 0);  // upper bound helper (not used directly)
-  (void)nchunks;
-
-  // ---- register staging buffers
   float wreg[WPT];
-  float vraw[CPT];              // plain: loaded values
-  f2u traw[MODE ? CPT : 1], braw[MODE ? CPT : 1];
-  Samp2 snext;                  // sampling state of the chunk being loaded (MODE 1)
+  float vraw[MODE ? 1 : CPT];
+  i2v traw[MODE ? CPT : 1], braw[MODE ? CPT : 1];
+  SampW snext;                                 // sampling state of the chunk being loaded
   float off_h = 0.f, off_w = 0.f, mlog = 0.f;  // raw offsets/mask of the chunk after it
-  int sp_ok = 0, sp_idx = 0;
 
-  auto load_params_raw = [&](const ChunkIt &c) {  // MODE 1: issue offset / mask loads
+  // offsets / mask / weights through buffer descriptors too: per-lane part fixed for the whole
+  // kernel, chunk-dependent part in an SGPR.
+  const auto offr = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)(MODE ? a.offset + (long)n * a.off_bs : a.x), (short)0, 0x7ffffff0, 0x00020000);
+  const auto mskr = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)(MODE ? a.mask + (long)n * a.mask_bs : a.x), (short)0, 0x7ffffff0, 0x00020000);
+  const int w_bytes = (int)((long)a.Co * Cg * K * 4);
+  const auto wr = __builtin_amdgcn_make_buffer_rsrc((void *)a.weight, (short)0, w_bytes, 0x00020000);
+  int wlane[WPT];  // per-lane weight byte offsets (chunk-invariant)
+#pragma unroll
+  for (int i = 0; i < WPT; ++i) {
+    const int e = tid + NT * i, co = e / KC, cl = e % KC;
+    // rows past the chunk read a neighbouring channel (multiplied by a zero im2col value);
+    // reads past the tensor are out of range -> 0; co past co_end is never stored
+    wlane[i] = PACKED ? (co * Cg + cl) * 4 : (co * Cg * K + cl * K) * 4;
+  }
+  const int pl4 = (int)psafe * 4;
+
+  auto load_params_raw = [&](const ChunkIt &c) {
     const int g = c.c0 / cpg;
-    const float *off = a.offset + (long)n * a.off_bs + (long)g * 2 * K * P;
-    off_h = off[(long)(2 * c.k) * P + psafe];
-    off_w = off[(long)(2 * c.k + 1) * P + psafe];
-    mlog = a.mask[(long)n * a.mask_bs + ((long)g * K + c.k) * P + psafe];
+    const int ob = (int)(((long)g * 2 * K + 2 * c.k) * P * 4);
+    off_h = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, pl4, ob, 0));
+    off_w = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, pl4, ob + (int)(P * 4), 0));
+    mlog = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                         mskr, pl4, (int)(((long)g * K + c.k) * P * 4), 0));
   };
-  auto finish_params = [&](const ChunkIt &c) {  // MODE 1: coordinates from the raw loads
+  auto finish_params = [&](const ChunkIt &c) {
 #pragma clang fp contract(off)
     const int i = c.k / a.kw, j = c.k % a.kw;
-    const float m = a.mask_logits ? a.mask_scale * (1.f / (1.f + expf(-mlog))) : mlog;
+    float m = a.mask_logits ? a.mask_scale * (1.f / (1.f + expf(-mlog))) : mlog;
     const float h = (float)(ho * a.stride - a.pad + i * a.dil) + off_h;
     const float w = (float)(wo * a.stride - a.pad + j * a.dil) + off_w;
-    make_samp2(snext, h, w, a.H, a.W, m);
+    make_sampw(snext, h, w, a.H, a.W, m);
+    if (!pvalid) snext.m = 0.f;
   };
   auto issue_loads = [&](const ChunkIt &c) {
     const int rows = c.c1 - c.c0;
+    const int wbase = PACKED ? (((c.k * a.Co + co0) * Cg + (c.c0 - cbeg)) * 4)
+                             : (((co0 * Cg + (c.c0 - cbeg)) * K + c.k) * 4);
 #pragma unroll
-    for (int i = 0; i < WPT; ++i) {
-      const int e = tid + NT * i, co = e / KC, cl = e % KC;
-      const int cog = co0 + co;
-      float v = 0.f;
-      if (cl < rows && cog < co_end) {
-        const int cc = c.c0 + cl - cbeg;
-        v = PACKED ? a.weight[((long)c.k * a.Co + cog) * Cg + cc]
-                   : a.weight[((long)cog * Cg + cc) * K + c.k];
-      }
-      wreg[i] = v;
-    }
+    for (int i = 0; i < WPT; ++i)
+      wreg[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, wlane[i], wbase, 0));
+    const int cbase = __builtin_amdgcn_readfirstlane((c.c0 + scb) * plane_bytes);
     if (MODE == 0) {
       const int hi = ho * a.stride - a.pad + (c.k / a.kw) * a.dil;
       const int wi = wo * a.stride - a.pad + (c.k % a.kw) * a.dil;
-      sp_ok = pvalid && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
-      sp_idx = sp_ok ? hi * a.W + wi : 0;
+      const bool ok = pvalid && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+      const int voff = ok ? (hi * a.W + wi) * 4 : img_bytes;  // past the end -> reads 0
 #pragma unroll
       for (int e = 0; e < CPT; ++e) {
-        const int cl = scb + e;
-        vraw[e] = cl < rows ? xn[(long)(c.c0 + cl) * HW + sp_idx] : 0.f;
+        const int soff = cbase + e * plane_bytes;
+        vraw[e] = (scb + e < rows)
+                      ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, voff, soff, 0))
+                      : 0.f;
       }
     } else {
 #pragma unroll
       for (int e = 0; e < CPT; ++e) {
-        const int cl = min(scb + e, rows - 1);
-        const float *im = xn + (long)(c.c0 + cl) * HW;
-        traw[e] = *reinterpret_cast<const f2u *>(im + snext.itop);
-        braw[e] = *reinterpret_cast<const f2u *>(im + snext.ibot);
+        const int soff = cbase + min(e, rows - 1 - scb) * plane_bytes;
+        traw[e] = __builtin_amdgcn_raw_buffer_load_b64(xr, snext.ot, soff, 0);
+        braw[e] = __builtin_amdgcn_raw_buffer_load_b64(xr, snext.ob, soff, 0);
       }
     }
   };
@@ -318,14 +378,13 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
 #pragma unroll
     for (int e = 0; e < CPT; ++e) {
       if (MODE == 0) {
-        v[e] = sp_ok ? vraw[e] : 0.f;
+        v[e] = vraw[e];
       } else {
 #pragma clang fp contract(off)
-        const Samp2 &s = snext;
-        const float v1 = s.swap ? traw[e].y : traw[e].x, v2 = s.swap ? traw[e].x : traw[e].y;
-        const float v3 = s.swap ? braw[e].y : braw[e].x, v4 = s.swap ? braw[e].x : braw[e].y;
-        const float t = s.w1 * v1 + s.w2 * v2 + s.w3 * v3 + s.w4 * v4;
-        v[e] = (scb + e < rows && pvalid) ? t * s.m : 0.f;
+        const float2 t = __builtin_bit_cast(float2, traw[e]);
+        const float2 b = __builtin_bit_cast(float2, braw[e]);
+        const float val = snext.wat * t.x + snext.wbt * t.y + snext.wab * b.x + snext.wbb * b.y;
+        v[e] = (scb + e < rows) ? val * snext.m : 0.f;
       }
     }
 #pragma unroll
@@ -343,7 +402,6 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
   const int kr = lane >> 4, jj = lane & 15;
   ChunkIt cur, nxt, nn;
   cur.first(cbeg, cend, cpg, MODE);
-  // prologue: chunk 0 -> LDS buffer 0; parameters of chunk 1 fetched
   if (MODE) {
     load_params_raw(cur);
     finish_params(cur);
@@ -351,8 +409,8 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
   issue_loads(cur);
   store_stage(cur, 0);
   nxt = cur;
-  nxt.advance(cbeg, cend, cpg, MODE);
-  bool has_next = nxt.k < K;
+  nxt.advance(K, cend, cpg, MODE);
+  bool has_next = nxt.c0 < cend;
   if (MODE && has_next) {
     load_params_raw(nxt);
     finish_params(nxt);
@@ -361,10 +419,10 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
 
   for (int buf = 0;; buf ^= 1) {
     nn = nxt;
-    nn.advance(cbeg, cend, cpg, MODE);
-    const bool has_nn = has_next && nn.k < K;
-    if (has_next) issue_loads(nxt);              // chunk c+1 loads in flight
-    if (MODE && has_nn) load_params_raw(nn);     // chunk c+2 offsets in flight
+    nn.advance(K, cend, cpg, MODE);
+    const bool has_nn = has_next && nn.c0 < cend;
+    if (has_next) issue_loads(nxt);
+    if (MODE && has_nn) load_params_raw(nn);
     {
       const float *sC = smem + buf * BUF, *sW = sC + PTT * SP;
 #pragma unroll
@@ -393,25 +451,50 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
     has_next = has_nn;
   }
 
-  // Epilogue: lane holds pixel column jj of block b, output channels 16m + 4kr + r.
+  // Epilogue: accumulators -> LDS [co][px] -> 16-byte row segments (+ residual) -> HBM.
+  __syncthreads();
+  float *sO = smem;
 #pragma unroll
-  for (int b = 0; b < NPB; ++b) {
-    const long pe = (long)tile * PTT + 16 * NPB * wave + 16 * b + jj;
-    if (pe >= P) continue;
+  for (int m = 0; m < NCB; ++m)
 #pragma unroll
-    for (int m = 0; m < NCB; ++m)
+    for (int b = 0; b < NPB; ++b)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + 16 * m + 4 * kr + r;
-        if (co < co_end) {
-          float v = acc[m][b][r];
-          if (a.bias) v += a.bias[co];
-          if (a.post_scale) v = v * a.post_scale[co] + a.post_shift[co];
-          const long o = ((long)n * a.Co + co) * P + pe;
-          if (a.residual) v += a.residual[o];
-          a.out[o] = apply_act(v, a.act);
-        }
+      for (int r = 0; r < 4; ++r)
+        sO[(16 * m + 4 * kr + r) * OP + 16 * NPB * wave + 16 * b + jj] = acc[m][b][r];
+  __syncthreads();
+  const long p0 = (long)tile * PTT;
+  const bool vec = (P & 3) == 0;
+  constexpr int QPR = PTT / 4;  // float4 per tile row
+  for (int e = tid; e < CO_T * QPR; e += NT) {
+    const int col = e / QPR, q = e % QPR;
+    const int co = co0 + col;
+    const long pe = p0 + 4 * q;
+    if (co >= co_end || pe >= P) continue;
+    const float bias = a.bias ? a.bias[co] : 0.f;
+    const float sc = a.post_scale ? a.post_scale[co] : 1.f;
+    const float sh = a.post_scale ? a.post_shift[co] : 0.f;
+    const long o = ((long)n * a.Co + co) * P + pe;
+    f32x4 v = *reinterpret_cast<const f32x4 *>(sO + col * OP + 4 * q);
+    if (vec && pe + 3 < P) {
+      f32x4 rv = a.residual ? *reinterpret_cast<const f32x4 *>(a.residual + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float t = v[u] + bias;
+        if (a.post_scale) t = t * sc + sh;
+        if (a.residual) t += rv[u];
+        v[u] = apply_act(t, a.act);
       }
+      *reinterpret_cast<f32x4 *>(a.out + o) = v;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (pe + u >= P) break;
+        float t = v[u] + bias;
+        if (a.post_scale) t = t * sc + sh;
+        if (a.residual) t += a.residual[o + u];
+        a.out[o + u] = apply_act(t, a.act);
+      }
+    }
   }
 }
 

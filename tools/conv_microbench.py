@@ -1,0 +1,50 @@
+"""Microbenchmark of the scale-0 layers of one AAModule (C2 shapes, B=8), each launched alone
+(for rocprofv3 passes and A/B timing).  Usage: python tools/conv_microbench.py [iters] [names]"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from aanet_amd import ops  # noqa: E402
+
+iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+names = sys.argv[2].split(",") if len(sys.argv) > 2 else None
+dev = "cuda"
+B, C, H, W = 8, 64, 128, 416
+g = torch.Generator(device=dev).manual_seed(0)
+x = torch.randn(B, C, H, W, device=dev, generator=g)
+res = torch.randn(B, C, H, W, device=dev, generator=g)
+w1 = torch.randn(C, C, 1, 1, device=dev, generator=g) * 0.1
+w3 = torch.randn(C, C, 3, 3, device=dev, generator=g) * 0.04
+wo = torch.randn(54, 32, 3, 3, device=dev, generator=g) * 0.01
+bo = torch.randn(54, device=dev, generator=g)
+b = torch.randn(C, device=dev, generator=g)
+p1, p3, po = ops.pack_weight(w1), ops.pack_weight(w3), ops.pack_weight(wo)
+om = ops.conv2d_fused(x, wo, bo, 1, 2, 2, 2, packed_weight=po)
+cases = {
+    "conv1x1": (lambda: ops.conv2d_fused(x, w1, b, act="relu", packed_weight=p1), 2 * B * H * W * C * C),
+    "conv1x1_res": (lambda: ops.conv2d_fused(x, w1, b, act="relu", residual=res, packed_weight=p1),
+                    2 * B * H * W * C * C),
+    "conv3x3": (lambda: ops.conv2d_fused(x, w3, b, 1, 1, 1, 1, "relu", packed_weight=p3),
+                2 * B * H * W * C * C * 9),
+    "offset_conv": (lambda: ops.conv2d_fused(x, wo, bo, 1, 2, 2, 2, packed_weight=po),
+                    2 * B * H * W * 54 * 32 * 9),
+    "dcn": (lambda: ops.mdcn_forward_fused(x, om, w3, None, b, b, "relu", 1, 2, 2, 2, 2.0,
+                                           packed_weight=p3), 2 * B * H * W * C * C * 9),
+    "csa_sum": (lambda: ops.csa_sum([x, res[:, :, :64, :208].contiguous(),
+                                     res[:, :, :32, :104].contiguous()]), 0),
+}
+for name, (fn, flops) in cases.items():
+    if names and name not in names:
+        continue
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / iters
+    print(f"{name:12s} {ms * 1e3:8.1f} us  {flops / ms / 1e9 if flops else 0:6.1f} TF/s")
