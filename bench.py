@@ -201,16 +201,11 @@ def main():
     elapsed = time.perf_counter() - t0
     disp = out  # graph output buffer (or last eager output)
 
-    record = torch.tensor([args.batch * args.steps, elapsed, float(disp.min()), float(disp.max())],
-                          dtype=torch.float64, device=device)
-    if world > 1:
-        gathered = [torch.empty_like(record) for _ in range(world)]
-        dist.all_gather(gathered, record)
-        recs = torch.stack(gathered).cpu()
-    else:
-        recs = record.cpu().view(1, -1)
-    total_pairs = float(recs[:, 0].sum())
-    t_max = float(recs[:, 1].max())
+    from aanet_amd import dist as adist
+    record = adist.make_record(device, pairs=args.batch * args.steps, elapsed_s=elapsed,
+                               disp_min=float(disp.min()), disp_max=float(disp.max()))
+    summary = adist.summarize(adist.gather_records(record))  # the one collective (metrics only)
+    total_pairs, t_max = summary["pairs"], summary["elapsed_max_s"]
 
     if rank == 0:
         roof = kernel_rooflines(model, left, right, args.batch, args.kernel_iters)

@@ -142,3 +142,26 @@ def test_mdcn_backward_vs_oracle(case, off_scale):
         scale = np.abs(ref).max() + 1e-12
         err = np.abs(got - ref)
         assert err.max() <= 1e-4 * scale + 1e-6, f"{name}: max err {err.max():.3g} (scale {scale:.3g})"
+
+
+def test_deform_conv_cuda_shim_matches_reference_call_sequence():
+    """The pybind-compatible module, called exactly as nets/deform_conv/deform_conv.py:140-166
+    calls deform_conv_cuda (in-place output, zeroed grads, vestigial bufs)."""
+    from aanet_amd import deform_conv_cuda
+    x, off, msk, w, b = make_case(8, 2, 32, 9, 26, 32)
+    xt, ot, mt, wt, bt = (g2t(a) for a in (x, off, msk, w, b))
+    bufs = [xt.new_empty(0), xt.new_empty(0)]
+    out = xt.new_empty((2, 32, 9, 26))
+    deform_conv_cuda.modulated_deform_conv_cuda_forward(xt, wt, bt, bufs[0], ot, mt, out, bufs[1],
+                                                        3, 3, 1, 1, 2, 2, 2, 2, 1, 2, True)
+    ref = oracle.mdcn_forward(x, off, msk, w, b, 1, 2, 2, 1, 2)
+    assert np.abs(t2n(out) - ref).max() <= 2e-5 * (1 + np.abs(ref).max())
+    go = np.random.default_rng(1).standard_normal(ref.shape).astype(np.float32)
+    gi, goff, gm = torch.zeros_like(xt), torch.zeros_like(ot), torch.zeros_like(mt)
+    gw, gb = torch.ones_like(wt), torch.ones_like(bt)  # accumulate semantics: start at 1
+    deform_conv_cuda.modulated_deform_conv_cuda_backward(xt, wt, bt, bufs[0], ot, mt, bufs[1], gi, gw,
+                                                         gb, goff, gm, g2t(go), 3, 3, 1, 1, 2, 2, 2,
+                                                         2, 1, 2, True)
+    rx, roff, rm, rw, rb = oracle.mdcn_backward(x, off, msk, w, go, True, 1, 2, 2, 1, 2)
+    for got, r in ((gi, rx), (goff, roff), (gm, rm), (gw, rw + 1), (gb, rb + 1)):
+        assert np.abs(t2n(got) - r).max() <= 1e-4 * (np.abs(r).max() + 1)
