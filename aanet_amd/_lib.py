@@ -33,6 +33,9 @@ _SIGNATURES = {
     "aanet_mdcn_bwd_f32": [_P] * 10 + [_I] * 12 + [_P],
     "aanet_conv2d_fused_f32": [_P] * 6 + [_I, _I, _P] + [_I] * 11 + [_P],
     "aanet_conv_weight_pack_f32": [_P, _P, _I, _I, _I, _I, _P],
+    "aanet_conv2d_pw_f32": [_P] * 5 + [_I] + [_P] * 3 + [_I, _I, _P] + [_I] * 10 + [_P],
+    "aanet_mdcn_pw_f32": [_P, _P, _L, _P, _L, _I, _F, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _P]
+    + [_I] * 11 + [_P],
     "aanet_csa_sum_f32": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P],
     "aanet_mdcn_im2col_f32": [_P, _P, _P, _P] + [_I] * 9 + [_P],
     "aanet_mdcn_sample_index": [_P, _P, _P, _P] + [_I] * 9 + [_P],

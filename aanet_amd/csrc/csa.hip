@@ -35,7 +35,43 @@ __device__ __forceinline__ float bilinear_resize(const float *__restrict__ im, i
   return h0l * (w0l * r0[w1] + w1l * r0[w1 + w1p]) + h1l * (w0l * r1[w1] + w1l * r1[w1 + w1p]);
 }
 
+// One thread = 4 consecutive output columns: the same-size term is read and the result written
+// as float4; resized terms (1/2, 1/4 resolution, L2-resident) are gathered per element.
 __global__ __launch_bounds__(256) void csa_sum_kernel(CsaArgs a) {
+  const int W4 = a.W >> 2;
+  const int HW = a.H * a.W;
+  const long total = (long)a.N * a.C * a.H * W4;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int xq = (int)(e % W4);
+    const long rowid = e / W4;             // (plane, y)
+    const int y = (int)(rowid % a.H);
+    const long plane = rowid / a.H;
+    const long base = plane * HW + (long)y * a.W + 4 * xq;
+    f32x4 acc;
+#pragma unroll
+    for (int j = 0; j < MAXIN; ++j) {
+      if (j >= a.num) break;
+      f32x4 v;
+      if (a.ih[j] == a.H && a.iw[j] == a.W) {
+        v = *reinterpret_cast<const f32x4 *>(a.in[j] + base);
+      } else {
+        const float *im = a.in[j] + plane * a.ih[j] * a.iw[j];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          v[u] = bilinear_resize(im, a.ih[j], a.iw[j], a.sh[j], a.sw[j], y, 4 * xq + u);
+      }
+      acc = j == 0 ? v : acc + v;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (a.act == 1) acc[u] = acc[u] > 0.f ? acc[u] : 0.f;
+      if (a.act == 2) acc[u] = acc[u] > 0.f ? acc[u] : 0.2f * acc[u];
+    }
+    *reinterpret_cast<f32x4 *>(a.out + base) = acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void csa_sum_scalar_kernel(CsaArgs a) {
   const long HW = (long)a.H * a.W;
   const long total = (long)a.N * a.C * HW;
   for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
@@ -83,9 +119,16 @@ extern "C" int aanet_csa_sum_f32(float *out, int n, int c, int h, int w, int num
   a.H = h;
   a.W = w;
   a.act = act;
-  const long total = (long)n * c * h * w;
+  bool vec = (w & 3) == 0;
+  for (int j = 0; j < num_inputs; ++j)
+    if (in_h[j] == h && in_w[j] == w && (reinterpret_cast<uintptr_t>(inputs[j]) & 15)) vec = false;
+  if (reinterpret_cast<uintptr_t>(out) & 15) vec = false;
+  const long total = (long)n * c * h * w / (vec ? 4 : 1);
   long g = (total + 255) / 256;
   if (g > 16384) g = 16384;
-  hipLaunchKernelGGL(csa_sum_kernel, dim3((unsigned)g), dim3(256), 0, as_hip(stream), a);
+  if (vec)
+    hipLaunchKernelGGL(csa_sum_kernel, dim3((unsigned)g), dim3(256), 0, as_hip(stream), a);
+  else
+    hipLaunchKernelGGL(csa_sum_scalar_kernel, dim3((unsigned)g), dim3(256), 0, as_hip(stream), a);
   return aanet_launch_status();
 }

@@ -34,8 +34,13 @@ struct MdcnArgs {
   const float *bias;
   const float *post_scale;
   const float *post_shift;
-  const float *residual;  // added before the activation (same shape as out) or NULL
+  const float *residual;  // added before the (last) activation, same shape as out, or NULL
   int act;
+  // pointwise tail (bottleneck conv3 fused into this conv's epilogue); tail_w == NULL: none.
+  // out = tail_act(tail_w . act(post_scale*(conv + bias) + post_shift) + tail_b + residual)
+  const float *tail_w;  // packed [Co2][Co]
+  const float *tail_b;
+  int tail_act, Co2;
   float *out;
   int N, C, H, W, Co, kh, kw, stride, pad, dil, groups, dg, Ho, Wo;
 };
@@ -258,7 +263,7 @@ __device__ __forceinline__ void make_sampw(SampW &s, float h, float w, int H, in
   s.m = m;
 }
 
-template <int MODE, int CO_T, int PTT, int PACKED>
+template <int MODE, int CO_T, int PTT, int PACKED, int TAIL>
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
   constexpr int NCB = CO_T / 16;         // 16-row output-channel blocks per wave
   constexpr int NPB = PTT / 64;          // 16-col pixel blocks per wave
@@ -417,38 +422,83 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
   }
   __syncthreads();
 
+  auto mfma_chunk = [&](int buf) {
+    const float *sC = smem + buf * BUF, *sW = sC + PTT * SP;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      f32x4 A[NCB], B[NPB];
+#pragma unroll
+      for (int m = 0; m < NCB; ++m)
+        A[m] = *reinterpret_cast<const f32x4 *>(sW + (16 * m + jj) * SP + 16 * h + 4 * kr);
+#pragma unroll
+      for (int b = 0; b < NPB; ++b)
+        B[b] = *reinterpret_cast<const f32x4 *>(sC + (16 * NPB * wave + 16 * b + jj) * SP +
+                                                16 * h + 4 * kr);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int m = 0; m < NCB; ++m)
+#pragma unroll
+          for (int b = 0; b < NPB; ++b) acc[m][b] = mfma16x16x4(A[m][s4], B[b][s4], acc[m][b]);
+    }
+  };
+
   for (int buf = 0;; buf ^= 1) {
     nn = nxt;
     nn.advance(K, cend, cpg, MODE);
     const bool has_nn = has_next && nn.c0 < cend;
     if (has_next) issue_loads(nxt);
     if (MODE && has_nn) load_params_raw(nn);
-    {
-      const float *sC = smem + buf * BUF, *sW = sC + PTT * SP;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        f32x4 A[NCB], B[NPB];
-#pragma unroll
-        for (int m = 0; m < NCB; ++m)
-          A[m] = *reinterpret_cast<const f32x4 *>(sW + (16 * m + jj) * SP + 16 * h + 4 * kr);
-#pragma unroll
-        for (int b = 0; b < NPB; ++b)
-          B[b] = *reinterpret_cast<const f32x4 *>(sC + (16 * NPB * wave + 16 * b + jj) * SP +
-                                                  16 * h + 4 * kr);
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-          for (int m = 0; m < NCB; ++m)
-#pragma unroll
-            for (int b = 0; b < NPB; ++b) acc[m][b] = mfma16x16x4(A[m][s4], B[b][s4], acc[m][b]);
-      }
-    }
+    mfma_chunk(buf);
     if (!has_next) break;
     store_stage(nxt, buf ^ 1);
     if (MODE && has_nn) finish_params(nn);
     __syncthreads();
     nxt = nn;
     has_next = has_nn;
+  }
+
+  if (TAIL) {
+    // act(post_scale*(acc+bias)+post_shift) -> LDS as the B operand [px][c] of a second GEMM with
+    // the pointwise weights [co2][c] (channels 32h..32h+31 in buffer h), then re-contract.
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < NCB; ++m) {
+      float *sC = smem + (m >> 1) * BUF;
+#pragma unroll
+      for (int b = 0; b < NPB; ++b) {
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = co0 + 16 * m + 4 * kr + r;
+          float t = 0.f;
+          if (co < co_end) {
+            t = acc[m][b][r] + (a.bias ? a.bias[co] : 0.f);
+            if (a.post_scale) t = t * a.post_scale[co] + a.post_shift[co];
+            t = apply_act(t, a.act);
+          }
+          v[r] = t;
+        }
+        *reinterpret_cast<f32x4 *>(sC + (16 * NPB * wave + 16 * b + jj) * SP + 16 * (m & 1) + 4 * kr) = v;
+        acc[m][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    constexpr int NH = (CO_T + 31) / 32;  // channel chunks of the pointwise GEMM
+#pragma unroll
+    for (int h2 = 0; h2 < NH; ++h2) {
+      float *sW = smem + h2 * BUF + PTT * SP;
+      for (int e = tid; e < KC * CO_T; e += NT) {
+        const int co2 = e / KC, cl = e % KC, c = 32 * h2 + cl;
+        sW[co2 * SP + cl] = (co2 < a.Co2 && c < a.Co) ? a.tail_w[(long)co2 * a.Co + c] : 0.f;
+      }
+      if (CO_T == 16) {  // channels 16..31 of the single chunk were never written
+        float *sC = smem;
+        for (int e = tid; e < PTT * 16; e += NT) sC[(e / 16) * SP + 16 + e % 16] = 0.f;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h2 = 0; h2 < NH; ++h2) mfma_chunk(h2);
   }
 
   // Epilogue: accumulators -> LDS [co][px] -> 16-byte row segments (+ residual) -> HBM.
@@ -465,24 +515,30 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
   const long p0 = (long)tile * PTT;
   const bool vec = (P & 3) == 0;
   constexpr int QPR = PTT / 4;  // float4 per tile row
+  const int cout = TAIL ? a.Co2 : a.Co;
+  const int cend_o = TAIL ? a.Co2 : co_end;
+  const float *ebias = TAIL ? a.tail_b : a.bias;
+  const float *esc = TAIL ? nullptr : a.post_scale;
+  const float *esh = TAIL ? nullptr : a.post_shift;
+  const int eact = TAIL ? a.tail_act : a.act;
   for (int e = tid; e < CO_T * QPR; e += NT) {
     const int col = e / QPR, q = e % QPR;
     const int co = co0 + col;
     const long pe = p0 + 4 * q;
-    if (co >= co_end || pe >= P) continue;
-    const float bias = a.bias ? a.bias[co] : 0.f;
-    const float sc = a.post_scale ? a.post_scale[co] : 1.f;
-    const float sh = a.post_scale ? a.post_shift[co] : 0.f;
-    const long o = ((long)n * a.Co + co) * P + pe;
+    if (co >= cend_o || pe >= P) continue;
+    const float bias = ebias ? ebias[co] : 0.f;
+    const float sc = esc ? esc[co] : 1.f;
+    const float sh = esc ? esh[co] : 0.f;
+    const long o = ((long)n * cout + co) * P + pe;
     f32x4 v = *reinterpret_cast<const f32x4 *>(sO + col * OP + 4 * q);
     if (vec && pe + 3 < P) {
       f32x4 rv = a.residual ? *reinterpret_cast<const f32x4 *>(a.residual + o) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         float t = v[u] + bias;
-        if (a.post_scale) t = t * sc + sh;
+        if (esc) t = t * sc + sh;
         if (a.residual) t += rv[u];
-        v[u] = apply_act(t, a.act);
+        v[u] = apply_act(t, eact);
       }
       *reinterpret_cast<f32x4 *>(a.out + o) = v;
     } else {
@@ -490,9 +546,9 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
       for (int u = 0; u < 4; ++u) {
         if (pe + u >= P) break;
         float t = v[u] + bias;
-        if (a.post_scale) t = t * sc + sh;
+        if (esc) t = t * sc + sh;
         if (a.residual) t += a.residual[o + u];
-        a.out[o + u] = apply_act(t, a.act);
+        a.out[o + u] = apply_act(t, eact);
       }
     }
   }
@@ -760,6 +816,10 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
   a.post_scale = ps;
   a.post_shift = psh;
   a.residual = nullptr;
+  a.tail_w = nullptr;
+  a.tail_b = nullptr;
+  a.tail_act = 0;
+  a.Co2 = co;
   a.act = act;
   a.out = out;
   a.N = n;
@@ -784,10 +844,12 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
 
 template <int MODE, int CO_T, int PTT>
 void launch_fwd_t(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
-  if (packed)
-    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1>), grid, dim3(NT), 0, st, a);
+  if (a.tail_w)
+    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1>), grid, dim3(NT), 0, st, a);
+  else if (packed)
+    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0>), grid, dim3(NT), 0, st, a);
   else
-    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 0>), grid, dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 0, 0>), grid, dim3(NT), 0, st, a);
 }
 
 template <int MODE>
@@ -800,7 +862,11 @@ int launch_fwd(const MdcnArgs &a, int packed, hipStream_t st) {
   if (a.post_scale && !a.post_shift) return AANET_EINVAL;
   const long P = (long)a.Ho * a.Wo;
   const int Cog = a.Co / a.groups;
-  const int co_t = Cog <= 16 ? 16 : (Cog <= 32 ? 32 : 64);
+  int co_t = Cog <= 16 ? 16 : (Cog <= 32 ? 32 : 64);
+  if (a.tail_w) {  // the whole conv output column of a pixel must sit in one workgroup
+    if (a.groups != 1 || a.Co > 64 || a.Co2 <= 0 || a.Co2 > 64 || !packed) return AANET_EUNSUPPORTED;
+    co_t = max(a.Co, a.Co2) <= 16 ? 16 : (max(a.Co, a.Co2) <= 32 ? 32 : 64);
+  }
   const int ncot = host_div_up(Cog, co_t);
   // 128-pixel tiles when they still give >= 4 workgroups per CU, else 64
   const int ptt = (long)a.N * host_div_up(P, 128) * a.groups * ncot >= 1024 ? 128 : 64;
@@ -861,6 +927,43 @@ extern "C" int aanet_conv2d_fused_f32(const float *x, const float *weight, const
                          act, out, n, c, h, w, co, kh, kw, stride, pad, dil, groups, 1);
   a.residual = residual;
   return launch_fwd<0>(a, weight_packed, as_hip(stream));
+}
+
+extern "C" int aanet_conv2d_pw_f32(const float *x, const float *weight_packed, const float *bias,
+                                   const float *post_scale, const float *post_shift, int act,
+                                   const float *pw_weight_packed, const float *pw_bias,
+                                   const float *residual, int pw_act, int co2, float *out, int n,
+                                   int c, int h, int w, int co, int kh, int kw, int stride,
+                                   int pad, int dil, aanet_stream_t stream) {
+  if (act < 0 || act > 2 || pw_act < 0 || pw_act > 2 || !pw_weight_packed) return AANET_EINVAL;
+  MdcnArgs a = make_args(x, nullptr, 0, nullptr, 0, 0, 1.f, weight_packed, bias, post_scale,
+                         post_shift, act, out, n, c, h, w, co, kh, kw, stride, pad, dil, 1, 1);
+  a.tail_w = pw_weight_packed;
+  a.tail_b = pw_bias;
+  a.tail_act = pw_act;
+  a.Co2 = co2;
+  a.residual = residual;
+  return launch_fwd<0>(a, 1, as_hip(stream));
+}
+
+extern "C" int aanet_mdcn_pw_f32(const float *x, const float *offset, long offset_batch_stride,
+                                 const float *mask, long mask_batch_stride, int mask_logits,
+                                 float mask_scale, const float *weight_packed, const float *bias,
+                                 const float *post_scale, const float *post_shift, int act,
+                                 const float *pw_weight_packed, const float *pw_bias,
+                                 const float *residual, int pw_act, int co2, float *out, int n,
+                                 int c, int h, int w, int co, int kh, int kw, int stride, int pad,
+                                 int dil, int dg, aanet_stream_t stream) {
+  if (act < 0 || act > 2 || pw_act < 0 || pw_act > 2 || !pw_weight_packed) return AANET_EINVAL;
+  MdcnArgs a = make_args(x, offset, offset_batch_stride, mask, mask_batch_stride, mask_logits,
+                         mask_scale, weight_packed, bias, post_scale, post_shift, act, out, n, c,
+                         h, w, co, kh, kw, stride, pad, dil, 1, dg);
+  a.tail_w = pw_weight_packed;
+  a.tail_b = pw_bias;
+  a.tail_act = pw_act;
+  a.Co2 = co2;
+  a.residual = residual;
+  return launch_fwd<1>(a, 1, as_hip(stream));
 }
 
 extern "C" int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset,

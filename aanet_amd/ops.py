@@ -189,6 +189,44 @@ def conv2d_fused(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1
     return out
 
 
+def conv2d_pw(x, weight, packed_weight, bias, post_scale, post_shift, act, pw_packed, pw_bias,
+              residual=None, pw_act=None, stride=1, padding=0, dilation=1):
+    """Plain conv + fused pointwise tail (bottleneck conv2 -> conv3, aanet_conv2d_pw_f32)."""
+    require_gpu(x, packed_weight, bias, post_scale, post_shift, pw_packed, pw_bias, residual)
+    N, C, H, W = x.shape
+    Co, _, kh, kw = weight.shape
+    Co2 = pw_packed.shape[-2]
+    Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
+    out = torch.empty((N, Co2, Ho, Wo), device=x.device, dtype=x.dtype)
+    call("aanet_conv2d_pw_f32", ptr(x), ptr(packed_weight), ptr(bias), ptr(post_scale),
+         ptr(post_shift), ACT[act], ptr(pw_packed), ptr(pw_bias), ptr(residual), ACT[pw_act], Co2,
+         ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation, stream_of(x))
+    return out
+
+
+def mdcn_pw(x, offset_mask, weight, packed_weight, bias, post_scale, post_shift, act, pw_packed,
+            pw_bias, residual=None, pw_act=None, stride=1, padding=0, dilation=1,
+            deformable_groups=1, mask_scale=2.0):
+    """DCN (offset/mask read in place from offset_conv's output) + fused pointwise tail."""
+    require_gpu(x, offset_mask, packed_weight, bias, post_scale, post_shift, pw_packed, pw_bias,
+                residual)
+    N, C, H, W = x.shape
+    Co, _, kh, kw = weight.shape
+    K = kh * kw
+    Co2 = pw_packed.shape[-2]
+    Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
+    if offset_mask.shape != (N, deformable_groups * 3 * K, Ho, Wo):
+        raise ValueError(f"offset_mask shape {tuple(offset_mask.shape)} unexpected")
+    out = torch.empty((N, Co2, Ho, Wo), device=x.device, dtype=x.dtype)
+    bs = offset_mask.stride(0)
+    mask_ptr = offset_mask.data_ptr() + 4 * deformable_groups * 2 * K * Ho * Wo
+    call("aanet_mdcn_pw_f32", ptr(x), ptr(offset_mask), bs, _lib.ctypes.c_void_p(mask_ptr), bs, 1,
+         float(mask_scale), ptr(packed_weight), ptr(bias), ptr(post_scale), ptr(post_shift),
+         ACT[act], ptr(pw_packed), ptr(pw_bias), ptr(residual), ACT[pw_act], Co2, ptr(out), N, C,
+         H, W, Co, kh, kw, stride, padding, dilation, deformable_groups, stream_of(x))
+    return out
+
+
 def csa_sum(inputs, act="leaky"):
     """act(inputs[0] + resize(inputs[1]) + ...) at inputs[0]'s size (aggregation.py:387-400)."""
     require_gpu(*inputs)

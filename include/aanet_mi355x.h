@@ -114,6 +114,28 @@ int aanet_conv2d_fused_f32(const float *x, const float *weight, const float *bia
                            int co, int kh, int kw, int stride, int pad, int dil, int groups,
                            aanet_stream_t stream);
 
+/* Bottleneck tail fusion (nets/deform.py:171-184 / 223-236 in eval): the pointwise conv3
+ * (+ folded BN3) runs in the epilogue of conv2, so the conv2 activation never goes to HBM:
+ *   t   = act(post_scale*(conv(x) + bias) + post_shift)                  [co channels]
+ *   out = pw_act(pw_weight . t + pw_bias + residual)                     [co2 channels]
+ * weight_packed / pw_weight_packed in the aanet_conv_weight_pack_f32 layout ([co2][co] for the
+ * pointwise one).  Requires groups == 1, co <= 64, co2 <= 64.  The _mdcn_ form takes the
+ * deformable sampler arguments of aanet_mdcn_fwd_fused_f32. */
+int aanet_conv2d_pw_f32(const float *x, const float *weight_packed, const float *bias,
+                        const float *post_scale, const float *post_shift, int act,
+                        const float *pw_weight_packed, const float *pw_bias,
+                        const float *residual, int pw_act, int co2, float *out, int n, int c,
+                        int h, int w, int co, int kh, int kw, int stride, int pad, int dil,
+                        aanet_stream_t stream);
+int aanet_mdcn_pw_f32(const float *x, const float *offset, long offset_batch_stride,
+                      const float *mask, long mask_batch_stride, int mask_logits,
+                      float mask_scale, const float *weight_packed, const float *bias,
+                      const float *post_scale, const float *post_shift, int act,
+                      const float *pw_weight_packed, const float *pw_bias, const float *residual,
+                      int pw_act, int co2, float *out, int n, int c, int h, int w, int co,
+                      int kh, int kw, int stride, int pad, int dil, int dg,
+                      aanet_stream_t stream);
+
 /* Weight repack for the conv engine: [co][cg][kh][kw] -> [kh][kw][co][cg].  Done once per
  * weight version by the caller (the eval path caches it with the folded BN). */
 int aanet_conv_weight_pack_f32(const float *weight, float *weight_packed, int co, int cg, int kh,

@@ -73,3 +73,49 @@ def test_csa_sum_vs_torch_interpolate(sizes, act):
     got = ops.csa_sum([t.to(DEV) for t in ins], act=act).cpu()
     err = (got - ref).abs().max().item()
     assert err <= 2e-5 * (1 + ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("C,H,W", [(64, 16, 52), (32, 9, 26), (16, 5, 13), (48, 7, 30)])
+def test_conv2d_pw_tail_vs_torch_cpu(C, H, W):
+    """conv3x3 + BN + ReLU -> 1x1 conv + BN + identity + ReLU (SimpleBottleneck tail) in one kernel."""
+    gen = torch.Generator().manual_seed(C)
+    N = 2
+    x = torch.randn(N, C, H, W, generator=gen)
+    w2 = torch.randn(C, C, 3, 3, generator=gen) / (3 * C ** 0.5)
+    b2 = torch.randn(C, generator=gen)
+    w3 = torch.randn(C, C, 1, 1, generator=gen) / C ** 0.5
+    b3 = torch.randn(C, generator=gen)
+    ident = torch.randn(N, C, H, W, generator=gen)
+    ref = F.relu(F.conv2d(F.relu(F.conv2d(x, w2, b2, 1, 1)), w3, b3) + ident)
+    d = lambda t: t.to(DEV)  # noqa: E731
+    got = ops.conv2d_pw(d(x), d(w2), ops.pack_weight(d(w2)), d(b2), None, None, "relu",
+                        ops.pack_weight(d(w3)), d(b3), d(ident), "relu", 1, 1, 1).cpu()
+    err = (got - ref).abs().max().item()
+    assert err <= 3e-5 * (1 + ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("C,H,W", [(64, 16, 52), (32, 9, 26), (16, 5, 13)])
+def test_mdcn_pw_tail_vs_oracle(C, H, W):
+    """DeformSimpleBottleneck tail: DCN (+BN2+ReLU, mask = 2*sigmoid) -> conv3 + BN3 + identity + ReLU."""
+    import numpy as np
+    from oracle import oracle
+    rng = np.random.default_rng(C)
+    N, dg = 2, 2
+    x = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    om = rng.standard_normal((N, dg * 27, H, W)).astype(np.float32)
+    w2 = (rng.standard_normal((C, C, 3, 3)) / (3 * C ** 0.5)).astype(np.float32)
+    sc = rng.uniform(0.5, 1.5, C).astype(np.float32)
+    sh = rng.standard_normal(C).astype(np.float32)
+    w3 = (rng.standard_normal((C, C, 1, 1)) / C ** 0.5).astype(np.float32)
+    b3 = rng.standard_normal(C).astype(np.float32)
+    ident = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    mask = (2.0 / (1.0 + np.exp(-om[:, dg * 18:].astype(np.float64)))).astype(np.float32)
+    t = oracle.mdcn_forward(x, om[:, :dg * 18], mask, w2, None, 1, 2, 2, 1, dg)
+    t = np.maximum(t * sc[None, :, None, None] + sh[None, :, None, None], 0)
+    ref = F.relu(F.conv2d(torch.from_numpy(t), torch.from_numpy(w3), torch.from_numpy(b3)) +
+                 torch.from_numpy(ident)).numpy()
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)  # noqa: E731
+    w2d, w3d = d(w2), d(w3)
+    got = ops.mdcn_pw(d(x), d(om), w2d, ops.pack_weight(w2d), None, d(sc), d(sh), "relu",
+                      ops.pack_weight(w3d), d(b3), d(ident), "relu", 1, 2, 2, dg, 2.0).cpu().numpy()
+    assert np.abs(got - ref).max() <= 1e-4 * (1 + np.abs(ref).max())

@@ -30,6 +30,10 @@ cases = {
                 2 * B * H * W * C * C * 9),
     "offset_conv": (lambda: ops.conv2d_fused(x, wo, bo, 1, 2, 2, 2, packed_weight=po),
                     2 * B * H * W * 54 * 32 * 9),
+    "dcn_pw": (lambda: ops.mdcn_pw(x, om, w3, p3, None, b, b, "relu", p1, b, res, "relu", 1, 2, 2, 2),
+               2 * B * H * W * C * C * 10),
+    "conv3x3_pw": (lambda: ops.conv2d_pw(x, w3, p3, b, None, None, "relu", p1, b, res, "relu", 1, 1, 1),
+                   2 * B * H * W * C * C * 10),
     "dcn": (lambda: ops.mdcn_forward_fused(x, om, w3, None, b, b, "relu", 1, 2, 2, 2, 2.0,
                                            packed_weight=p3), 2 * B * H * W * C * C * 9),
     "csa_sum": (lambda: ops.csa_sum([x, res[:, :, :64, :208].contiguous(),

@@ -17,7 +17,7 @@ print(f"step wall {(t1 - t0) / 1e6:.3f} ms, {len(seg)} kernels")
 agg = defaultdict(lambda: [0, 0.0])
 for r in seg:
     d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
-    name = r['Kernel_Name'].split('(')[0].replace('void ', '').replace('(anonymous namespace)::', '')
+    name = r['Kernel_Name'].replace('void ', '').replace('(anonymous namespace)::', '').split('(')[0]
     key = f"{name[:48]} g{r['Grid_Size_X']}x{r['Grid_Size_Y']}"
     agg[key][0] += 1
     agg[key][1] += d
