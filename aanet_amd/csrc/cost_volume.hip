@@ -28,52 +28,99 @@ struct CorrSmem {
   static constexpr int BYTES = BYTES_STAGE > BYTES_OUT ? BYTES_STAGE : BYTES_OUT;
 };
 
-// grid: (ceil(W/TX) * nchunks, H, N).  dchunk = disparities per chunk (<= 16*(NJ-1)+1).
-template <int NJ>
+// grid: 1-D, ntx * nchunks * H * N blocks.  Block ids are remapped so that every XCD owns a
+// contiguous range of (x tile fastest, then d chunk, row, image): the right-feature windows of
+// neighbouring x tiles overlap by half, and the overlap is then served by the same L2.
+// Loads are 16-byte buffer loads whose range check supplies the zero padding (x < 0, x >= W,
+// c >= C); requires W % 4 == 0 (the launcher falls back to the scalar kernel otherwise).
+template <int NJ, int VEC>
 __global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
     const float *__restrict__ L, const float *__restrict__ R, float *__restrict__ out, int C,
-    int H, int W, int D, int dchunk, int ntx) {
+    int H, int W, int D, int dchunk, int ntx, int nchunks) {
   using S = CorrSmem<NJ>;
   constexpr int RW = S::RW;
   __shared__ __attribute__((aligned(16))) float smem[S::BYTES / 4];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tx = blockIdx.x % ntx, chunk = blockIdx.x / ntx;
-  const int y = blockIdx.y, b = blockIdx.z;
+  const int nwg = gridDim.x, b0 = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b0 & 7;
+  int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b0 >> 3);
+  const int tx = id % ntx;
+  id /= ntx;
+  const int chunk = id % nchunks;
+  id /= nchunks;
+  const int y = id % H, b = id / H;
   const int x0 = tx * TX, d0 = chunk * dchunk;
   const int xr0 = x0 - d0 - 16 * (NJ - 1);  // first x' of the right window
   const long HW = (long)H * W;
+  const int img_bytes = (int)(C * HW * 4);
+  const auto Lr = __builtin_amdgcn_make_buffer_rsrc((void *)(L + (long)b * C * HW), (short)0,
+                                                     img_bytes, 0x00020000);
+  const auto Rr = __builtin_amdgcn_make_buffer_rsrc((void *)(R + (long)b * C * HW), (short)0,
+                                                     img_bytes, 0x00020000);
   const float *Lrow = L + (long)b * C * HW + (long)y * W;
   const float *Rrow = R + (long)b * C * HW + (long)y * W;
 
-  constexpr int LPT = CC * TX / NTHREADS;                 // L floats per thread per stage
-  constexpr int RPT = (CC * RW + NTHREADS - 1) / NTHREADS;  // R floats per thread per stage
-  float lreg[LPT], rreg[RPT];
+  constexpr int LQ = CC * TX / 4;            // float4 per stage of L (256: one per thread)
+  constexpr int RQ = CC * RW / 4;            // float4 per stage of R
+  constexpr int RPT4 = (RQ + NTHREADS - 1) / NTHREADS;
+  constexpr int LPT = CC * TX / NTHREADS;    // scalar fallback
+  constexpr int RPT = (CC * RW + NTHREADS - 1) / NTHREADS;
+  f32x4 lq[VEC ? 1 : 1], rq[VEC ? RPT4 : 1];
+  float lreg[VEC ? 1 : LPT], rreg[VEC ? 1 : RPT];
 
   auto load_stage = [&](int c0) {
+    if (VEC) {
+      {
+        const int row = tid / (TX / 4), col4 = tid % (TX / 4);
+        const int c = c0 + row, x = x0 + 4 * col4;
+        const int off = (c < C && x < W) ? (int)((((long)c * H + y) * W + x) * 4) : img_bytes;
+        lq[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(Lr, off, 0, 0));
+      }
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int e = tid + i * NTHREADS, row = e / TX, col = e % TX;
-      const int c = c0 + row, x = x0 + col;
-      lreg[i] = (c < C && x < W) ? Lrow[(long)c * HW + x] : 0.f;
-    }
+      for (int i = 0; i < RPT4; ++i) {
+        const int e = tid + i * NTHREADS;
+        const int row = e / (RW / 4), col4 = e % (RW / 4);
+        const int c = c0 + row, x = xr0 + 4 * col4;
+        const bool ok = e < RQ && c < C && x >= 0 && x < W;
+        const int off = ok ? (int)((((long)c * H + y) * W + x) * 4) : img_bytes;
+        rq[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(Rr, off, 0, 0));
+      }
+    } else {
 #pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-      const int e = tid + i * NTHREADS, row = e / RW, col = e % RW;
-      const int c = c0 + row, x = xr0 + col;
-      rreg[i] = (e < CC * RW && c < C && x >= 0 && x < W) ? Rrow[(long)c * HW + x] : 0.f;
+      for (int i = 0; i < LPT; ++i) {
+        const int e = tid + i * NTHREADS, row = e / TX, col = e % TX;
+        const int c = c0 + row, x = x0 + col;
+        lreg[i] = (c < C && x < W) ? Lrow[(long)c * HW + x] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const int e = tid + i * NTHREADS, row = e / RW, col = e % RW;
+        const int c = c0 + row, x = xr0 + col;
+        rreg[i] = (e < CC * RW && c < C && x >= 0 && x < W) ? Rrow[(long)c * HW + x] : 0.f;
+      }
     }
   };
   auto store_stage = [&](int buf) {
     float *sL = smem + buf * S::STAGE, *sR = sL + CC * TX;
+    if (VEC) {
+      reinterpret_cast<f32x4 *>(sL)[tid] = lq[0];
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) sL[tid + i * NTHREADS] = lreg[i];
+      for (int i = 0; i < RPT4; ++i) {
+        const int e = tid + i * NTHREADS;
+        if (e < RQ) reinterpret_cast<f32x4 *>(sR)[e] = rq[i];
+      }
+    } else {
 #pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-      const int e = tid + i * NTHREADS;
-      if (e < CC * RW) sR[e] = rreg[i];
+      for (int i = 0; i < LPT; ++i) sL[tid + i * NTHREADS] = lreg[i];
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const int e = tid + i * NTHREADS;
+        if (e < CC * RW) sR[e] = rreg[i];
+      }
     }
   };
+  (void)LQ;
 
   f32x4 acc[NJ];
 #pragma unroll
@@ -115,9 +162,20 @@ __global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
       if (dl >= 0 && dl < dmax) sO[dl * S::OUTP + 16 * wave + i] = acc[j][r] / Cf;
     }
   __syncthreads();
-  for (int e = tid; e < dmax * TX; e += NTHREADS) {
-    const int dl = e / TX, xl = e % TX;
-    if (x0 + xl < W) out[(((long)b * D + d0 + dl) * H + y) * W + x0 + xl] = sO[dl * S::OUTP + xl];
+  if (VEC) {
+    for (int e = tid; e < dmax * (TX / 4); e += NTHREADS) {
+      const int dl = e / (TX / 4), xq = e % (TX / 4);
+      if (x0 + 4 * xq < W) {
+        const float *src = sO + dl * S::OUTP + 4 * xq;
+        *reinterpret_cast<f32x4 *>(out + (((long)b * D + d0 + dl) * H + y) * W + x0 + 4 * xq) =
+            f32x4{src[0], src[1], src[2], src[3]};
+      }
+    }
+  } else {
+    for (int e = tid; e < dmax * TX; e += NTHREADS) {
+      const int dl = e / TX, xl = e % TX;
+      if (x0 + xl < W) out[(((long)b * D + d0 + dl) * H + y) * W + x0 + xl] = sO[dl * S::OUTP + xl];
+    }
   }
 }
 
@@ -126,9 +184,15 @@ int launch_corr(const float *L, const float *R, float *out, int n, int c, int h,
                 hipStream_t st) {
   const int dchunk = CorrSmem<NJ>::DC;
   const int nchunks = host_div_up(D, dchunk), ntx = host_div_up(w, TX);
-  dim3 grid(ntx * nchunks, h, n);
-  hipLaunchKernelGGL(corr_volume_kernel<NJ>, grid, dim3(NTHREADS), 0, st, L, R, out, c, h, w, D,
-                     dchunk, ntx);
+  const long nblk = (long)ntx * nchunks * h * n;
+  if (nblk > 0x7fffffffL) return AANET_EUNSUPPORTED;
+  const bool vec = (w % 4) == 0 && (long)c * h * w * 4 < 0x7fffffffL;
+  if (vec)
+    hipLaunchKernelGGL((corr_volume_kernel<NJ, 1>), dim3((unsigned)nblk), dim3(NTHREADS), 0, st,
+                       L, R, out, c, h, w, D, dchunk, ntx, nchunks);
+  else
+    hipLaunchKernelGGL((corr_volume_kernel<NJ, 0>), dim3((unsigned)nblk), dim3(NTHREADS), 0, st,
+                       L, R, out, c, h, w, D, dchunk, ntx, nchunks);
   return aanet_launch_status();
 }
 

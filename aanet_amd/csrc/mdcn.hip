@@ -15,6 +15,8 @@
 // and sampling indices equal the CPU oracle's bit for bit (tests/test_gpu_mdcn.py).
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 constexpr int NT = 256;
@@ -263,7 +265,7 @@ __device__ __forceinline__ void make_sampw(SampW &s, float h, float w, int H, in
   s.m = m;
 }
 
-template <int MODE, int CO_T, int PTT, int PACKED, int TAIL>
+template <int MODE, int CO_T, int PTT, int PACKED, int TAIL, int SCHED, int ABLATE = 0>
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
   constexpr int NCB = CO_T / 16;         // 16-row output-channel blocks per wave
   constexpr int NPB = PTT / 64;          // 16-col pixel blocks per wave
@@ -343,6 +345,19 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
     if (!pvalid) snext.m = 0.f;
   };
   auto issue_loads = [&](const ChunkIt &c) {
+    if (ABLATE == 1) return;
+    if (ABLATE == 4) {  // no global loads: LDS writes of register constants
+#pragma unroll
+      for (int i = 0; i < WPT; ++i) wreg[i] = (float)i;
+      if (MODE == 0) {
+#pragma unroll
+        for (int e = 0; e < CPT; ++e) vraw[e] = (float)e;
+      } else {
+#pragma unroll
+        for (int e = 0; e < CPT; ++e) traw[e] = braw[e] = i2v{e, e};
+      }
+      return;
+    }
     const int rows = c.c1 - c.c0;
     const int wbase = PACKED ? (((c.k * a.Co + co0) * Cg + (c.c0 - cbeg)) * 4)
                              : (((co0 * Cg + (c.c0 - cbeg)) * K + c.k) * 4);
@@ -372,6 +387,19 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
     }
   };
   auto store_stage = [&](const ChunkIt &c, int buf) {
+    if (ABLATE == 1) return;
+    if (ABLATE == 3) {  // loads kept alive, no LDS writes
+#pragma unroll
+      for (int i = 0; i < WPT; ++i) asm volatile("" ::"v"(wreg[i]));
+      if (MODE == 0) {
+#pragma unroll
+        for (int e = 0; e < CPT; ++e) asm volatile("" ::"v"(vraw[e]));
+      } else {
+#pragma unroll
+        for (int e = 0; e < CPT; ++e) asm volatile("" ::"v"(traw[e]), "v"(braw[e]));
+      }
+      return;
+    }
     float *sC = smem + buf * BUF, *sW = sC + PTT * SP;
     const int rows = c.c1 - c.c0;
 #pragma unroll
@@ -422,10 +450,9 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
   }
   __syncthreads();
 
-  auto mfma_chunk = [&](int buf) {
+  auto mfma_half = [&](int buf, int h) {
     const float *sC = smem + buf * BUF, *sW = sC + PTT * SP;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    {
       f32x4 A[NCB], B[NPB];
 #pragma unroll
       for (int m = 0; m < NCB; ++m)
@@ -439,8 +466,17 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
 #pragma unroll
         for (int m = 0; m < NCB; ++m)
 #pragma unroll
-          for (int b = 0; b < NPB; ++b) acc[m][b] = mfma16x16x4(A[m][s4], B[b][s4], acc[m][b]);
+          for (int b = 0; b < NPB; ++b) {
+            if (ABLATE == 2)
+              acc[m][b] += A[m][s4] * B[b][s4];  // keeps the LDS reads live, no matrix pipe
+            else
+              acc[m][b] = mfma16x16x4(A[m][s4], B[b][s4], acc[m][b]);
+          }
     }
+  };
+  auto mfma_chunk = [&](int buf) {
+    mfma_half(buf, 0);
+    mfma_half(buf, 1);
   };
 
   for (int buf = 0;; buf ^= 1) {
@@ -449,9 +485,28 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
     const bool has_nn = has_next && nn.c0 < cend;
     if (has_next) issue_loads(nxt);
     if (MODE && has_nn) load_params_raw(nn);
-    mfma_chunk(buf);
-    if (!has_next) break;
-    store_stage(nxt, buf ^ 1);
+    if (SCHED) {
+      // chunk c+1's staging math + LDS writes are interleaved with the second half of chunk c's
+      // MFMAs (different LDS buffers), so each wave keeps its matrix pipe busy by itself.
+      mfma_half(buf, 0);
+      if (!has_next) {
+        mfma_half(buf, 1);
+        break;
+      }
+      store_stage(nxt, buf ^ 1);
+      mfma_half(buf, 1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * (NCB + NPB), 0);  // DS_READ
+#pragma unroll
+      for (int i = 0; i < 4 * NCB * NPB; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);  // VALU
+        if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS_WRITE
+      }
+    } else {
+      mfma_chunk(buf);
+      if (!has_next) break;
+      store_stage(nxt, buf ^ 1);
+    }
     if (MODE && has_nn) finish_params(nn);
     __syncthreads();
     nxt = nn;
@@ -842,14 +897,41 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
   return a;
 }
 
+static int sched_mode() {  // A/B switch for the interleaved schedule (AANET_SCHED=0/1)
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("AANET_SCHED");
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+
 template <int MODE, int CO_T, int PTT>
 void launch_fwd_t(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
-  if (a.tail_w)
-    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1>), grid, dim3(NT), 0, st, a);
-  else if (packed)
-    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0>), grid, dim3(NT), 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 0, 0>), grid, dim3(NT), 0, st, a);
+  const int sc = sched_mode();
+  if (a.tail_w) {
+    if (sc)
+      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1>), grid, dim3(NT), 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 0>), grid, dim3(NT), 0, st, a);
+  } else if (packed) {
+    const char *ab = getenv("AANET_ABLATE");
+    const int abl = ab ? atoi(ab) : 0;
+    if (CO_T == 64 && PTT == 128 && abl == 1)
+      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, 1>), grid, dim3(NT), 0, st, a);
+    else if (CO_T == 64 && PTT == 128 && abl == 2)
+      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, 2>), grid, dim3(NT), 0, st, a);
+    else if (CO_T == 64 && PTT == 128 && abl == 3)
+      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, 3>), grid, dim3(NT), 0, st, a);
+    else if (CO_T == 64 && PTT == 128 && abl == 4)
+      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, 4>), grid, dim3(NT), 0, st, a);
+    else if (sc)
+      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1>), grid, dim3(NT), 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 0>), grid, dim3(NT), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 0, 0, 0>), grid, dim3(NT), 0, st, a);
+  }
 }
 
 template <int MODE>
