@@ -231,12 +231,15 @@ struct ChunkIt {
   }
 };
 
-// Pair-gather sampling state with the corner selection folded into the weights:
-// val = (wa_t*t.x + wb_t*t.y) + wa_b*b.x + wb_b*b.y equals kernel.cu:494-496 bit for bit
-// (terms that the reference adds as w*0 are exact zeros here too).
+// Pair-gather sampling state with the corner selection and the modulation mask folded into the
+// weights: val = (wa_t*t.x + wa_b*b.x) + (wb_t*t.y + wb_b*b.y), evaluated with two packed-fp32
+// ops and one add (kernel.cu:494-496 computes the same sum in another order: the values agree
+// to rounding; the sampling positions and corner indices are bit-exact).  f32 MFMA and VALU
+// never co-issue on gfx950, so every VALU op here is taken from the matrix pipe.
+typedef float f2v __attribute__((ext_vector_type(2)));
 struct SampW {
   int ot, ob;  // byte offsets of the 2-wide pairs in rows hl, hl+1
-  float wat, wbt, wab, wbb, m;
+  f2v wt, wb;  // (wa_t, wb_t) * m, (wa_b, wb_b) * m
 };
 
 __device__ __forceinline__ void make_sampw(SampW &s, float h, float w, int H, int W, float m) {
@@ -258,14 +261,18 @@ __device__ __forceinline__ void make_sampw(SampW &s, float h, float w, int H, in
   s.ob = (rb * W + pb) * 4;
   const bool swap = valid && pb != wl;  // wl == -1: pair = (wl+1, wl+2); wl == W-1: (wl-1, wl)
   const bool left = wl < pb;             // wl == -1
-  s.wat = swap ? (left ? w2 : 0.f) : w1;
-  s.wbt = swap ? (left ? 0.f : w1) : w2;
-  s.wab = swap ? (left ? w4 : 0.f) : w3;
-  s.wbb = swap ? (left ? 0.f : w3) : w4;
-  s.m = m;
+  const float wat = swap ? (left ? w2 : 0.f) : w1;
+  const float wbt = swap ? (left ? 0.f : w1) : w2;
+  const float wab = swap ? (left ? w4 : 0.f) : w3;
+  const float wbb = swap ? (left ? 0.f : w3) : w4;
+  s.wt = f2v{wat, wbt} * m;
+  s.wb = f2v{wab, wbb} * m;
 }
 
-template <int MODE, int CO_T, int PTT, int PACKED, int TAIL, int SCHED, int ABLATE = 0>
+// FULL: every chunk holds KC channels (Cg % KC == 0, and cpg % KC == 0 for the DCN), so the
+// staging code has no per-row guards.  Those guards are wave-uniform, and the compiler turns
+// them into scalar branches, which split the loop body and defeat the MFMA/staging interleave.
+template <int MODE, int CO_T, int PTT, int PACKED, int TAIL, int SCHED, int FULL, int ABLATE = 0>
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
   constexpr int NCB = CO_T / 16;         // 16-row output-channel blocks per wave
   constexpr int NPB = PTT / 64;          // 16-col pixel blocks per wave
@@ -338,11 +345,11 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
   auto finish_params = [&](const ChunkIt &c) {
 #pragma clang fp contract(off)
     const int i = c.k / a.kw, j = c.k % a.kw;
-    float m = a.mask_logits ? a.mask_scale * (1.f / (1.f + expf(-mlog))) : mlog;
+    float m = a.mask_logits ? a.mask_scale * __builtin_amdgcn_rcpf(1.f + __expf(-mlog)) : mlog;
+    if (!pvalid) m = 0.f;
     const float h = (float)(ho * a.stride - a.pad + i * a.dil) + off_h;
     const float w = (float)(wo * a.stride - a.pad + j * a.dil) + off_w;
     make_sampw(snext, h, w, a.H, a.W, m);
-    if (!pvalid) snext.m = 0.f;
   };
   auto issue_loads = [&](const ChunkIt &c) {
     if (ABLATE == 1) return;
@@ -373,14 +380,14 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
 #pragma unroll
       for (int e = 0; e < CPT; ++e) {
         const int soff = cbase + e * plane_bytes;
-        vraw[e] = (scb + e < rows)
+        vraw[e] = (FULL || scb + e < rows)
                       ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, voff, soff, 0))
                       : 0.f;
       }
     } else {
 #pragma unroll
       for (int e = 0; e < CPT; ++e) {
-        const int soff = cbase + min(e, rows - 1 - scb) * plane_bytes;
+        const int soff = cbase + (FULL ? e : min(e, rows - 1 - scb)) * plane_bytes;
         traw[e] = __builtin_amdgcn_raw_buffer_load_b64(xr, snext.ot, soff, 0);
         braw[e] = __builtin_amdgcn_raw_buffer_load_b64(xr, snext.ob, soff, 0);
       }
@@ -413,11 +420,11 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
       if (MODE == 0) {
         v[e] = vraw[e];
       } else {
-#pragma clang fp contract(off)
-        const float2 t = __builtin_bit_cast(float2, traw[e]);
-        const float2 b = __builtin_bit_cast(float2, braw[e]);
-        const float val = snext.wat * t.x + snext.wbt * t.y + snext.wab * b.x + snext.wbb * b.y;
-        v[e] = (scb + e < rows) ? val * snext.m : 0.f;
+        const f2v p = __builtin_elementwise_fma(snext.wb, __builtin_bit_cast(f2v, braw[e]),
+                                                snext.wt * __builtin_bit_cast(f2v, traw[e]));
+        float r;  // scalar add of the two halves (keeps the vectorizer from re-pairing them)
+        asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(p.x), "v"(p.y));
+        v[e] = (FULL || scb + e < rows) ? r : 0.f;
       }
     }
 #pragma unroll
@@ -450,29 +457,36 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
   }
   __syncthreads();
 
-  auto mfma_half = [&](int buf, int h) {
+  struct Frag {
+    f32x4 A[NCB], B[NPB];
+  };
+  auto read_frag = [&](int buf, int h, Frag &f) {
     const float *sC = smem + buf * BUF, *sW = sC + PTT * SP;
-    {
-      f32x4 A[NCB], B[NPB];
+#pragma unroll
+    for (int m = 0; m < NCB; ++m)
+      f.A[m] = *reinterpret_cast<const f32x4 *>(sW + (16 * m + jj) * SP + 16 * h + 4 * kr);
+#pragma unroll
+    for (int b = 0; b < NPB; ++b)
+      f.B[b] = *reinterpret_cast<const f32x4 *>(sC + (16 * NPB * wave + 16 * b + jj) * SP +
+                                                16 * h + 4 * kr);
+  };
+  auto mma = [&](const Frag &f) {
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
       for (int m = 0; m < NCB; ++m)
-        A[m] = *reinterpret_cast<const f32x4 *>(sW + (16 * m + jj) * SP + 16 * h + 4 * kr);
 #pragma unroll
-      for (int b = 0; b < NPB; ++b)
-        B[b] = *reinterpret_cast<const f32x4 *>(sC + (16 * NPB * wave + 16 * b + jj) * SP +
-                                                16 * h + 4 * kr);
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-        for (int m = 0; m < NCB; ++m)
-#pragma unroll
-          for (int b = 0; b < NPB; ++b) {
-            if (ABLATE == 2)
-              acc[m][b] += A[m][s4] * B[b][s4];  // keeps the LDS reads live, no matrix pipe
-            else
-              acc[m][b] = mfma16x16x4(A[m][s4], B[b][s4], acc[m][b]);
-          }
-    }
+        for (int b = 0; b < NPB; ++b) {
+          if (ABLATE == 2)
+            acc[m][b] += f.A[m][s4] * f.B[b][s4];  // keeps the LDS reads live, no matrix pipe
+          else
+            acc[m][b] = mfma16x16x4(f.A[m][s4], f.B[b][s4], acc[m][b]);
+        }
+  };
+  auto mfma_half = [&](int buf, int h) {
+    Frag f;
+    read_frag(buf, h, f);
+    mma(f);
   };
   auto mfma_chunk = [&](int buf) {
     mfma_half(buf, 0);
@@ -488,14 +502,18 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
     if (SCHED) {
       // chunk c+1's staging math + LDS writes are interleaved with the second half of chunk c's
       // MFMAs (different LDS buffers), so each wave keeps its matrix pipe busy by itself.
+      // The half-1 operands are read before the staging writes: LDS reads and writes of the two
+      // buffers cannot be proven disjoint, so reads issued after the writes would hold every
+      // MFMA of half 1 behind the whole staging store.
       mfma_half(buf, 0);
+      Frag f1;
+      read_frag(buf, 1, f1);
       if (!has_next) {
-        mfma_half(buf, 1);
+        mma(f1);
         break;
       }
       store_stage(nxt, buf ^ 1);
-      mfma_half(buf, 1);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2 * (NCB + NPB), 0);  // DS_READ
+      mma(f1);
 #pragma unroll
       for (int i = 0; i < 4 * NCB * NPB; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
@@ -897,41 +915,33 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
   return a;
 }
 
-static int sched_mode() {  // A/B switch for the interleaved schedule (AANET_SCHED=0/1)
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("AANET_SCHED");
-    v = e ? atoi(e) : 1;
+template <int MODE, int CO_T, int PTT, int FULL>
+void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
+  if (a.tail_w) {
+    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1, FULL>), grid, dim3(NT), 0, st, a);
+  } else if (packed) {
+    // AANET_ABLATE=1..4 selects the staging ablations (tools/ab_ablate.sh); default 0
+    static const int abl = [] { const char *e = getenv("AANET_ABLATE"); return e ? atoi(e) : 0; }();
+    if (FULL && CO_T == 64 && PTT == 128 && abl >= 1 && abl <= 4) {
+      if (abl == 1) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 1>), grid, dim3(NT), 0, st, a);
+      if (abl == 2) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 2>), grid, dim3(NT), 0, st, a);
+      if (abl == 3) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 3>), grid, dim3(NT), 0, st, a);
+      if (abl == 4) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 4>), grid, dim3(NT), 0, st, a);
+    } else {
+      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL>), grid, dim3(NT), 0, st, a);
+    }
+  } else {
+    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 0, 0, 0, FULL>), grid, dim3(NT), 0, st, a);
   }
-  return v;
 }
 
 template <int MODE, int CO_T, int PTT>
 void launch_fwd_t(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
-  const int sc = sched_mode();
-  if (a.tail_w) {
-    if (sc)
-      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1>), grid, dim3(NT), 0, st, a);
-    else
-      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 0>), grid, dim3(NT), 0, st, a);
-  } else if (packed) {
-    const char *ab = getenv("AANET_ABLATE");
-    const int abl = ab ? atoi(ab) : 0;
-    if (CO_T == 64 && PTT == 128 && abl == 1)
-      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, 1>), grid, dim3(NT), 0, st, a);
-    else if (CO_T == 64 && PTT == 128 && abl == 2)
-      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, 2>), grid, dim3(NT), 0, st, a);
-    else if (CO_T == 64 && PTT == 128 && abl == 3)
-      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, 3>), grid, dim3(NT), 0, st, a);
-    else if (CO_T == 64 && PTT == 128 && abl == 4)
-      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, 4>), grid, dim3(NT), 0, st, a);
-    else if (sc)
-      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1>), grid, dim3(NT), 0, st, a);
-    else
-      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 0>), grid, dim3(NT), 0, st, a);
-  } else {
-    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 0, 0, 0>), grid, dim3(NT), 0, st, a);
-  }
+  const int Cg = a.C / a.groups, cpg = a.C / a.dg;
+  if (Cg % KC == 0 && (!MODE || cpg % KC == 0))
+    launch_fwd_f<MODE, CO_T, PTT, 1>(a, packed, grid, st);
+  else
+    launch_fwd_f<MODE, CO_T, PTT, 0>(a, packed, grid, st);
 }
 
 template <int MODE>

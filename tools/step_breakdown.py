@@ -7,8 +7,8 @@ path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof_step/run_kernel_tr
 rows = list(csv.DictReader(open(path)))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
 # a step starts with the scale-0 correlation launch followed by the scale-1 one
-idx = [i for i, r in enumerate(rows[:-1]) if 'corr_volume_kernel<5>' in r['Kernel_Name']
-       and 'corr_volume_kernel<3>' in rows[i + 1]['Kernel_Name']]
+idx = [i for i, r in enumerate(rows[:-1]) if 'corr_volume_kernel<5' in r['Kernel_Name']
+       and 'corr_volume_kernel<3' in rows[i + 1]['Kernel_Name']]
 a, b = idx[-2], idx[-1]
 seg = rows[a:b]
 t0 = int(seg[0]['Start_Timestamp'])
