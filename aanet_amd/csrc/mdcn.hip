@@ -206,6 +206,7 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 // Epilogue: the tile is transposed through LDS and written as 16-byte row segments:
 // y = act(post_scale*(acc + bias) + post_shift + residual).
 // grid: x = N * ceil(P/PTT), y = groups * ceil(Cog/CO_T).
+constexpr int FNT = 512;  // forward conv engine: 8 waves = 2 (output channels) x 4 (pixels)
 constexpr int SP = 40;  // LDS row pitch (floats) of both staging tiles: conflict-free b128 reads
 
 typedef int i2v __attribute__((ext_vector_type(2)));
@@ -273,17 +274,27 @@ __device__ __forceinline__ void make_sampw(SampW &s, float h, float w, int H, in
 // staging code has no per-row guards.  Those guards are wave-uniform, and the compiler turns
 // them into scalar branches, which split the loop body and defeat the MFMA/staging interleave.
 template <int MODE, int CO_T, int PTT, int PACKED, int TAIL, int SCHED, int FULL, int ABLATE = 0>
-__global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
-  constexpr int NCB = CO_T / 16;         // 16-row output-channel blocks per wave
-  constexpr int NPB = PTT / 64;          // 16-col pixel blocks per wave
-  constexpr int CPT = KC * PTT / NT;     // im2col values staged per thread per chunk
-  constexpr int WPT = KC * CO_T / NT;    // weights staged per thread per chunk
+__global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
+  constexpr int WC = CO_T >= 32 ? 2 : 1;   // waves along the output channels
+  constexpr int WP = FNT / 64 / WC;        // waves along the pixels
+  constexpr int NCB = CO_T / 16 / WC;      // 16-row output-channel blocks per wave
+  constexpr int NPB = PTT / 16 / WP;       // 16-col pixel blocks per wave
+  constexpr int CPT = KC * PTT / FNT;      // im2col values staged per thread per chunk
+  constexpr int WPT = KC * CO_T / FNT;     // weights staged per thread per chunk
+  static_assert(NCB >= 1 && NPB >= 1 && WPT >= 1 && CPT % 4 == 0, "tile shape");
   constexpr int BUF = (PTT + CO_T) * SP; // floats per LDS buffer
   constexpr int OP = PTT + 4;            // epilogue tile pitch
   static_assert(CO_T * OP <= 2 * BUF, "epilogue tile must fit the staging buffers");
-  __shared__ __attribute__((aligned(16))) float smem[2 * BUF];
+  // DCN: the sampling state of a (pixel, tap, deformable group) is computed once, by the threads
+  // tid < PTT, and published through a double-buffered LDS slot to the FNT/PTT threads that
+  // stage channels of that pixel (the VALU it saves is matrix-pipe time).
+  constexpr int PSLOT = PTT * 8;
+  __shared__ __attribute__((aligned(16))) float smem[2 * BUF + (MODE ? 2 * PSLOT : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool pwave = __builtin_amdgcn_readfirstlane(wave) < PTT / 64;  // tid < PTT, as an SGPR
+  const int wc0 = __builtin_amdgcn_readfirstlane((wave / WP) * NCB);  // first co block of the wave
+  const int wp0 = __builtin_amdgcn_readfirstlane((wave % WP) * NPB);  // first px block of the wave
   const long P = (long)a.Ho * a.Wo;
   const int ntiles = (int)((P + PTT - 1) / PTT);
   // XCD-aware remap of the pixel-tile index (bijective for any grid size)
@@ -327,7 +338,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
   int wlane[WPT];  // per-lane weight byte offsets (chunk-invariant)
 #pragma unroll
   for (int i = 0; i < WPT; ++i) {
-    const int e = tid + NT * i, co = e / KC, cl = e % KC;
+    const int e = tid + FNT * i, co = e / KC, cl = e % KC;
     // rows past the chunk read a neighbouring channel (multiplied by a zero im2col value);
     // reads past the tensor are out of range -> 0; co past co_end is never stored
     wlane[i] = PACKED ? (co * Cg + cl) * 4 : (co * Cg * K + cl * K) * 4;
@@ -336,20 +347,36 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
 
   auto load_params_raw = [&](const ChunkIt &c) {
     const int g = c.c0 / cpg;
-    const int ob = (int)(((long)g * 2 * K + 2 * c.k) * P * 4);
+    const int ob = __builtin_amdgcn_readfirstlane((int)(((long)g * 2 * K + 2 * c.k) * P * 4));
+    const int mb = __builtin_amdgcn_readfirstlane((int)(((long)g * K + c.k) * P * 4));
     off_h = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, pl4, ob, 0));
     off_w = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, pl4, ob + (int)(P * 4), 0));
-    mlog = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                         mskr, pl4, (int)(((long)g * K + c.k) * P * 4), 0));
+    mlog = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mskr, pl4, mb, 0));
   };
-  auto finish_params = [&](const ChunkIt &c) {
+  auto finish_params = [&](const ChunkIt &c, int slot) {
 #pragma clang fp contract(off)
     const int i = c.k / a.kw, j = c.k % a.kw;
     float m = a.mask_logits ? a.mask_scale * __builtin_amdgcn_rcpf(1.f + __expf(-mlog)) : mlog;
     if (!pvalid) m = 0.f;
     const float h = (float)(ho * a.stride - a.pad + i * a.dil) + off_h;
     const float w = (float)(wo * a.stride - a.pad + j * a.dil) + off_w;
-    make_sampw(snext, h, w, a.H, a.W, m);
+    SampW sw;
+    make_sampw(sw, h, w, a.H, a.W, m);
+    float *d = smem + 2 * BUF + slot * PSLOT + spx * 8;
+    *reinterpret_cast<f32x4 *>(d) = f32x4{__builtin_bit_cast(float, sw.ot),
+                                          __builtin_bit_cast(float, sw.ob), sw.wt.x, sw.wt.y};
+    *reinterpret_cast<f2v *>(d + 4) = sw.wb;
+  };
+  auto get_params = [&](int slot) {
+    const float *d = smem + 2 * BUF + slot * PSLOT + spx * 8;
+    const f32x4 q = *reinterpret_cast<const f32x4 *>(d);
+    // copy the elements to scalars first: __builtin_bit_cast of an ext-vector element lvalue
+    // (q[1]) reads element 0 with this clang
+    const float q0 = q[0], q1 = q[1];
+    snext.ot = __builtin_bit_cast(int, q0);
+    snext.ob = __builtin_bit_cast(int, q1);
+    snext.wt = f2v{q[2], q[3]};
+    snext.wb = *reinterpret_cast<const f2v *>(d + 4);
   };
   auto issue_loads = [&](const ChunkIt &c) {
     if (ABLATE == 1) return;
@@ -411,7 +438,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
     const int rows = c.c1 - c.c0;
 #pragma unroll
     for (int i = 0; i < WPT; ++i) {
-      const int e = tid + NT * i;
+      const int e = tid + FNT * i;
       sW[(e / KC) * SP + e % KC] = wreg[i];
     }
     float v[CPT];
@@ -443,18 +470,23 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
   ChunkIt cur, nxt, nn;
   cur.first(cbeg, cend, cpg, MODE);
   if (MODE) {
-    load_params_raw(cur);
-    finish_params(cur);
+    if (pwave) {
+      load_params_raw(cur);
+      finish_params(cur, 0);
+    }
+    __syncthreads();
+    get_params(0);
   }
   issue_loads(cur);
   store_stage(cur, 0);
   nxt = cur;
   nxt.advance(K, cend, cpg, MODE);
   bool has_next = nxt.c0 < cend;
-  if (MODE && has_next) {
+  if (MODE && has_next && pwave) {
     load_params_raw(nxt);
-    finish_params(nxt);
+    finish_params(nxt, 1);
   }
+  int slot = 1;  // parameter slot of `nxt`
   __syncthreads();
 
   struct Frag {
@@ -464,11 +496,10 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
     const float *sC = smem + buf * BUF, *sW = sC + PTT * SP;
 #pragma unroll
     for (int m = 0; m < NCB; ++m)
-      f.A[m] = *reinterpret_cast<const f32x4 *>(sW + (16 * m + jj) * SP + 16 * h + 4 * kr);
+      f.A[m] = *reinterpret_cast<const f32x4 *>(sW + (16 * (wc0 + m) + jj) * SP + 16 * h + 4 * kr);
 #pragma unroll
     for (int b = 0; b < NPB; ++b)
-      f.B[b] = *reinterpret_cast<const f32x4 *>(sC + (16 * NPB * wave + 16 * b + jj) * SP +
-                                                16 * h + 4 * kr);
+      f.B[b] = *reinterpret_cast<const f32x4 *>(sC + (16 * (wp0 + b) + jj) * SP + 16 * h + 4 * kr);
   };
   auto mma = [&](const Frag &f) {
 #pragma unroll
@@ -497,8 +528,11 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
     nn = nxt;
     nn.advance(K, cend, cpg, MODE);
     const bool has_nn = has_next && nn.c0 < cend;
-    if (has_next) issue_loads(nxt);
-    if (MODE && has_nn) load_params_raw(nn);
+    if (has_next) {
+      if (MODE) get_params(slot);
+      issue_loads(nxt);
+    }
+    if (MODE && has_nn && pwave) load_params_raw(nn);
     if (SCHED) {
       // chunk c+1's staging math + LDS writes are interleaved with the second half of chunk c's
       // MFMAs (different LDS buffers), so each wave keeps its matrix pipe busy by itself.
@@ -525,8 +559,9 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
       if (!has_next) break;
       store_stage(nxt, buf ^ 1);
     }
-    if (MODE && has_nn) finish_params(nn);
+    if (MODE && has_nn && pwave) finish_params(nn, slot ^ 1);
     __syncthreads();
+    slot ^= 1;
     nxt = nn;
     has_next = has_nn;
   }
@@ -537,13 +572,14 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
     __syncthreads();
 #pragma unroll
     for (int m = 0; m < NCB; ++m) {
-      float *sC = smem + (m >> 1) * BUF;
+      const int mg = wc0 + m;
+      float *sC = smem + (mg >> 1) * BUF;
 #pragma unroll
       for (int b = 0; b < NPB; ++b) {
         f32x4 v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int co = co0 + 16 * m + 4 * kr + r;
+          const int co = co0 + 16 * mg + 4 * kr + r;
           float t = 0.f;
           if (co < co_end) {
             t = acc[m][b][r] + (a.bias ? a.bias[co] : 0.f);
@@ -552,7 +588,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
           }
           v[r] = t;
         }
-        *reinterpret_cast<f32x4 *>(sC + (16 * NPB * wave + 16 * b + jj) * SP + 16 * (m & 1) + 4 * kr) = v;
+        *reinterpret_cast<f32x4 *>(sC + (16 * (wp0 + b) + jj) * SP + 16 * (mg & 1) + 4 * kr) = v;
         acc[m][b] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
@@ -560,13 +596,13 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
 #pragma unroll
     for (int h2 = 0; h2 < NH; ++h2) {
       float *sW = smem + h2 * BUF + PTT * SP;
-      for (int e = tid; e < KC * CO_T; e += NT) {
+      for (int e = tid; e < KC * CO_T; e += FNT) {
         const int co2 = e / KC, cl = e % KC, c = 32 * h2 + cl;
         sW[co2 * SP + cl] = (co2 < a.Co2 && c < a.Co) ? a.tail_w[(long)co2 * a.Co + c] : 0.f;
       }
       if (CO_T == 16) {  // channels 16..31 of the single chunk were never written
         float *sC = smem;
-        for (int e = tid; e < PTT * 16; e += NT) sC[(e / 16) * SP + 16 + e % 16] = 0.f;
+        for (int e = tid; e < PTT * 16; e += FNT) sC[(e / 16) * SP + 16 + e % 16] = 0.f;
       }
     }
     __syncthreads();
@@ -583,7 +619,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
     for (int b = 0; b < NPB; ++b)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        sO[(16 * m + 4 * kr + r) * OP + 16 * NPB * wave + 16 * b + jj] = acc[m][b][r];
+        sO[(16 * (wc0 + m) + 4 * kr + r) * OP + 16 * (wp0 + b) + jj] = acc[m][b][r];
   __syncthreads();
   const long p0 = (long)tile * PTT;
   const bool vec = (P & 3) == 0;
@@ -594,7 +630,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(MdcnArgs a) {
   const float *esc = TAIL ? nullptr : a.post_scale;
   const float *esh = TAIL ? nullptr : a.post_shift;
   const int eact = TAIL ? a.tail_act : a.act;
-  for (int e = tid; e < CO_T * QPR; e += NT) {
+  for (int e = tid; e < CO_T * QPR; e += FNT) {
     const int col = e / QPR, q = e % QPR;
     const int co = co0 + col;
     const long pe = p0 + 4 * q;
@@ -918,20 +954,20 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
 template <int MODE, int CO_T, int PTT, int FULL>
 void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
   if (a.tail_w) {
-    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1, FULL>), grid, dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1, FULL>), grid, dim3(FNT), 0, st, a);
   } else if (packed) {
     // AANET_ABLATE=1..4 selects the staging ablations (tools/ab_ablate.sh); default 0
     static const int abl = [] { const char *e = getenv("AANET_ABLATE"); return e ? atoi(e) : 0; }();
     if (FULL && CO_T == 64 && PTT == 128 && abl >= 1 && abl <= 4) {
-      if (abl == 1) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 1>), grid, dim3(NT), 0, st, a);
-      if (abl == 2) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 2>), grid, dim3(NT), 0, st, a);
-      if (abl == 3) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 3>), grid, dim3(NT), 0, st, a);
-      if (abl == 4) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 4>), grid, dim3(NT), 0, st, a);
+      if (abl == 1) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 1>), grid, dim3(FNT), 0, st, a);
+      if (abl == 2) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 2>), grid, dim3(FNT), 0, st, a);
+      if (abl == 3) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 3>), grid, dim3(FNT), 0, st, a);
+      if (abl == 4) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 4>), grid, dim3(FNT), 0, st, a);
     } else {
-      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL>), grid, dim3(NT), 0, st, a);
+      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL>), grid, dim3(FNT), 0, st, a);
     }
   } else {
-    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 0, 0, 0, FULL>), grid, dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 0, 0, 0, FULL>), grid, dim3(FNT), 0, st, a);
   }
 }
 
@@ -961,7 +997,7 @@ int launch_fwd(const MdcnArgs &a, int packed, hipStream_t st) {
   }
   const int ncot = host_div_up(Cog, co_t);
   // 128-pixel tiles when they still give >= 4 workgroups per CU, else 64
-  const int ptt = (long)a.N * host_div_up(P, 128) * a.groups * ncot >= 1024 ? 128 : 64;
+  const int ptt = co_t == 16 || (long)a.N * host_div_up(P, 128) * a.groups * ncot >= 1024 ? 128 : 64;
   dim3 grid((unsigned)(a.N * host_div_up(P, ptt)), (unsigned)(a.groups * ncot));
   if (ptt == 128) {
     switch (co_t) {
@@ -971,7 +1007,7 @@ int launch_fwd(const MdcnArgs &a, int packed, hipStream_t st) {
     }
   } else {
     switch (co_t) {
-      case 16: launch_fwd_t<MODE, 16, 64>(a, packed, grid, st); break;
+      case 16: break;  // unreachable: 16-channel tiles always take 128-pixel tiles
       case 32: launch_fwd_t<MODE, 32, 64>(a, packed, grid, st); break;
       default: launch_fwd_t<MODE, 64, 64>(a, packed, grid, st); break;
     }
