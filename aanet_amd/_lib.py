@@ -29,13 +29,13 @@ _SIGNATURES = {
     "aanet_disp_regress_f32": [_P, _P, _I, _I, _I, _I, _I, _P],
     "aanet_disp_regress_bwd_f32": [_P, _P, _P, _I, _I, _I, _I, _I, _P],
     "aanet_mdcn_fwd_f32": [_P, _P, _P, _P, _P, _P] + [_I] * 12 + [_P],
-    "aanet_mdcn_fwd_fused_f32": [_P, _P, _L, _P, _L, _I, _F, _P, _I, _P, _P, _P, _I, _P] + [_I] * 12 + [_P],
+    "aanet_mdcn_fwd_fused_f32": [_P, _P, _L, _P, _L, _I, _F, _P, _I, _P, _P, _P, _I, _P] + [_I] * 13 + [_P],
     "aanet_mdcn_bwd_f32": [_P] * 10 + [_I] * 12 + [_P],
-    "aanet_conv2d_fused_f32": [_P] * 6 + [_I, _I, _P] + [_I] * 11 + [_P],
+    "aanet_conv2d_fused_f32": [_P] * 6 + [_I, _I, _P] + [_I] * 12 + [_P],
     "aanet_conv_weight_pack_f32": [_P, _P, _I, _I, _I, _I, _P],
-    "aanet_conv2d_pw_f32": [_P] * 5 + [_I] + [_P] * 3 + [_I, _I, _P] + [_I] * 10 + [_P],
+    "aanet_conv2d_pw_f32": [_P] * 5 + [_I] + [_P] * 3 + [_I, _I, _P] + [_I] * 11 + [_P],
     "aanet_mdcn_pw_f32": [_P, _P, _L, _P, _L, _I, _F, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _P]
-    + [_I] * 11 + [_P],
+    + [_I] * 12 + [_P],
     "aanet_csa_sum_f32": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P],
     "aanet_mdcn_im2col_f32": [_P, _P, _P, _P] + [_I] * 9 + [_P],
     "aanet_mdcn_sample_index": [_P, _P, _P, _P] + [_I] * 9 + [_P],
@@ -83,12 +83,22 @@ def ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+def is_nhwc(t):
+    """channels_last 4-D tensor that is not also NCHW-contiguous (physical layout NHWC)."""
+    return (t is not None and t.dim() == 4 and not t.is_contiguous()
+            and t.is_contiguous(memory_format=torch.channels_last))
+
+
+LAYOUT_IN_NHWC, LAYOUT_OUT_NHWC = 1, 2  # AANET_LAYOUT_* (include/aanet_mi355x.h)
+
+
 def stream_of(t):
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
-def require_gpu(*tensors, names=None):
-    """fp32, contiguous, on the same ROCm device: the C ABI takes raw NCHW pointers."""
+def require_gpu(*tensors, names=None, nhwc_ok=()):
+    """fp32, contiguous, on the same ROCm device: the C ABI takes raw NCHW pointers.  Tensors at
+    the positions in nhwc_ok may instead be channels_last (physically NHWC, AANET_LAYOUT_*)."""
     dev = None
     for i, t in enumerate(tensors):
         if t is None:
@@ -99,7 +109,7 @@ def require_gpu(*tensors, names=None):
                 f"aanet_amd ops run only on the MI355X (HIP) device; {nm} is on {t.device}")
         if t.dtype != torch.float32:
             raise TypeError(f"aanet_amd ops compute in fp32; {nm} is {t.dtype}")
-        if not t.is_contiguous():
+        if not (t.is_contiguous() or (i in nhwc_ok and is_nhwc(t))):
             raise ValueError(f"{nm} must be contiguous")
         if dev is None:
             dev = t.device

@@ -45,6 +45,7 @@ struct MdcnArgs {
   int tail_act, Co2;
   float *out;
   int N, C, H, W, Co, kh, kw, stride, pad, dil, groups, dg, Ho, Wo;
+  int layout;  // AANET_LAYOUT_* bits (conv engine only)
 };
 
 // Bilinear sampling state of one (pixel, tap, deformable group).  Invalid corners get
@@ -270,10 +271,34 @@ __device__ __forceinline__ void make_sampw(SampW &s, float h, float w, int H, in
   s.wb = f2v{wab, wbb} * m;
 }
 
+// NHWC sampling state: byte offsets of the 4 corners (`oob` for an invalid corner: the buffer
+// range check reads it as 0) and their weights with the mask folded in.  Same validity rules
+// and corner indices as make_samp (kernel.cu:467-497).
+__device__ __forceinline__ void make_samp4(int o[4], f32x4 &wv, float h, float w, int H, int W,
+                                           int rowb, int oob, float m) {
+#pragma clang fp contract(off)
+  const bool valid = h > -1.f && w > -1.f && h < (float)H && w < (float)W;
+  const int hl = (int)floorf(h), wl = (int)floorf(w);
+  const float lh = h - (float)hl, lw = w - (float)wl;
+  const float hh = 1.f - lh, hw = 1.f - lw;
+  const bool ok1 = valid && hl >= 0 && wl >= 0;
+  const bool ok2 = valid && hl >= 0 && wl + 1 <= W - 1;
+  const bool ok3 = valid && hl + 1 <= H - 1 && wl >= 0;
+  const bool ok4 = valid && hl + 1 <= H - 1 && wl + 1 <= W - 1;
+  wv = f32x4{ok1 ? hh * hw : 0.f, ok2 ? hh * lw : 0.f, ok3 ? lh * hw : 0.f, ok4 ? lh * lw : 0.f} * m;
+  o[0] = ok1 ? (hl * W + wl) * rowb : oob;
+  o[1] = ok2 ? (hl * W + wl + 1) * rowb : oob;
+  o[2] = ok3 ? ((hl + 1) * W + wl) * rowb : oob;
+  o[3] = ok4 ? ((hl + 1) * W + wl + 1) * rowb : oob;
+}
+
 // FULL: every chunk holds KC channels (Cg % KC == 0, and cpg % KC == 0 for the DCN), so the
 // staging code has no per-row guards.  Those guards are wave-uniform, and the compiler turns
 // them into scalar branches, which split the loop body and defeat the MFMA/staging interleave.
-template <int MODE, int CO_T, int PTT, int PACKED, int TAIL, int SCHED, int FULL, int ABLATE = 0>
+// LAYOUT bit 0: input NHWC (channels-last; each staging item is one 16-byte load of 4 channels
+// at one position, so a DCN corner or a conv tap of 32 channels is 8 lanes x 16 B = one 128-B
+// line; needs FULL).  Bit 1: output NHWC.
+template <int MODE, int CO_T, int PTT, int PACKED, int TAIL, int SCHED, int FULL, int LAYOUT>
 __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   constexpr int WC = CO_T >= 32 ? 2 : 1;   // waves along the output channels
   constexpr int WP = FNT / 64 / WC;        // waves along the pixels
@@ -282,6 +307,10 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   constexpr int CPT = KC * PTT / FNT;      // im2col values staged per thread per chunk
   constexpr int WPT = KC * CO_T / FNT;     // weights staged per thread per chunk
   static_assert(NCB >= 1 && NPB >= 1 && WPT >= 1 && CPT % 4 == 0, "tile shape");
+  constexpr bool INH = (LAYOUT & 1) != 0, ONH = (LAYOUT & 2) != 0;
+  constexpr int NIT = INH ? PTT * (KC / 4) / FNT : 1;  // NHWC staging items per thread
+  static_assert(!INH || (FULL && NIT >= 1 && FNT % (KC / 4) == 0), "NHWC staging needs full chunks");
+  static_assert(!(ONH && TAIL), "NHWC output with a pointwise tail is not instantiated");
   constexpr int BUF = (PTT + CO_T) * SP; // floats per LDS buffer
   constexpr int OP = PTT + 4;            // epilogue tile pitch
   static_assert(CO_T * OP <= 2 * BUF, "epilogue tile must fit the staging buffers");
@@ -320,6 +349,22 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   const bool pvalid = p < P;
   const int ho = pvalid ? (int)(p / a.Wo) : 0, wo = pvalid ? (int)(p % a.Wo) : 0;
   const long psafe = pvalid ? p : 0;
+  // NHWC staging roles: lane quad nq = channels 4nq..4nq+3, pixels npx[i]
+  const int nq = tid & (KC / 4 - 1);
+  int npx[NIT], nho[NIT], nwo[NIT];
+  bool nval[NIT];
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {
+    npx[i] = tid / (KC / 4) + (FNT / (KC / 4)) * i;
+    const long pp = (long)tile * PTT + npx[i];
+    nval[i] = pp < P;
+    nho[i] = nval[i] ? (int)(pp / a.Wo) : 0;
+    nwo[i] = nval[i] ? (int)(pp % a.Wo) : 0;
+  }
+  f32x4 nv[INH && MODE == 0 ? NIT : 1];        // conv tap values (NHWC)
+  f32x4 nc[INH && MODE ? NIT : 1][4];          // DCN corner values (NHWC)
+  int noff[INH && MODE ? NIT : 1][4];          // DCN corner byte offsets (NHWC)
+  f32x4 nw[INH && MODE ? NIT : 1];             // DCN corner weights (mask folded)
 
   float wreg[WPT];
   float vraw[MODE ? 1 : CPT];
@@ -360,14 +405,37 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     if (!pvalid) m = 0.f;
     const float h = (float)(ho * a.stride - a.pad + i * a.dil) + off_h;
     const float w = (float)(wo * a.stride - a.pad + j * a.dil) + off_w;
-    SampW sw;
-    make_sampw(sw, h, w, a.H, a.W, m);
     float *d = smem + 2 * BUF + slot * PSLOT + spx * 8;
-    *reinterpret_cast<f32x4 *>(d) = f32x4{__builtin_bit_cast(float, sw.ot),
-                                          __builtin_bit_cast(float, sw.ob), sw.wt.x, sw.wt.y};
-    *reinterpret_cast<f2v *>(d + 4) = sw.wb;
+    if constexpr (INH) {
+      int o[4];
+      f32x4 wv;
+      make_samp4(o, wv, h, w, a.H, a.W, a.C * 4, img_bytes, m);
+      *reinterpret_cast<f32x4 *>(d) = f32x4{__builtin_bit_cast(float, o[0]), __builtin_bit_cast(float, o[1]),
+                                            __builtin_bit_cast(float, o[2]), __builtin_bit_cast(float, o[3])};
+      *reinterpret_cast<f32x4 *>(d + 4) = wv;
+    } else {
+      SampW sw;
+      make_sampw(sw, h, w, a.H, a.W, m);
+      *reinterpret_cast<f32x4 *>(d) = f32x4{__builtin_bit_cast(float, sw.ot),
+                                            __builtin_bit_cast(float, sw.ob), sw.wt.x, sw.wt.y};
+      *reinterpret_cast<f2v *>(d + 4) = sw.wb;
+    }
   };
   auto get_params = [&](int slot) {
+    if constexpr (INH) {
+#pragma unroll
+      for (int i = 0; i < NIT; ++i) {
+        const float *d = smem + 2 * BUF + slot * PSLOT + npx[i] * 8;
+        const f32x4 q = *reinterpret_cast<const f32x4 *>(d);
+        const float q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];  // see below
+        noff[i][0] = __builtin_bit_cast(int, q0);
+        noff[i][1] = __builtin_bit_cast(int, q1);
+        noff[i][2] = __builtin_bit_cast(int, q2);
+        noff[i][3] = __builtin_bit_cast(int, q3);
+        nw[i] = *reinterpret_cast<const f32x4 *>(d + 4);
+      }
+      return;
+    }
     const float *d = smem + 2 * BUF + slot * PSLOT + spx * 8;
     const f32x4 q = *reinterpret_cast<const f32x4 *>(d);
     // copy the elements to scalars first: __builtin_bit_cast of an ext-vector element lvalue
@@ -379,25 +447,33 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     snext.wb = *reinterpret_cast<const f2v *>(d + 4);
   };
   auto issue_loads = [&](const ChunkIt &c) {
-    if (ABLATE == 1) return;
-    if (ABLATE == 4) {  // no global loads: LDS writes of register constants
-#pragma unroll
-      for (int i = 0; i < WPT; ++i) wreg[i] = (float)i;
-      if (MODE == 0) {
-#pragma unroll
-        for (int e = 0; e < CPT; ++e) vraw[e] = (float)e;
-      } else {
-#pragma unroll
-        for (int e = 0; e < CPT; ++e) traw[e] = braw[e] = i2v{e, e};
-      }
-      return;
-    }
     const int rows = c.c1 - c.c0;
     const int wbase = PACKED ? (((c.k * a.Co + co0) * Cg + (c.c0 - cbeg)) * 4)
                              : (((co0 * Cg + (c.c0 - cbeg)) * K + c.k) * 4);
 #pragma unroll
     for (int i = 0; i < WPT; ++i)
       wreg[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, wlane[i], wbase, 0));
+    if constexpr (INH) {
+      const int soff = __builtin_amdgcn_readfirstlane(c.c0 * 4);
+      if (MODE == 0) {
+#pragma unroll
+        for (int i = 0; i < NIT; ++i) {
+          const int hi = nho[i] * a.stride - a.pad + (c.k / a.kw) * a.dil;
+          const int wi = nwo[i] * a.stride - a.pad + (c.k % a.kw) * a.dil;
+          const bool ok = nval[i] && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+          const int voff = ok ? (hi * a.W + wi) * (a.C * 4) + nq * 16 : img_bytes;
+          nv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, voff, soff, 0));
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NIT; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            nc[i][j] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, noff[i][j] + nq * 16, soff, 0));
+      }
+      return;
+    }
     const int cbase = __builtin_amdgcn_readfirstlane((c.c0 + scb) * plane_bytes);
     if (MODE == 0) {
       const int hi = ho * a.stride - a.pad + (c.k / a.kw) * a.dil;
@@ -421,25 +497,28 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     }
   };
   auto store_stage = [&](const ChunkIt &c, int buf) {
-    if (ABLATE == 1) return;
-    if (ABLATE == 3) {  // loads kept alive, no LDS writes
-#pragma unroll
-      for (int i = 0; i < WPT; ++i) asm volatile("" ::"v"(wreg[i]));
-      if (MODE == 0) {
-#pragma unroll
-        for (int e = 0; e < CPT; ++e) asm volatile("" ::"v"(vraw[e]));
-      } else {
-#pragma unroll
-        for (int e = 0; e < CPT; ++e) asm volatile("" ::"v"(traw[e]), "v"(braw[e]));
-      }
-      return;
-    }
     float *sC = smem + buf * BUF, *sW = sC + PTT * SP;
     const int rows = c.c1 - c.c0;
 #pragma unroll
     for (int i = 0; i < WPT; ++i) {
       const int e = tid + FNT * i;
       sW[(e / KC) * SP + e % KC] = wreg[i];
+    }
+    if constexpr (INH) {
+#pragma unroll
+      for (int i = 0; i < NIT; ++i) {
+        f32x4 v;
+        if (MODE == 0) {
+          v = nv[i];
+        } else {
+          v = nc[i][0] * nw[i][0];
+          v = __builtin_elementwise_fma(nc[i][1], f32x4(nw[i][1]), v);
+          v = __builtin_elementwise_fma(nc[i][2], f32x4(nw[i][2]), v);
+          v = __builtin_elementwise_fma(nc[i][3], f32x4(nw[i][3]), v);
+        }
+        *reinterpret_cast<f32x4 *>(sC + npx[i] * SP + 4 * nq) = v;
+      }
+      return;
     }
     float v[CPT];
 #pragma unroll
@@ -508,10 +587,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       for (int m = 0; m < NCB; ++m)
 #pragma unroll
         for (int b = 0; b < NPB; ++b) {
-          if (ABLATE == 2)
-            acc[m][b] += f.A[m][s4] * f.B[b][s4];  // keeps the LDS reads live, no matrix pipe
-          else
-            acc[m][b] = mfma16x16x4(f.A[m][s4], f.B[b][s4], acc[m][b]);
+          acc[m][b] = mfma16x16x4(f.A[m][s4], f.B[b][s4], acc[m][b]);
         }
   };
   auto mfma_half = [&](int buf, int h) {
@@ -622,6 +698,27 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
         sO[(16 * (wc0 + m) + 4 * kr + r) * OP + 16 * (wp0 + b) + jj] = acc[m][b][r];
   __syncthreads();
   const long p0 = (long)tile * PTT;
+  if constexpr (ONH) {  // [px][co] rows of 16-byte channel quads
+    constexpr int CQ = CO_T / 4;
+    for (int e = tid; e < PTT * CQ; e += FNT) {
+      const int px = e / CQ, cq = e % CQ, co = co0 + 4 * cq;
+      const long pe = p0 + px;
+      if (co >= co_end || pe >= P) continue;
+      f32x4 v;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float t = sO[(4 * cq + u) * OP + px] + (a.bias ? a.bias[co + u] : 0.f);
+        if (a.post_scale) t = t * a.post_scale[co + u] + a.post_shift[co + u];
+        v[u] = t;
+      }
+      const long o = ((long)n * P + pe) * a.Co + co;
+      if (a.residual) v += *reinterpret_cast<const f32x4 *>(a.residual + o);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = apply_act(v[u], a.act);
+      *reinterpret_cast<f32x4 *>(a.out + o) = v;
+    }
+    return;
+  }
   const bool vec = (P & 3) == 0;
   constexpr int QPR = PTT / 4;  // float4 per tile row
   const int cout = TAIL ? a.Co2 : a.Co;
@@ -943,6 +1040,7 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
   a.dil = dil;
   a.groups = groups;
   a.dg = dg;
+  a.layout = 0;
   a.Ho = conv_out_size(h, kh, stride, pad, dil);
   a.Wo = conv_out_size(w, kw, stride, pad, dil);
   const long P = (long)a.Ho * a.Wo, K = (long)kh * kw;
@@ -953,21 +1051,21 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
 
 template <int MODE, int CO_T, int PTT, int FULL>
 void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
+  const dim3 blk(FNT);
   if (a.tail_w) {
-    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1, FULL>), grid, dim3(FNT), 0, st, a);
+    if (FULL && a.layout == 1)
+      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1, FULL, FULL ? 1 : 0>), grid, blk, 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1, FULL, 0>), grid, blk, 0, st, a);
   } else if (packed) {
-    // AANET_ABLATE=1..4 selects the staging ablations (tools/ab_ablate.sh); default 0
-    static const int abl = [] { const char *e = getenv("AANET_ABLATE"); return e ? atoi(e) : 0; }();
-    if (FULL && CO_T == 64 && PTT == 128 && abl >= 1 && abl <= 4) {
-      if (abl == 1) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 1>), grid, dim3(FNT), 0, st, a);
-      if (abl == 2) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 2>), grid, dim3(FNT), 0, st, a);
-      if (abl == 3) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 3>), grid, dim3(FNT), 0, st, a);
-      if (abl == 4) hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 4>), grid, dim3(FNT), 0, st, a);
-    } else {
-      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL>), grid, dim3(FNT), 0, st, a);
+    switch (FULL ? a.layout : 0) {
+      case 1: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, FULL ? 1 : 0>), grid, blk, 0, st, a); break;
+      case 2: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 2>), grid, blk, 0, st, a); break;
+      case 3: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, FULL ? 3 : 2>), grid, blk, 0, st, a); break;
+      default: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 0>), grid, blk, 0, st, a); break;
     }
   } else {
-    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 0, 0, 0, FULL>), grid, dim3(FNT), 0, st, a);
+    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 0, 0, 0, FULL, 0>), grid, blk, 0, st, a);
   }
 }
 
@@ -990,6 +1088,12 @@ int launch_fwd(const MdcnArgs &a, int packed, hipStream_t st) {
   if (a.post_scale && !a.post_shift) return AANET_EINVAL;
   const long P = (long)a.Ho * a.Wo;
   const int Cog = a.Co / a.groups;
+  if (a.layout < 0 || a.layout > 3) return AANET_EINVAL;
+  if (a.layout) {  // NHWC paths: packed weights, full 32-channel chunks, 4-channel quads
+    const int Cg = a.C / a.groups, cpg = a.C / a.dg;
+    if (!packed || Cg % KC || (MODE && cpg % KC) || a.C % 4) return AANET_EUNSUPPORTED;
+    if ((a.layout & 2) && (a.tail_w || Cog % 4)) return AANET_EUNSUPPORTED;
+  }
   int co_t = Cog <= 16 ? 16 : (Cog <= 32 ? 32 : 64);
   if (a.tail_w) {  // the whole conv output column of a pixel must sit in one workgroup
     if (a.groups != 1 || a.Co > 64 || a.Co2 <= 0 || a.Co2 > 64 || !packed) return AANET_EUNSUPPORTED;
@@ -1048,12 +1152,13 @@ extern "C" int aanet_conv2d_fused_f32(const float *x, const float *weight, const
                                       const float *post_scale, const float *post_shift,
                                       const float *residual, int act, int weight_packed,
                                       float *out, int n, int c, int h, int w, int co, int kh,
-                                      int kw, int stride, int pad, int dil, int groups,
+                                      int kw, int stride, int pad, int dil, int groups, int layout,
                                       aanet_stream_t stream) {
   if (act < 0 || act > 2) return AANET_EINVAL;
   MdcnArgs a = make_args(x, nullptr, 0, nullptr, 0, 0, 1.f, weight, bias, post_scale, post_shift,
                          act, out, n, c, h, w, co, kh, kw, stride, pad, dil, groups, 1);
   a.residual = residual;
+  a.layout = layout;
   return launch_fwd<0>(a, weight_packed, as_hip(stream));
 }
 
@@ -1062,10 +1167,12 @@ extern "C" int aanet_conv2d_pw_f32(const float *x, const float *weight_packed, c
                                    const float *pw_weight_packed, const float *pw_bias,
                                    const float *residual, int pw_act, int co2, float *out, int n,
                                    int c, int h, int w, int co, int kh, int kw, int stride,
-                                   int pad, int dil, aanet_stream_t stream) {
+                                   int pad, int dil, int layout, aanet_stream_t stream) {
   if (act < 0 || act > 2 || pw_act < 0 || pw_act > 2 || !pw_weight_packed) return AANET_EINVAL;
+  if (layout != 0 && layout != 1) return AANET_EINVAL;
   MdcnArgs a = make_args(x, nullptr, 0, nullptr, 0, 0, 1.f, weight_packed, bias, post_scale,
                          post_shift, act, out, n, c, h, w, co, kh, kw, stride, pad, dil, 1, 1);
+  a.layout = layout;
   a.tail_w = pw_weight_packed;
   a.tail_b = pw_bias;
   a.tail_act = pw_act;
@@ -1081,11 +1188,13 @@ extern "C" int aanet_mdcn_pw_f32(const float *x, const float *offset, long offse
                                  const float *pw_weight_packed, const float *pw_bias,
                                  const float *residual, int pw_act, int co2, float *out, int n,
                                  int c, int h, int w, int co, int kh, int kw, int stride, int pad,
-                                 int dil, int dg, aanet_stream_t stream) {
+                                 int dil, int dg, int layout, aanet_stream_t stream) {
   if (act < 0 || act > 2 || pw_act < 0 || pw_act > 2 || !pw_weight_packed) return AANET_EINVAL;
+  if (layout != 0 && layout != 1) return AANET_EINVAL;
   MdcnArgs a = make_args(x, offset, offset_batch_stride, mask, mask_batch_stride, mask_logits,
                          mask_scale, weight_packed, bias, post_scale, post_shift, act, out, n, c,
                          h, w, co, kh, kw, stride, pad, dil, 1, dg);
+  a.layout = layout;
   a.tail_w = pw_weight_packed;
   a.tail_b = pw_bias;
   a.tail_act = pw_act;
@@ -1101,11 +1210,12 @@ extern "C" int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset,
                                         const float *post_scale, const float *post_shift, int act,
                                         float *out, int n, int c, int h, int w, int co, int kh,
                                         int kw, int stride, int pad, int dil, int groups, int dg,
-                                        aanet_stream_t stream) {
+                                        int layout, aanet_stream_t stream) {
   if (act < 0 || act > 2) return AANET_EINVAL;
   MdcnArgs a = make_args(x, offset, offset_batch_stride, mask, mask_batch_stride, mask_logits,
                          mask_scale, weight, bias, post_scale, post_shift, act, out, n, c, h, w,
                          co, kh, kw, stride, pad, dil, groups, dg);
+  a.layout = layout;
   return launch_fwd<1>(a, weight_packed, as_hip(stream));
 }
 

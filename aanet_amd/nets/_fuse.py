@@ -7,6 +7,7 @@ op sequence with autograd.
 import torch
 
 from .. import ops
+from .._lib import is_nhwc
 
 
 def bn_scale_shift(bn):
@@ -60,14 +61,17 @@ def _int(v):
     return v[0] if isinstance(v, (tuple, list)) else v
 
 
-def conv_bn_act(x, conv, bn=None, act=None, residual=None):
-    """act(BN(conv(x)) [+ residual]) as ONE HIP kernel (BN folded into the conv)."""
+def conv_bn_act(x, conv, bn=None, act=None, residual=None, out_nhwc=False):
+    """act(BN(conv(x)) [+ residual]) as ONE HIP kernel (BN folded into the conv).  A channels_last
+    x is read as NHWC in place; out_nhwc=True returns a channels_last (NHWC) tensor."""
     w, b, wp = folded(conv, bn)
     for v in (conv.stride, conv.padding, conv.dilation):
         if isinstance(v, (tuple, list)) and v[0] != v[1]:
             raise NotImplementedError("asymmetric conv parameters")
-    return ops.conv2d_fused(x.contiguous(), w, b, _int(conv.stride), _int(conv.padding),
-                            _int(conv.dilation), conv.groups, act, residual, packed_weight=wp)
+    xin = x if is_nhwc(x) else x.contiguous()
+    return ops.conv2d_fused(xin, w, b, _int(conv.stride), _int(conv.padding),
+                            _int(conv.dilation), conv.groups, act, residual, packed_weight=wp,
+                            out_nhwc=out_nhwc)
 
 
 def use_fused(module, x):

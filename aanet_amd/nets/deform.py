@@ -104,17 +104,30 @@ class _BottleneckBase(nn.Module):
 
     def _forward_fused(self, x, deform, conv1_out=None):
         """conv1+bn1+relu, then conv2+bn2+relu -> conv3+bn3 (+identity) + relu as ONE HIP kernel
-        (the conv3 GEMM runs in conv2's epilogue).  conv1_out: precomputed conv1 branch."""
-        out = conv_bn_act(x, self.conv1, self.bn1, "relu") if conv1_out is None else conv1_out
-        identity = (self.downsample(x) if self.downsample is not None else x).contiguous()
+        (the conv3 GEMM runs in conv2's epilogue).  When the tail kernel takes the block, conv1
+        writes its output channels-last (NHWC) so that conv2 / offset_conv / the DCN read each
+        32-channel chunk of a position as one 128-byte line.  conv1_out: precomputed conv1."""
         w3, b3, p3 = folded(self.conv3, self.bn3)
+        width = self.conv1.weight.shape[0]
+        c2 = self.conv2
+        if deform:
+            pw = c2.modulation and c2.deform_conv.stride == 1 and width <= 64 and w3.shape[0] <= 64
+            nhwc = pw and width % 32 == 0 and (width // c2.deformable_groups) % 32 == 0
+        else:
+            pw = c2.groups == 1 and width <= 64 and w3.shape[0] <= 64 and \
+                c2.stride[0] == c2.stride[1] and c2.padding[0] == c2.padding[1]
+            nhwc = pw and width % 32 == 0
+        if conv1_out is None:
+            out = conv_bn_act(x, self.conv1, self.bn1, "relu", out_nhwc=nhwc)
+        else:
+            out = conv1_out
+        identity = (self.downsample(x) if self.downsample is not None else x).contiguous()
         if deform and self.conv2.modulation:
-            c2 = self.conv2
             dc = c2.deform_conv
             offset_mask = conv_bn_act(out, c2.offset_conv)
             ps, psh = bn_affine(self.bn2)
             _, _, wp = folded(dc, None)
-            if dc.stride == 1 and self.conv3.weight.shape[1] <= 64 and w3.shape[0] <= 64:
+            if pw:
                 return ops.mdcn_pw(out, offset_mask, dc.weight, wp, dc.bias, ps, psh, "relu", p3, b3,
                                    identity, "relu", dc.stride, dc.padding, dc.dilation,
                                    c2.deformable_groups, 2.0 if c2.double_mask else 1.0)
@@ -123,11 +136,9 @@ class _BottleneckBase(nn.Module):
             out = F.relu_(self.bn2(self.conv2(out)))
         else:
             w2, b2, p2 = folded(self.conv2, self.bn2)
-            cv = self.conv2
-            if cv.groups == 1 and w2.shape[0] <= 64 and w3.shape[0] <= 64 and \
-                    cv.stride[0] == cv.stride[1] and cv.padding[0] == cv.padding[1]:
+            if pw:
                 return ops.conv2d_pw(out, w2, p2, b2, None, None, "relu", p3, b3, identity, "relu",
-                                     cv.stride[0], cv.padding[0], cv.dilation[0])
+                                     c2.stride[0], c2.padding[0], c2.dilation[0])
             out = conv_bn_act(out, self.conv2, self.bn2, "relu")
         return conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity)
 

@@ -138,10 +138,12 @@ def mdcn_forward_fused(x, offset_mask, weight, bias=None, post_scale=None, post_
     offsets, the rest mask logits (m = mask_scale * sigmoid), read in place (no slicing copies).
     """
     require_gpu(x, offset_mask, weight, bias, post_scale, post_shift, packed_weight,
-                names=("input", "offset_mask", "weight", "bias", "post_scale", "post_shift", "packed"))
+                names=("input", "offset_mask", "weight", "bias", "post_scale", "post_shift", "packed"),
+                nhwc_ok=(0,))
     N, C, H, W = x.shape
     Co, _, kh, kw = weight.shape
     K = kh * kw
+    layout = _lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0
     Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
     if offset_mask.shape != (N, deformable_groups * 3 * K, Ho, Wo):
         raise ValueError(f"offset_mask shape {tuple(offset_mask.shape)} unexpected")
@@ -153,7 +155,7 @@ def mdcn_forward_fused(x, offset_mask, weight, bias=None, post_scale=None, post_
          bs, 1, float(mask_scale), ptr(wsrc), int(packed_weight is not None), ptr(bias),
          ptr(post_scale), ptr(post_shift),
          ACT[act] if not isinstance(act, int) else act, ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation, 1,
-         deformable_groups, stream_of(x))
+         deformable_groups, layout, stream_of(x))
     return out
 
 
@@ -170,29 +172,39 @@ def pack_weight(weight):
 
 
 def conv2d_fused(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None,
-                 residual=None, post_scale=None, post_shift=None, packed_weight=None):
+                 residual=None, post_scale=None, post_shift=None, packed_weight=None,
+                 out_nhwc=False):
     """Plain conv on the HIP implicit-GEMM engine: act(post_scale*(conv+bias)+post_shift+residual).
     weight gives the shape ([co][cg][kh][kw]); packed_weight (pack_weight(weight)) if given is
-    what the kernel reads."""
+    what the kernel reads.  x may be channels_last (NHWC staging); out_nhwc=True returns a
+    channels_last tensor (residual then channels_last too).  NHWC needs packed_weight and
+    32-channel groups (AANET_LAYOUT_*)."""
     require_gpu(x, weight, bias, residual, post_scale, post_shift, packed_weight,
-                names=("input", "weight", "bias", "residual", "post_scale", "post_shift", "packed"))
+                names=("input", "weight", "bias", "residual", "post_scale", "post_shift", "packed"),
+                nhwc_ok=(0, 3) if out_nhwc else (0,))
     N, C, H, W = x.shape
     Co, _, kh, kw = weight.shape
     Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
     if residual is not None and tuple(residual.shape) != (N, Co, Ho, Wo):
         raise ValueError("residual shape must match the output")
-    out = torch.empty((N, Co, Ho, Wo), device=x.device, dtype=x.dtype)
+    layout = (_lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0) | (_lib.LAYOUT_OUT_NHWC if out_nhwc else 0)
+    if residual is not None and out_nhwc and not (_lib.is_nhwc(residual) or Co == 1):
+        raise ValueError("residual must be channels_last when out_nhwc=True")
+    out = torch.empty((N, Co, Ho, Wo), device=x.device, dtype=x.dtype,
+                      memory_format=torch.channels_last if out_nhwc else torch.contiguous_format)
     wsrc = packed_weight if packed_weight is not None else weight
     call("aanet_conv2d_fused_f32", ptr(x), ptr(wsrc), ptr(bias), ptr(post_scale), ptr(post_shift),
          ptr(residual), ACT[act], int(packed_weight is not None), ptr(out), N, C, H, W, Co, kh, kw,
-         stride, padding, dilation, groups, stream_of(x))
+         stride, padding, dilation, groups, layout, stream_of(x))
     return out
 
 
 def conv2d_pw(x, weight, packed_weight, bias, post_scale, post_shift, act, pw_packed, pw_bias,
               residual=None, pw_act=None, stride=1, padding=0, dilation=1):
-    """Plain conv + fused pointwise tail (bottleneck conv2 -> conv3, aanet_conv2d_pw_f32)."""
-    require_gpu(x, packed_weight, bias, post_scale, post_shift, pw_packed, pw_bias, residual)
+    """Plain conv + fused pointwise tail (bottleneck conv2 -> conv3, aanet_conv2d_pw_f32).
+    x may be channels_last (NHWC staging); the output is NCHW."""
+    require_gpu(x, packed_weight, bias, post_scale, post_shift, pw_packed, pw_bias, residual,
+                nhwc_ok=(0,))
     N, C, H, W = x.shape
     Co, _, kh, kw = weight.shape
     Co2 = pw_packed.shape[-2]
@@ -200,16 +212,18 @@ def conv2d_pw(x, weight, packed_weight, bias, post_scale, post_shift, act, pw_pa
     out = torch.empty((N, Co2, Ho, Wo), device=x.device, dtype=x.dtype)
     call("aanet_conv2d_pw_f32", ptr(x), ptr(packed_weight), ptr(bias), ptr(post_scale),
          ptr(post_shift), ACT[act], ptr(pw_packed), ptr(pw_bias), ptr(residual), ACT[pw_act], Co2,
-         ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation, stream_of(x))
+         ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation,
+         _lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0, stream_of(x))
     return out
 
 
 def mdcn_pw(x, offset_mask, weight, packed_weight, bias, post_scale, post_shift, act, pw_packed,
             pw_bias, residual=None, pw_act=None, stride=1, padding=0, dilation=1,
             deformable_groups=1, mask_scale=2.0):
-    """DCN (offset/mask read in place from offset_conv's output) + fused pointwise tail."""
+    """DCN (offset/mask read in place from offset_conv's output) + fused pointwise tail.
+    x may be channels_last (NHWC corner loads); the output is NCHW."""
     require_gpu(x, offset_mask, packed_weight, bias, post_scale, post_shift, pw_packed, pw_bias,
-                residual)
+                residual, nhwc_ok=(0,))
     N, C, H, W = x.shape
     Co, _, kh, kw = weight.shape
     K = kh * kw
@@ -223,7 +237,8 @@ def mdcn_pw(x, offset_mask, weight, packed_weight, bias, post_scale, post_shift,
     call("aanet_mdcn_pw_f32", ptr(x), ptr(offset_mask), bs, _lib.ctypes.c_void_p(mask_ptr), bs, 1,
          float(mask_scale), ptr(packed_weight), ptr(bias), ptr(post_scale), ptr(post_shift),
          ACT[act], ptr(pw_packed), ptr(pw_bias), ptr(residual), ACT[pw_act], Co2, ptr(out), N, C,
-         H, W, Co, kh, kw, stride, padding, dilation, deformable_groups, stream_of(x))
+         H, W, Co, kh, kw, stride, padding, dilation, deformable_groups,
+         _lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0, stream_of(x))
     return out
 
 

@@ -27,6 +27,16 @@ enum {
   AANET_EUNSUPPORTED = -2 /* valid for the reference but outside what this build implements */
 };
 
+/* Activation layouts of the conv engine (the `layout` argument of the fused entry points).
+ * NHWC ("channels-last") intermediates let a 32-channel chunk at one position be read as one
+ * 128-byte line (8 lanes x 16 B); the bottleneck keeps its conv1 output in NHWC.  NHWC needs
+ * packed weights and 32-channel groups (c/groups % 32 == 0, and c/dg % 32 == 0 for the DCN). */
+enum {
+  AANET_LAYOUT_NCHW = 0,
+  AANET_LAYOUT_IN_NHWC = 1,  /* x is [n][h][w][c] */
+  AANET_LAYOUT_OUT_NHWC = 2  /* out (and residual) are [n][ho][wo][co] */
+};
+
 int aanet_version(void);
 const char *aanet_status_string(int status);
 
@@ -100,7 +110,8 @@ int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset, long offset_ba
                              const float *bias,
                              const float *post_scale, const float *post_shift, int act, float *out,
                              int n, int c, int h, int w, int co, int kh, int kw, int stride,
-                             int pad, int dil, int groups, int dg, aanet_stream_t stream);
+                             int pad, int dil, int groups, int dg, int layout,
+                             aanet_stream_t stream);
 
 /* Plain convolution on the same implicit-GEMM engine, for the eval fast path of every other
  * conv in the ISA/CSA blocks (nets/deform.py:6-14 conv1x1/conv3x3, nets/deform.py:70-72
@@ -112,7 +123,7 @@ int aanet_conv2d_fused_f32(const float *x, const float *weight, const float *bia
                            const float *post_scale, const float *post_shift, const float *residual,
                            int act, int weight_packed, float *out, int n, int c, int h, int w,
                            int co, int kh, int kw, int stride, int pad, int dil, int groups,
-                           aanet_stream_t stream);
+                           int layout, aanet_stream_t stream);
 
 /* Bottleneck tail fusion (nets/deform.py:171-184 / 223-236 in eval): the pointwise conv3
  * (+ folded BN3) runs in the epilogue of conv2, so the conv2 activation never goes to HBM:
@@ -120,20 +131,21 @@ int aanet_conv2d_fused_f32(const float *x, const float *weight, const float *bia
  *   out = pw_act(pw_weight . t + pw_bias + residual)                     [co2 channels]
  * weight_packed / pw_weight_packed in the aanet_conv_weight_pack_f32 layout ([co2][co] for the
  * pointwise one).  Requires groups == 1, co <= 64, co2 <= 64.  The _mdcn_ form takes the
- * deformable sampler arguments of aanet_mdcn_fwd_fused_f32. */
+ * deformable sampler arguments of aanet_mdcn_fwd_fused_f32.  layout: AANET_LAYOUT_NCHW or
+ * AANET_LAYOUT_IN_NHWC (the output is NCHW). */
 int aanet_conv2d_pw_f32(const float *x, const float *weight_packed, const float *bias,
                         const float *post_scale, const float *post_shift, int act,
                         const float *pw_weight_packed, const float *pw_bias,
                         const float *residual, int pw_act, int co2, float *out, int n, int c,
                         int h, int w, int co, int kh, int kw, int stride, int pad, int dil,
-                        aanet_stream_t stream);
+                        int layout, aanet_stream_t stream);
 int aanet_mdcn_pw_f32(const float *x, const float *offset, long offset_batch_stride,
                       const float *mask, long mask_batch_stride, int mask_logits,
                       float mask_scale, const float *weight_packed, const float *bias,
                       const float *post_scale, const float *post_shift, int act,
                       const float *pw_weight_packed, const float *pw_bias, const float *residual,
                       int pw_act, int co2, float *out, int n, int c, int h, int w, int co,
-                      int kh, int kw, int stride, int pad, int dil, int dg,
+                      int kh, int kw, int stride, int pad, int dil, int dg, int layout,
                       aanet_stream_t stream);
 
 /* Weight repack for the conv engine: [co][cg][kh][kw] -> [kh][kw][co][cg].  Done once per

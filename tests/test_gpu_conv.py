@@ -119,3 +119,119 @@ def test_mdcn_pw_tail_vs_oracle(C, H, W):
     got = ops.mdcn_pw(d(x), d(om), w2d, ops.pack_weight(w2d), None, d(sc), d(sh), "relu",
                       ops.pack_weight(w3d), d(b3), d(ident), "relu", 1, 2, 2, dg, 2.0).cpu().numpy()
     assert np.abs(got - ref).max() <= 1e-4 * (1 + np.abs(ref).max())
+
+
+# ---------------------------------------------------------------- NHWC (channels_last) paths
+NHWC_CASES = [
+    # N, C, H, W, Co, k, stride, pad, dil, groups   (32-channel groups, as NHWC requires)
+    (2, 64, 16, 52, 64, 1, 1, 0, 1, 1),      # bottleneck conv1 (NCHW in -> NHWC out)
+    (2, 64, 16, 52, 64, 3, 1, 1, 1, 1),      # SimpleBottleneck conv2 (NHWC in)
+    (2, 64, 16, 52, 54, 3, 1, 2, 2, 2),      # offset_conv on the NHWC conv1 output
+    (1, 64, 9, 27, 32, 3, 2, 1, 1, 1),       # strided, odd sizes, 64-px tiles
+    (1, 128, 5, 11, 40, 3, 1, 1, 1, 4),      # 4 groups of 32, Co not a tile multiple
+]
+
+
+@pytest.mark.parametrize("case", NHWC_CASES)
+@pytest.mark.parametrize("layout", [1, 2, 3])
+def test_conv2d_fused_nhwc_vs_torch_cpu(case, layout):
+    """AANET_LAYOUT_IN_NHWC / OUT_NHWC: same values as the NCHW path (channels_last tensors)."""
+    N, C, H, W, Co, k, s, p, d, g = case
+    gen = torch.Generator().manual_seed(7 + layout)
+    x = torch.randn(N, C, H, W, generator=gen)
+    w = torch.randn(Co, C // g, k, k, generator=gen) / (C // g * k * k) ** 0.5
+    b = torch.randn(Co, generator=gen)
+    res = torch.randn(N, Co, (H + 2 * p - d * (k - 1) - 1) // s + 1,
+                      (W + 2 * p - d * (k - 1) - 1) // s + 1, generator=gen)
+    ref = F.relu(F.conv2d(x, w, b, s, p, d, g) + res)
+    xd = x.to(DEV)
+    if layout & 1:
+        xd = xd.contiguous(memory_format=torch.channels_last)
+    rd = res.to(DEV)
+    if layout & 2 and (Co // g) % 4:
+        pytest.skip("NHWC output needs (Co / groups) % 4 == 0")
+    if layout & 2:
+        rd = rd.contiguous(memory_format=torch.channels_last)
+    wd = w.to(DEV)
+    got = ops.conv2d_fused(xd, wd, b.to(DEV), s, p, d, g, "relu", rd,
+                           packed_weight=ops.pack_weight(wd), out_nhwc=bool(layout & 2))
+    if layout & 2:
+        assert got.is_contiguous(memory_format=torch.channels_last)
+    got = got.cpu().contiguous()
+    err = (got - ref).abs().max().item()
+    assert err <= 2e-5 * (1 + ref.abs().max().item()), err
+
+
+def test_conv2d_nhwc_requires_full_chunks():
+    x = torch.randn(1, 16, 8, 8, device=DEV).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(16, 16, 3, 3, device=DEV)
+    with pytest.raises(Exception):
+        ops.conv2d_fused(x, w, None, 1, 1, 1, 1, packed_weight=ops.pack_weight(w))
+
+
+@pytest.mark.parametrize("C,H,W", [(64, 16, 52), (64, 9, 26)])
+def test_conv2d_pw_tail_nhwc_input(C, H, W):
+    gen = torch.Generator().manual_seed(C + H)
+    N = 2
+    x = torch.randn(N, C, H, W, generator=gen)
+    w2 = torch.randn(C, C, 3, 3, generator=gen) / (3 * C ** 0.5)
+    b2 = torch.randn(C, generator=gen)
+    w3 = torch.randn(C, C, 1, 1, generator=gen) / C ** 0.5
+    b3 = torch.randn(C, generator=gen)
+    ident = torch.randn(N, C, H, W, generator=gen)
+    ref = F.relu(F.conv2d(F.relu(F.conv2d(x, w2, b2, 1, 1)), w3, b3) + ident)
+    d = lambda t: t.to(DEV)  # noqa: E731
+    xd = d(x).contiguous(memory_format=torch.channels_last)
+    got = ops.conv2d_pw(xd, d(w2), ops.pack_weight(d(w2)), d(b2), None, None, "relu",
+                        ops.pack_weight(d(w3)), d(b3), d(ident), "relu", 1, 1, 1).cpu()
+    err = (got - ref).abs().max().item()
+    assert err <= 3e-5 * (1 + ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("C,H,W,off_scale", [(64, 16, 52, 1.0), (64, 9, 26, 3.0), (32, 7, 19, 1.0)])
+def test_mdcn_pw_tail_nhwc_input_vs_oracle(C, H, W, off_scale):
+    """DCN with NHWC corner loads (+BN2+ReLU, mask = 2*sigmoid) -> conv3 + identity + ReLU."""
+    from oracle import oracle
+    rng = np.random.default_rng(C + W)
+    N, dg = 2, C // 32
+    x = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    om = rng.standard_normal((N, dg * 27, H, W)).astype(np.float32)
+    om[:, :dg * 18] *= off_scale
+    w2 = (rng.standard_normal((C, C, 3, 3)) / (3 * C ** 0.5)).astype(np.float32)
+    sc = rng.uniform(0.5, 1.5, C).astype(np.float32)
+    sh = rng.standard_normal(C).astype(np.float32)
+    w3 = (rng.standard_normal((C, C, 1, 1)) / C ** 0.5).astype(np.float32)
+    b3 = rng.standard_normal(C).astype(np.float32)
+    ident = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    mask = (2.0 / (1.0 + np.exp(-om[:, dg * 18:].astype(np.float64)))).astype(np.float32)
+    t = oracle.mdcn_forward(x, om[:, :dg * 18], mask, w2, None, 1, 2, 2, 1, dg)
+    t = np.maximum(t * sc[None, :, None, None] + sh[None, :, None, None], 0)
+    ref = F.relu(F.conv2d(torch.from_numpy(t), torch.from_numpy(w3), torch.from_numpy(b3)) +
+                 torch.from_numpy(ident)).numpy()
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)  # noqa: E731
+    w2d, w3d = d(w2), d(w3)
+    xd = d(x).contiguous(memory_format=torch.channels_last)
+    got = ops.mdcn_pw(xd, d(om), w2d, ops.pack_weight(w2d), None, d(sc), d(sh), "relu",
+                      ops.pack_weight(w3d), d(b3), d(ident), "relu", 1, 2, 2, dg, 2.0).cpu().numpy()
+    assert np.abs(got - ref).max() <= 1e-4 * (1 + np.abs(ref).max())
+    # and the same kernel family on NCHW input agrees to rounding
+    got2 = ops.mdcn_pw(d(x), d(om), w2d, ops.pack_weight(w2d), None, d(sc), d(sh), "relu",
+                       ops.pack_weight(w3d), d(b3), d(ident), "relu", 1, 2, 2, dg, 2.0).cpu().numpy()
+    assert np.abs(got - got2).max() <= 2e-5 * (1 + np.abs(ref).max())
+
+
+def test_mdcn_forward_fused_nhwc_input_vs_oracle():
+    from oracle import oracle
+    rng = np.random.default_rng(5)
+    N, C, H, W, dg = 2, 64, 12, 40, 2
+    x = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    om = rng.standard_normal((N, dg * 27, H, W)).astype(np.float32) * 1.5
+    w = (rng.standard_normal((C, C, 3, 3)) / (3 * C ** 0.5)).astype(np.float32)
+    mask = (2.0 / (1.0 + np.exp(-om[:, dg * 18:].astype(np.float64)))).astype(np.float32)
+    ref = oracle.mdcn_forward(x, om[:, :dg * 18], mask, w, None, 1, 2, 2, 1, dg)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)  # noqa: E731
+    wd = d(w)
+    got = ops.mdcn_forward_fused(d(x).contiguous(memory_format=torch.channels_last), d(om), wd,
+                                 None, None, None, None, 1, 2, 2, dg, 2.0,
+                                 packed_weight=ops.pack_weight(wd)).cpu().numpy()
+    assert np.abs(got - ref).max() <= 2e-5 * (1 + np.abs(ref).max())

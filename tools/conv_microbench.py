@@ -22,6 +22,7 @@ bo = torch.randn(54, device=dev, generator=g)
 b = torch.randn(C, device=dev, generator=g)
 p1, p3, po = ops.pack_weight(w1), ops.pack_weight(w3), ops.pack_weight(wo)
 om = ops.conv2d_fused(x, wo, bo, 1, 2, 2, 2, packed_weight=po)
+xn = x.contiguous(memory_format=torch.channels_last)
 cases = {
     "conv1x1": (lambda: ops.conv2d_fused(x, w1, b, act="relu", packed_weight=p1), 2 * B * H * W * C * C),
     "conv1x1_res": (lambda: ops.conv2d_fused(x, w1, b, act="relu", residual=res, packed_weight=p1),
@@ -36,6 +37,18 @@ cases = {
                    2 * B * H * W * C * C * 10),
     "dcn": (lambda: ops.mdcn_forward_fused(x, om, w3, None, b, b, "relu", 1, 2, 2, 2, 2.0,
                                            packed_weight=p3), 2 * B * H * W * C * C * 9),
+    "conv1x1_onhwc": (lambda: ops.conv2d_fused(x, w1, b, act="relu", packed_weight=p1, out_nhwc=True),
+                      2 * B * H * W * C * C),
+    "conv3x3_nhwc": (lambda: ops.conv2d_fused(xn, w3, b, 1, 1, 1, 1, "relu", packed_weight=p3),
+                     2 * B * H * W * C * C * 9),
+    "offset_nhwc": (lambda: ops.conv2d_fused(xn, wo, bo, 1, 2, 2, 2, packed_weight=po),
+                    2 * B * H * W * 54 * 32 * 9),
+    "dcn_nhwc": (lambda: ops.mdcn_forward_fused(xn, om, w3, None, b, b, "relu", 1, 2, 2, 2, 2.0,
+                                                packed_weight=p3), 2 * B * H * W * C * C * 9),
+    "dcn_pw_nhwc": (lambda: ops.mdcn_pw(xn, om, w3, p3, None, b, b, "relu", p1, b, res, "relu", 1, 2, 2, 2),
+                    2 * B * H * W * C * C * 10),
+    "conv3x3_pw_nhwc": (lambda: ops.conv2d_pw(xn, w3, p3, b, None, None, "relu", p1, b, res, "relu", 1, 1, 1),
+                        2 * B * H * W * C * C * 10),
     "csa_sum": (lambda: ops.csa_sum([x, res[:, :, :64, :208].contiguous(),
                                      res[:, :, :32, :104].contiguous()]), 0),
 }
