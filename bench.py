@@ -105,21 +105,25 @@ def kernel_rooflines(model, left, right, batch, iters):
     ms = time_events(lambda: ops.disp_regress(vol), iters, stream)
     res["disp_regress_s0"] = dict(bound="hbm", ms=ms, algo=reg_bytes, unit="GB/s",
                                   achieved=reg_bytes / ms / 1e6, peak=HBM_PEAK_GBS)
-    # modulated DCN (fused eval form: + BN + ReLU), scale 0 of the last fusion
+    # modulated DCN as the hot path runs it (DeformSimpleBottleneck of the last fusion, scale 0):
+    # NHWC conv1 output in, DCN + BN2 + ReLU -> conv3 + BN3 + identity + ReLU in one kernel
     blk = model.aggregation.fusions[5].branches[0][0]
     with torch.no_grad():
-        x1 = conv_bn_act(vol, blk.conv1, blk.bn1, "relu")
-        om = blk.conv2.offset_conv(x1)
+        x1 = conv_bn_act(vol, blk.conv1, blk.bn1, "relu", out_nhwc=True)
+        c2 = blk.conv2
+        dc = c2.deform_conv
+        om = conv_bn_act(x1, c2.offset_conv)
         ps, psh = bn_affine(blk.bn2)
-        w = blk.conv2.deform_conv.weight
-        wp = folded(blk.conv2.deform_conv, None)[2]
-        fn = lambda: ops.mdcn_forward_fused(x1, om, w, None, ps, psh, 1, 1, 2, 2, 2, 2.0,  # noqa: E731
-                                            packed_weight=wp)
+        wp = folded(dc, None)[2]
+        w3, b3, p3 = folded(blk.conv3, blk.bn3)
+        fn = lambda: ops.mdcn_pw(x1, om, dc.weight, wp, dc.bias, ps, psh, "relu", p3, b3, vol,  # noqa: E731
+                                 "relu", 1, dc.padding, dc.dilation, c2.deformable_groups, 2.0)
         ms = time_events(fn, iters, stream)
-    Co, Ci = w.shape[:2]
-    flops = 2.0 * B * H * W * Co * Ci * 9
-    res["mdcn_fwd_s0"] = dict(bound="mfma", ms=ms, algo=flops, unit="TFLOP/s",
-                              achieved=flops / ms / 1e9, peak=FP32_MFMA_PEAK_TF)
+    Co, Ci = dc.weight.shape[:2]
+    Co2 = w3.shape[0]
+    flops = 2.0 * B * H * W * (Co * Ci * 9 + Co2 * Co)
+    res["mdcn_pw_s0"] = dict(bound="mfma", ms=ms, algo=flops, unit="TFLOP/s",
+                             achieved=flops / ms / 1e9, peak=FP32_MFMA_PEAK_TF)
     for v in res.values():
         v["frac"] = v["achieved"] / v["peak"]
     return res

@@ -54,7 +54,7 @@ def test_conv2d_fused_vs_torch_cpu(case, epi, packed):
     assert err <= 2e-5 * (1 + ref.abs().max().item()), err
 
 
-@pytest.mark.parametrize("sizes", [[(24, 48), (12, 24), (6, 12)], [(12, 24), (24, 48), (6, 12)],
+@pytest.mark.parametrize("sizes", [[(24, 48), (12, 24), (6, 12)], [(8, 20), (4, 10), (2, 5)], [(4, 8), (1, 2)], [(12, 24), (24, 48), (6, 12)],
                                    [(6, 12), (12, 24), (24, 48)], [(128, 416), (64, 208), (32, 104)],
                                    [(7, 13), (4, 7)], [(5, 9)]])
 @pytest.mark.parametrize("act", [None, "leaky"])

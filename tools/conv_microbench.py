@@ -23,6 +23,7 @@ b = torch.randn(C, device=dev, generator=g)
 p1, p3, po = ops.pack_weight(w1), ops.pack_weight(w3), ops.pack_weight(wo)
 om = ops.conv2d_fused(x, wo, bo, 1, 2, 2, 2, packed_weight=po)
 xn = x.contiguous(memory_format=torch.channels_last)
+up1, up2 = res[:, :, :64, :208].contiguous(), res[:, :, :32, :104].contiguous()
 cases = {
     "conv1x1": (lambda: ops.conv2d_fused(x, w1, b, act="relu", packed_weight=p1), 2 * B * H * W * C * C),
     "conv1x1_res": (lambda: ops.conv2d_fused(x, w1, b, act="relu", residual=res, packed_weight=p1),
@@ -49,8 +50,7 @@ cases = {
                     2 * B * H * W * C * C * 10),
     "conv3x3_pw_nhwc": (lambda: ops.conv2d_pw(xn, w3, p3, b, None, None, "relu", p1, b, res, "relu", 1, 1, 1),
                         2 * B * H * W * C * C * 10),
-    "csa_sum": (lambda: ops.csa_sum([x, res[:, :, :64, :208].contiguous(),
-                                     res[:, :, :32, :104].contiguous()]), 0),
+    "csa_sum": (lambda: ops.csa_sum([x, up1, up2]), 0),
 }
 for name, (fn, flops) in cases.items():
     if names and name not in names:

@@ -15,8 +15,10 @@ tag = sys.argv[2]
 dst = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
 os.makedirs(dst, exist_ok=True)
 
-KMAP = {"corr_volume_s0": r"corr_volume_kernel<5>", "disp_regress_s0": r"disp_regress_kernel",
-        "mdcn_fwd_s0": r"conv_fwd_kernel<1, 64, 128, 1>"}
+# bench.py kernel_rooflines keys -> kernel names (DCN: MODE 1, CO_T 64, PTT 128, packed, tail,
+# sched, full chunks, NHWC input)
+KMAP = {"corr_volume_s0": r"corr_volume_kernel<5, 1>", "disp_regress_s0": r"disp_regress_kernel",
+        "mdcn_pw_s0": r"conv_fwd_kernel<1, 64, 128, 1, 1, 1, 1, 1>"}
 
 # 1. kernel stats of the bench command
 stats = list(csv.DictReader(open(os.path.join(src, "trace", "bench_kernel_stats.csv"))))
