@@ -1101,7 +1101,9 @@ int launch_fwd(const MdcnArgs &a, int packed, hipStream_t st) {
   }
   const int ncot = host_div_up(Cog, co_t);
   // 128-pixel tiles when they still give >= 4 workgroups per CU, else 64
-  const int ptt = co_t == 16 || (long)a.N * host_div_up(P, 128) * a.groups * ncot >= 1024 ? 128 : 64;
+  int ptt = co_t == 16 || (long)a.N * host_div_up(P, 128) * a.groups * ncot >= 1024 ? 128 : 64;
+  static const int ptt_env = [] { const char *e = getenv("AANET_PTT"); return e ? atoi(e) : 0; }();
+  if (ptt_env == 64 && co_t != 16) ptt = 64;  // A/B switch (tools/conv_microbench.py)
   dim3 grid((unsigned)(a.N * host_div_up(P, ptt)), (unsigned)(a.groups * ncot));
   if (ptt == 128) {
     switch (co_t) {
