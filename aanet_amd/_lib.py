@@ -33,9 +33,9 @@ _SIGNATURES = {
     "aanet_mdcn_bwd_f32": [_P] * 10 + [_I] * 12 + [_P],
     "aanet_conv2d_fused_f32": [_P] * 6 + [_I, _I, _P] + [_I] * 12 + [_P],
     "aanet_conv_weight_pack_f32": [_P, _P, _I, _I, _I, _I, _P],
-    "aanet_conv2d_pw_f32": [_P] * 5 + [_I] + [_P] * 3 + [_I, _I, _P] + [_I] * 11 + [_P],
+    "aanet_conv2d_pw_f32": [_P] * 5 + [_I] + [_P] * 3 + [_I, _I, _P] + [_I] * 10 + [_P, _I, _P],
     "aanet_mdcn_pw_f32": [_P, _P, _L, _P, _L, _I, _F, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _P]
-    + [_I] * 12 + [_P],
+    + [_I] * 11 + [_P, _I, _P],
     "aanet_csa_sum_f32": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P],
     "aanet_mdcn_im2col_f32": [_P, _P, _P, _P] + [_I] * 9 + [_P],
     "aanet_mdcn_sample_index": [_P, _P, _P, _P] + [_I] * 9 + [_P],
@@ -90,6 +90,13 @@ def is_nhwc(t):
 
 
 LAYOUT_IN_NHWC, LAYOUT_OUT_NHWC = 1, 2  # AANET_LAYOUT_* (include/aanet_mi355x.h)
+
+
+class CsaEpilogue(ctypes.Structure):
+    """aanet_csa_epilogue_t (include/aanet_mi355x.h)."""
+    _fields_ = [("out", ctypes.c_void_p), ("num_up", ctypes.c_int),
+                ("up", ctypes.c_void_p * 3), ("up_h", ctypes.c_int * 3),
+                ("up_w", ctypes.c_int * 3), ("act", ctypes.c_int)]
 
 
 def stream_of(t):

@@ -34,3 +34,44 @@ static inline int host_div_up(long a, long b) { return (int)((a + b - 1) / b); }
 static inline int conv_out_size(int in, int k, int s, int p, int d) {
   return (in + 2 * p - (d * (k - 1) + 1)) / s + 1;
 }
+
+// ---- exact 2x / 4x bilinear upsampling of a 4-column output quad (PyTorch align_corners=False,
+// F.interpolate as in nets/aggregation.py:395-396).  With scale 1/r the source coordinate of
+// output column 4q+u is 4q/r + (u+0.5)/r - 0.5, so the quad reads one 4-wide source segment
+// (s0 = 2q-1 for r = 2, q-1 for r = 4; indices clamped into the row exactly as PyTorch's
+// max(src, 0) / x1 = x0 + (x0 < in-1) do) with constant lambdas:
+//   r = 2: (0.25, 0.75) pairs; r = 4: lambdas 0.625, 0.875, 0.125, 0.375.
+__device__ __forceinline__ f32x4 load_seg(const float *__restrict__ row, int iw, int s0) {
+  if (s0 >= 0 && s0 + 3 <= iw - 1) {
+    // dword-aligned 16-byte load (unaligned vector access is enabled on gfx9 Linux)
+    typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+    const f4u v = *reinterpret_cast<const f4u *>(row + s0);
+    return f32x4{v.x, v.y, v.z, v.w};
+  }
+  f32x4 v;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) v[u] = row[min(max(s0 + u, 0), iw - 1)];
+  return v;
+}
+
+__device__ __forceinline__ f32x4 hlerp(const f32x4 v, int r) {
+  if (r == 2)
+    return f32x4{0.25f * v[0] + 0.75f * v[1], 0.75f * v[1] + 0.25f * v[2],
+                 0.25f * v[1] + 0.75f * v[2], 0.75f * v[2] + 0.25f * v[3]};
+  return f32x4{0.375f * v[0] + 0.625f * v[1], 0.125f * v[0] + 0.875f * v[1],
+               0.875f * v[1] + 0.125f * v[2], 0.625f * v[1] + 0.375f * v[2]};
+}
+
+// Output quad (row y, columns 4q..4q+3) of an r-times upsampled plane im [ih][iw];
+// sh = ih / H (the PyTorch area_pixel_compute_scale for align_corners=False).
+__device__ __forceinline__ f32x4 upsample_quad(const float *__restrict__ im, int ih, int iw,
+                                               float sh, int r, int y, int q) {
+  float hr = sh * ((float)y + 0.5f) - 0.5f;
+  hr = hr < 0.f ? 0.f : hr;
+  const int h1 = (int)hr, h1p = h1 < ih - 1 ? 1 : 0;
+  const float h1l = hr - (float)h1, h0l = 1.f - h1l;
+  const int s0 = r == 2 ? 2 * q - 1 : q - 1;
+  const f32x4 t = hlerp(load_seg(im + (long)h1 * iw, iw, s0), r);
+  const f32x4 b = hlerp(load_seg(im + (long)(h1 + h1p) * iw, iw, s0), r);
+  return h0l * t + h1l * b;
+}

@@ -71,33 +71,8 @@ __global__ __launch_bounds__(256) void csa_sum_kernel(CsaArgs a) {
   }
 }
 
-// Exact 2x / 4x upsampling (the AANet pyramid: 1/3 -> 1/6 -> 1/12).  With scale 1/r the source
-// coordinate of output column 4q+u is q*4/r + (u+0.5)/r - 0.5, so the four columns of a thread
-// read one 4-wide source segment (s0 = 2q-1 for r = 2, q-1 for r = 4; indices clamped into the
-// row exactly as PyTorch's max(src, 0) / x1 = x0 + (x0 < in-1) do) with constant lambdas:
-//   r = 2: (0.25, 0.75) pairs; r = 4: lambdas 0.625, 0.875, 0.125, 0.375.
-// One 16-byte load per source row instead of four gathered dwords per output element.
-__device__ __forceinline__ f32x4 load_seg(const float *__restrict__ row, int iw, int s0) {
-  if (s0 >= 0 && s0 + 3 <= iw - 1) {
-    // dword-aligned 16-byte load (unaligned vector access is enabled on gfx9 Linux)
-    typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
-    const f4u v = *reinterpret_cast<const f4u *>(row + s0);
-    return f32x4{v.x, v.y, v.z, v.w};
-  }
-  f32x4 v;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) v[u] = row[min(max(s0 + u, 0), iw - 1)];
-  return v;
-}
-
-__device__ __forceinline__ f32x4 hlerp(const f32x4 v, int r) {
-  if (r == 2)
-    return f32x4{0.25f * v[0] + 0.75f * v[1], 0.75f * v[1] + 0.25f * v[2],
-                 0.25f * v[1] + 0.75f * v[2], 0.75f * v[2] + 0.25f * v[3]};
-  return f32x4{0.375f * v[0] + 0.625f * v[1], 0.125f * v[0] + 0.875f * v[1],
-               0.875f * v[1] + 0.125f * v[2], 0.625f * v[1] + 0.375f * v[2]};
-}
-
+// Exact 2x / 4x upsampling (the AANet pyramid: 1/3 -> 1/6 -> 1/12): upsample_quad (common.h)
+// reads one 16-byte source segment per row instead of four gathered dwords per output element.
 __global__ __launch_bounds__(256) void csa_sum_int_kernel(CsaArgs a, int r0, int r1, int r2, int r3) {
   const int rr[MAXIN] = {r0, r1, r2, r3};
   const unsigned W4 = a.W >> 2, H = a.H;
@@ -117,15 +92,7 @@ __global__ __launch_bounds__(256) void csa_sum_int_kernel(CsaArgs a, int r0, int
         v = *reinterpret_cast<const f32x4 *>(a.in[j] + base);
       } else {
         const int ih = a.ih[j], iw = a.iw[j];
-        float hr = a.sh[j] * ((float)y + 0.5f) - 0.5f;
-        hr = hr < 0.f ? 0.f : hr;
-        const int h1 = (int)hr, h1p = h1 < ih - 1 ? 1 : 0;
-        const float h1l = hr - (float)h1, h0l = 1.f - h1l;
-        const float *im = a.in[j] + (long)plane * ih * iw;
-        const int s0 = r == 2 ? 2 * (int)q - 1 : (int)q - 1;
-        const f32x4 t = hlerp(load_seg(im + (long)h1 * iw, iw, s0), r);
-        const f32x4 b = hlerp(load_seg(im + (long)(h1 + h1p) * iw, iw, s0), r);
-        v = h0l * t + h1l * b;
+        v = upsample_quad(a.in[j] + (long)plane * ih * iw, ih, iw, a.sh[j], r, (int)y, (int)q);
       }
       acc = j == 0 ? v : acc + v;
     }

@@ -46,6 +46,10 @@ struct MdcnArgs {
   float *out;
   int N, C, H, W, Co, kh, kw, stride, pad, dil, groups, dg, Ho, Wo;
   int layout;  // AANET_LAYOUT_* bits (conv engine only)
+  // CSA epilogue (tail kernels): csa_out = csa_act(out + sum_j up_r[j](up[j])), r = 2 or 4
+  float *csa_out;
+  const float *up[3];
+  int up_h[3], up_w[3], up_r[3], num_up, csa_act;
 };
 
 // Bilinear sampling state of one (pixel, tap, deformable group).  Invalid corners get
@@ -727,27 +731,93 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   const float *esc = TAIL ? nullptr : a.post_scale;
   const float *esh = TAIL ? nullptr : a.post_shift;
   const int eact = TAIL ? a.tail_act : a.act;
-  for (int e = tid; e < CO_T * QPR; e += FNT) {
-    const int col = e / QPR, q = e % QPR;
-    const int co = co0 + col;
-    const long pe = p0 + 4 * q;
-    if (co >= cend_o || pe >= P) continue;
-    const float bias = ebias ? ebias[co] : 0.f;
-    const float sc = esc ? esc[co] : 1.f;
-    const float sh = esc ? esh[co] : 0.f;
-    const long o = ((long)n * cout + co) * P + pe;
-    f32x4 v = *reinterpret_cast<const f32x4 *>(sO + col * OP + 4 * q);
-    if (vec && pe + 3 < P) {
-      f32x4 rv = a.residual ? *reinterpret_cast<const f32x4 *>(a.residual + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+  // Items (4 pixels x 1 channel) are processed two at a time with every global load of the pair
+  // (residual, CSA source segments) issued before any use: a per-item load->use chain would
+  // expose the HBM / L2 latency once per item.
+  constexpr int NE = CO_T * QPR;
+  constexpr int EPT = (NE + FNT - 1) / FNT;
+  constexpr int EB = EPT >= 2 ? 2 : 1;
+  const bool csa = TAIL && a.csa_out;
+#pragma unroll
+  for (int i0 = 0; i0 < EPT; i0 += EB) {
+    f32x4 ev[EB], er[EB], eu[EB][2][2];
+    bool eok[EB];
+#pragma unroll
+    for (int b = 0; b < EB; ++b) {
+      const int e = tid + (i0 + b) * FNT;
+      const int col = e / QPR, q = e % QPR, co = co0 + col;
+      const long pe = p0 + 4 * q;
+      eok[b] = (NE % FNT == 0 || e < NE) && co < cend_o && vec && pe + 3 < P;
+      if (!eok[b]) continue;
+      const long o = ((long)n * cout + co) * P + pe;
+      ev[b] = *reinterpret_cast<const f32x4 *>(sO + col * OP + 4 * q);
+      if (a.residual) er[b] = *reinterpret_cast<const f32x4 *>(a.residual + o);
+      if (csa) {
+        const int y = (int)(pe / a.Wo), qq = (int)(pe % a.Wo) >> 2;  // Wo % 4 == 0 (launcher)
+        const long plane = (long)n * cout + co;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if (j >= a.num_up) break;
+          const int ih = a.up_h[j], iw = a.up_w[j], r = a.up_r[j];
+          float hr = ((float)ih / (float)a.Ho) * ((float)y + 0.5f) - 0.5f;
+          hr = hr < 0.f ? 0.f : hr;
+          const int h1 = (int)hr, h1p = h1 < ih - 1 ? 1 : 0;
+          const float *im = a.up[j] + plane * ih * iw;
+          const int s0 = r == 2 ? 2 * qq - 1 : qq - 1;
+          eu[b][j][0] = load_seg(im + (long)h1 * iw, iw, s0);
+          eu[b][j][1] = load_seg(im + (long)(h1 + h1p) * iw, iw, s0);
+        }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < EB; ++b) {
+      if (!eok[b]) continue;
+      const int e = tid + (i0 + b) * FNT;
+      const int col = e / QPR, q = e % QPR, co = co0 + col;
+      const long pe = p0 + 4 * q;
+      const long o = ((long)n * cout + co) * P + pe;
+      const float bias = ebias ? ebias[co] : 0.f;
+      const float sc = esc ? esc[co] : 1.f;
+      const float sh = esc ? esh[co] : 0.f;
+      f32x4 v = ev[b];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         float t = v[u] + bias;
         if (esc) t = t * sc + sh;
-        if (a.residual) t += rv[u];
+        if (a.residual) t += er[b][u];
         v[u] = apply_act(t, eact);
       }
       *reinterpret_cast<f32x4 *>(a.out + o) = v;
-    } else {
+      if (csa) {
+        // cross-scale sum of this output branch (nets/aggregation.py:387-400): the block output
+        // (the identity term) + exact 2x/4x upsamplings of the coarser exchange terms, LeakyReLU
+        const int y = (int)(pe / a.Wo);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if (j >= a.num_up) break;
+          const int ih = a.up_h[j];
+          float hr = ((float)ih / (float)a.Ho) * ((float)y + 0.5f) - 0.5f;
+          hr = hr < 0.f ? 0.f : hr;
+          const float h1l = hr - (float)(int)hr, h0l = 1.f - h1l;
+          v += h0l * hlerp(eu[b][j][0], a.up_r[j]) + h1l * hlerp(eu[b][j][1], a.up_r[j]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = apply_act(v[u], a.csa_act);
+        *reinterpret_cast<f32x4 *>(a.csa_out + o) = v;
+      }
+    }
+  }
+  // pixels the quad path does not cover (P % 4 != 0, ragged last tile): one element at a time
+  if (!vec || p0 + PTT > P) {
+    for (int e = tid; e < NE; e += FNT) {
+      const int col = e / QPR, q = e % QPR, co = co0 + col;
+      const long pe = p0 + 4 * q;
+      if (co >= cend_o || pe >= P || (vec && pe + 3 < P)) continue;
+      const float bias = ebias ? ebias[co] : 0.f;
+      const float sc = esc ? esc[co] : 1.f;
+      const float sh = esc ? esh[co] : 0.f;
+      const long o = ((long)n * cout + co) * P + pe;
+      const f32x4 v = *reinterpret_cast<const f32x4 *>(sO + col * OP + 4 * q);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (pe + u >= P) break;
@@ -1041,6 +1111,13 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
   a.groups = groups;
   a.dg = dg;
   a.layout = 0;
+  a.csa_out = nullptr;
+  a.num_up = 0;
+  a.csa_act = 0;
+  for (int j = 0; j < 3; ++j) {
+    a.up[j] = nullptr;
+    a.up_h[j] = a.up_w[j] = a.up_r[j] = 1;
+  }
   a.Ho = conv_out_size(h, kh, stride, pad, dil);
   a.Wo = conv_out_size(w, kw, stride, pad, dil);
   const long P = (long)a.Ho * a.Wo, K = (long)kh * kw;
@@ -1089,6 +1166,14 @@ int launch_fwd(const MdcnArgs &a, int packed, hipStream_t st) {
   const long P = (long)a.Ho * a.Wo;
   const int Cog = a.Co / a.groups;
   if (a.layout < 0 || a.layout > 3) return AANET_EINVAL;
+  if (a.csa_out) {  // CSA epilogue: tail kernels, quad-aligned rows, exact 2x / 4x terms
+    if (!a.tail_w || a.Wo % 4 || a.num_up < 0 || a.num_up > 2) return AANET_EUNSUPPORTED;
+    for (int j = 0; j < a.num_up; ++j) {
+      const int r = a.up_r[j];
+      if (!a.up[j] || (r != 2 && r != 4) || a.up_h[j] * r != a.Ho || a.up_w[j] * r != a.Wo)
+        return AANET_EUNSUPPORTED;
+    }
+  }
   if (a.layout) {  // NHWC paths: packed weights, full 32-channel chunks, 4-channel quads
     const int Cg = a.C / a.groups, cpg = a.C / a.dg;
     if (!packed || Cg % KC || (MODE && cpg % KC) || a.C % 4) return AANET_EUNSUPPORTED;
@@ -1133,6 +1218,23 @@ __global__ void pack_weight_kernel(const float *__restrict__ w, float *__restric
   }
 }
 
+int set_csa(MdcnArgs &a, const aanet_csa_epilogue_t *csa) {
+  if (!csa) return AANET_OK;
+  if (!csa->out || csa->num_up < 0 || csa->num_up > 3 || csa->act < 0 || csa->act > 2)
+    return AANET_EINVAL;
+  a.csa_out = csa->out;
+  a.num_up = csa->num_up;
+  a.csa_act = csa->act;
+  for (int j = 0; j < csa->num_up; ++j) {
+    if (!csa->up[j] || csa->up_h[j] <= 0 || csa->up_w[j] <= 0) return AANET_EINVAL;
+    a.up[j] = csa->up[j];
+    a.up_h[j] = csa->up_h[j];
+    a.up_w[j] = csa->up_w[j];
+    a.up_r[j] = csa->up_h[j] > 0 ? a.Ho / csa->up_h[j] : 0;
+  }
+  return AANET_OK;
+}
+
 int round_pitch(int v, int mod32) {  // smallest p >= v with p % 32 == mod32
   int p = v;
   while (p % 32 != mod32) ++p;
@@ -1169,12 +1271,15 @@ extern "C" int aanet_conv2d_pw_f32(const float *x, const float *weight_packed, c
                                    const float *pw_weight_packed, const float *pw_bias,
                                    const float *residual, int pw_act, int co2, float *out, int n,
                                    int c, int h, int w, int co, int kh, int kw, int stride,
-                                   int pad, int dil, int layout, aanet_stream_t stream) {
+                                   int pad, int dil, const aanet_csa_epilogue_t *csa, int layout,
+                                   aanet_stream_t stream) {
   if (act < 0 || act > 2 || pw_act < 0 || pw_act > 2 || !pw_weight_packed) return AANET_EINVAL;
   if (layout != 0 && layout != 1) return AANET_EINVAL;
   MdcnArgs a = make_args(x, nullptr, 0, nullptr, 0, 0, 1.f, weight_packed, bias, post_scale,
                          post_shift, act, out, n, c, h, w, co, kh, kw, stride, pad, dil, 1, 1);
   a.layout = layout;
+  const int rc = set_csa(a, csa);
+  if (rc) return rc;
   a.tail_w = pw_weight_packed;
   a.tail_b = pw_bias;
   a.tail_act = pw_act;
@@ -1190,13 +1295,16 @@ extern "C" int aanet_mdcn_pw_f32(const float *x, const float *offset, long offse
                                  const float *pw_weight_packed, const float *pw_bias,
                                  const float *residual, int pw_act, int co2, float *out, int n,
                                  int c, int h, int w, int co, int kh, int kw, int stride, int pad,
-                                 int dil, int dg, int layout, aanet_stream_t stream) {
+                                 int dil, int dg, const aanet_csa_epilogue_t *csa, int layout,
+                                 aanet_stream_t stream) {
   if (act < 0 || act > 2 || pw_act < 0 || pw_act > 2 || !pw_weight_packed) return AANET_EINVAL;
   if (layout != 0 && layout != 1) return AANET_EINVAL;
   MdcnArgs a = make_args(x, offset, offset_batch_stride, mask, mask_batch_stride, mask_logits,
                          mask_scale, weight_packed, bias, post_scale, post_shift, act, out, n, c,
                          h, w, co, kh, kw, stride, pad, dil, 1, dg);
   a.layout = layout;
+  const int rc = set_csa(a, csa);
+  if (rc) return rc;
   a.tail_w = pw_weight_packed;
   a.tail_b = pw_bias;
   a.tail_act = pw_act;

@@ -69,17 +69,49 @@ class AdaptiveAggregationModule(nn.Module):
 
         self.relu = nn.LeakyReLU(0.2, inplace=True)
 
-    def _fuse_eval(self, x):
+    def _exchange_up(self, x, i, j):
+        """Exchange term fuse_layers[i][j] for i < j: 1x1 conv + BN at scale j's resolution."""
+        layer = self.fuse_layers[i][j]
+        return conv_bn_act(x[j], layer[0], layer[1], None)
+
+    def _forward_eval(self, x):
+        """Eval ISA + CSA.  The coarser scales run first, so that their exchange terms for output
+        branch 0 exist when the scale-0 bottleneck runs: its tail kernel then writes both the
+        block output and the cross-scale sum of branch 0 (aanet_csa_epilogue_t), which removes
+        the scale-0 resize-sum kernel.  The in-place list mutation of aggregation.py:382 and the
+        term order of aggregation.py:388-400 are unchanged (the branches are independent)."""
+        S = len(self.branches)
+        for i in range(1, S):
+            for j in range(self.num_blocks):
+                x[i] = self.branches[i][j](x[i])
+        up0 = [self._exchange_up(x, 0, j) for j in range(1, S)]
+        for j in range(self.num_blocks - 1):
+            x[0] = self.branches[0][j](x[0])
+        last = self.branches[0][self.num_blocks - 1]
+        x[0], csa0 = last.forward_csa(x[0], up0)
+        return self._fuse_eval(x, {0: csa0} if csa0 is not None else {}, {(0, j): t for j, t in
+                                                                         zip(range(1, S), up0)})
+
+    def _fuse_eval(self, x, done=None, terms_cache=None):
         """Eval CSA: each exchange conv (+BN folded, +LeakyReLU inside strided chains) is one HIP
         conv kernel at its own resolution; the resize + sum + LeakyReLU of every output branch is
-        one aanet_csa_sum_f32 kernel (same term order as aggregation.py:388-400)."""
+        one aanet_csa_sum_f32 kernel (same term order as aggregation.py:388-400).  done: output
+        branches already summed (by a tail-kernel epilogue); terms_cache: exchange terms already
+        computed, keyed (i, j)."""
+        done = done or {}
+        terms_cache = terms_cache or {}
         x_fused = []
         for i in range(len(self.fuse_layers)):
+            if i in done:
+                x_fused.append(done[i])
+                continue
             terms = []
             for j in range(len(self.branches)):
                 layer = self.fuse_layers[i][j]
                 if i == j:
                     terms.append(x[j])
+                elif (i, j) in terms_cache:
+                    terms.append(terms_cache[(i, j)])
                 elif i < j:
                     terms.append(conv_bn_act(x[j], layer[0], layer[1], None))
                 else:
@@ -93,6 +125,8 @@ class AdaptiveAggregationModule(nn.Module):
     def forward(self, x):
         """aggregation.py:375-402."""
         assert len(self.branches) == len(x)
+        if self.num_scales > 1 and use_fused(self, x[0]) and getattr(self, "aanet_fuse_csa", True):
+            return self._forward_eval(x)
         for i in range(len(self.branches)):
             branch = self.branches[i]
             for j in range(self.num_blocks):

@@ -102,11 +102,14 @@ class _BottleneckBase(nn.Module):
         out = self.relu(out)
         return out
 
-    def _forward_fused(self, x, deform, conv1_out=None):
+    def _forward_fused(self, x, deform, conv1_out=None, csa_up=None):
         """conv1+bn1+relu, then conv2+bn2+relu -> conv3+bn3 (+identity) + relu as ONE HIP kernel
         (the conv3 GEMM runs in conv2's epilogue).  When the tail kernel takes the block, conv1
         writes its output channels-last (NHWC) so that conv2 / offset_conv / the DCN read each
-        32-channel chunk of a position as one 128-byte line.  conv1_out: precomputed conv1."""
+        32-channel chunk of a position as one 128-byte line.  conv1_out: precomputed conv1.
+        csa_up: coarser CSA exchange terms of this resolution's output branch; the tail kernel
+        then also writes that branch's cross-scale sum, and (out, csa_out) is returned
+        (csa_out None when the tail kernel does not take the block)."""
         w3, b3, p3 = folded(self.conv3, self.bn3)
         width = self.conv1.weight.shape[0]
         c2 = self.conv2
@@ -130,7 +133,8 @@ class _BottleneckBase(nn.Module):
             if pw:
                 return ops.mdcn_pw(out, offset_mask, dc.weight, wp, dc.bias, ps, psh, "relu", p3, b3,
                                    identity, "relu", dc.stride, dc.padding, dc.dilation,
-                                   c2.deformable_groups, 2.0 if c2.double_mask else 1.0)
+                                   c2.deformable_groups, 2.0 if c2.double_mask else 1.0,
+                                   csa_up=csa_up)
             out = c2.forward_fused(out, self.bn2, act="relu")
         elif deform:
             out = F.relu_(self.bn2(self.conv2(out)))
@@ -138,9 +142,16 @@ class _BottleneckBase(nn.Module):
             w2, b2, p2 = folded(self.conv2, self.bn2)
             if pw:
                 return ops.conv2d_pw(out, w2, p2, b2, None, None, "relu", p3, b3, identity, "relu",
-                                     c2.stride[0], c2.padding[0], c2.dilation[0])
+                                     c2.stride[0], c2.padding[0], c2.dilation[0], csa_up=csa_up)
             out = conv_bn_act(out, self.conv2, self.bn2, "relu")
-        return conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity)
+        out = conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity)
+        return out if csa_up is None else (out, None)
+
+    def forward_csa(self, x, csa_up):
+        """Eval-only: (block output, its output branch's CSA sum or None); see _forward_fused."""
+        deform = isinstance(self, DeformSimpleBottleneck) or isinstance(self, DeformBottleneck)
+        r = self._forward_fused(x, deform=deform, csa_up=list(csa_up))
+        return r if isinstance(r, tuple) else (r, None)
 
 
 class DeformBottleneck(_BottleneckBase):

@@ -199,10 +199,33 @@ def conv2d_fused(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1
     return out
 
 
+def _csa_epilogue(out, csa_up, csa_act):
+    """(aanet_csa_epilogue_t, its output) for the tail kernels; csa_up: the coarser exchange
+    terms [n][co2][h/r][w/r] (r = 2 or 4) summed into this output branch."""
+    if csa_up is None:
+        return None, None
+    if len(csa_up) > 3:
+        raise ValueError("at most 3 upsampled CSA terms")
+    require_gpu(*csa_up)
+    csa_out = torch.empty_like(out)
+    d = _lib.CsaEpilogue()
+    d.out = csa_out.data_ptr()
+    d.num_up = len(csa_up)
+    for j, t in enumerate(csa_up):
+        if t.shape[:2] != out.shape[:2]:
+            raise ValueError("CSA term batch/channels must match the output")
+        d.up[j] = t.data_ptr()
+        d.up_h[j], d.up_w[j] = t.shape[2], t.shape[3]
+    d.act = ACT[csa_act]
+    return d, csa_out
+
+
 def conv2d_pw(x, weight, packed_weight, bias, post_scale, post_shift, act, pw_packed, pw_bias,
-              residual=None, pw_act=None, stride=1, padding=0, dilation=1):
+              residual=None, pw_act=None, stride=1, padding=0, dilation=1, csa_up=None,
+              csa_act="leaky"):
     """Plain conv + fused pointwise tail (bottleneck conv2 -> conv3, aanet_conv2d_pw_f32).
-    x may be channels_last (NHWC staging); the output is NCHW."""
+    x may be channels_last (NHWC staging); the output is NCHW.  csa_up (list of coarser
+    exchange terms): also return the CSA sum act(out + up(csa_up...)) -> (out, csa_out)."""
     require_gpu(x, packed_weight, bias, post_scale, post_shift, pw_packed, pw_bias, residual,
                 nhwc_ok=(0,))
     N, C, H, W = x.shape
@@ -210,18 +233,20 @@ def conv2d_pw(x, weight, packed_weight, bias, post_scale, post_shift, act, pw_pa
     Co2 = pw_packed.shape[-2]
     Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
     out = torch.empty((N, Co2, Ho, Wo), device=x.device, dtype=x.dtype)
+    desc, csa_out = _csa_epilogue(out, csa_up, csa_act)
     call("aanet_conv2d_pw_f32", ptr(x), ptr(packed_weight), ptr(bias), ptr(post_scale),
          ptr(post_shift), ACT[act], ptr(pw_packed), ptr(pw_bias), ptr(residual), ACT[pw_act], Co2,
          ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation,
+         None if desc is None else _lib.ctypes.byref(desc),
          _lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0, stream_of(x))
-    return out
+    return out if desc is None else (out, csa_out)
 
 
 def mdcn_pw(x, offset_mask, weight, packed_weight, bias, post_scale, post_shift, act, pw_packed,
             pw_bias, residual=None, pw_act=None, stride=1, padding=0, dilation=1,
-            deformable_groups=1, mask_scale=2.0):
+            deformable_groups=1, mask_scale=2.0, csa_up=None, csa_act="leaky"):
     """DCN (offset/mask read in place from offset_conv's output) + fused pointwise tail.
-    x may be channels_last (NHWC corner loads); the output is NCHW."""
+    x may be channels_last (NHWC corner loads); the output is NCHW.  csa_up: as conv2d_pw."""
     require_gpu(x, offset_mask, packed_weight, bias, post_scale, post_shift, pw_packed, pw_bias,
                 residual, nhwc_ok=(0,))
     N, C, H, W = x.shape
@@ -232,14 +257,16 @@ def mdcn_pw(x, offset_mask, weight, packed_weight, bias, post_scale, post_shift,
     if offset_mask.shape != (N, deformable_groups * 3 * K, Ho, Wo):
         raise ValueError(f"offset_mask shape {tuple(offset_mask.shape)} unexpected")
     out = torch.empty((N, Co2, Ho, Wo), device=x.device, dtype=x.dtype)
+    desc, csa_out = _csa_epilogue(out, csa_up, csa_act)
     bs = offset_mask.stride(0)
     mask_ptr = offset_mask.data_ptr() + 4 * deformable_groups * 2 * K * Ho * Wo
     call("aanet_mdcn_pw_f32", ptr(x), ptr(offset_mask), bs, _lib.ctypes.c_void_p(mask_ptr), bs, 1,
          float(mask_scale), ptr(packed_weight), ptr(bias), ptr(post_scale), ptr(post_shift),
          ACT[act], ptr(pw_packed), ptr(pw_bias), ptr(residual), ACT[pw_act], Co2, ptr(out), N, C,
          H, W, Co, kh, kw, stride, padding, dilation, deformable_groups,
+         None if desc is None else _lib.ctypes.byref(desc),
          _lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0, stream_of(x))
-    return out
+    return out if desc is None else (out, csa_out)
 
 
 def csa_sum(inputs, act="leaky"):

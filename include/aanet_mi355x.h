@@ -125,6 +125,21 @@ int aanet_conv2d_fused_f32(const float *x, const float *weight, const float *bia
                            int co, int kh, int kw, int stride, int pad, int dil, int groups,
                            int layout, aanet_stream_t stream);
 
+/* Cross-scale-aggregation epilogue of a tail kernel (nets/aggregation.py:387-400 for the output
+ * branch at the tail's resolution): besides `out`, write
+ *   out_csa = act(out + up(up[0]) + ... + up(up[num_up-1]))
+ * where up() is F.interpolate(bilinear, align_corners=False) by an exact factor 2 or 4
+ * (up_h * r == ho and up_w * r == wo); each up[j] is [n][co2][up_h][up_w].  Needs wo % 4 == 0
+ * and num_up <= 2 in this build (AANET_EUNSUPPORTED otherwise; 3 scales give at most 2 terms).
+ * act: 0 none, 1 ReLU, 2 LeakyReLU(0.2). */
+typedef struct {
+  float *out;
+  int num_up;
+  const float *up[3];
+  int up_h[3], up_w[3];
+  int act;
+} aanet_csa_epilogue_t;
+
 /* Bottleneck tail fusion (nets/deform.py:171-184 / 223-236 in eval): the pointwise conv3
  * (+ folded BN3) runs in the epilogue of conv2, so the conv2 activation never goes to HBM:
  *   t   = act(post_scale*(conv(x) + bias) + post_shift)                  [co channels]
@@ -132,21 +147,21 @@ int aanet_conv2d_fused_f32(const float *x, const float *weight, const float *bia
  * weight_packed / pw_weight_packed in the aanet_conv_weight_pack_f32 layout ([co2][co] for the
  * pointwise one).  Requires groups == 1, co <= 64, co2 <= 64.  The _mdcn_ form takes the
  * deformable sampler arguments of aanet_mdcn_fwd_fused_f32.  layout: AANET_LAYOUT_NCHW or
- * AANET_LAYOUT_IN_NHWC (the output is NCHW). */
+ * AANET_LAYOUT_IN_NHWC (the output is NCHW).  csa: optional CSA epilogue (NULL = none). */
 int aanet_conv2d_pw_f32(const float *x, const float *weight_packed, const float *bias,
                         const float *post_scale, const float *post_shift, int act,
                         const float *pw_weight_packed, const float *pw_bias,
                         const float *residual, int pw_act, int co2, float *out, int n, int c,
                         int h, int w, int co, int kh, int kw, int stride, int pad, int dil,
-                        int layout, aanet_stream_t stream);
+                        const aanet_csa_epilogue_t *csa, int layout, aanet_stream_t stream);
 int aanet_mdcn_pw_f32(const float *x, const float *offset, long offset_batch_stride,
                       const float *mask, long mask_batch_stride, int mask_logits,
                       float mask_scale, const float *weight_packed, const float *bias,
                       const float *post_scale, const float *post_shift, int act,
                       const float *pw_weight_packed, const float *pw_bias, const float *residual,
                       int pw_act, int co2, float *out, int n, int c, int h, int w, int co,
-                      int kh, int kw, int stride, int pad, int dil, int dg, int layout,
-                      aanet_stream_t stream);
+                      int kh, int kw, int stride, int pad, int dil, int dg,
+                      const aanet_csa_epilogue_t *csa, int layout, aanet_stream_t stream);
 
 /* Weight repack for the conv engine: [co][cg][kh][kw] -> [kh][kw][co][cg].  Done once per
  * weight version by the caller (the eval path caches it with the folded BN). */

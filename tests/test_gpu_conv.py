@@ -235,3 +235,68 @@ def test_mdcn_forward_fused_nhwc_input_vs_oracle():
                                  None, None, None, None, 1, 2, 2, dg, 2.0,
                                  packed_weight=ops.pack_weight(wd)).cpu().numpy()
     assert np.abs(got - ref).max() <= 2e-5 * (1 + np.abs(ref).max())
+
+
+@pytest.mark.parametrize("nhwc", [False, True])
+@pytest.mark.parametrize("H,W,ups", [(16, 52, [(8, 26), (4, 13)]), (12, 40, [(6, 20)]),
+                                     (8, 24, [(2, 6), (4, 12)])])
+def test_tail_csa_epilogue_matches_separate_sum(nhwc, H, W, ups):
+    """aanet_csa_epilogue_t: the tail kernel's cross-scale sum equals csa_sum over its output."""
+    gen = torch.Generator().manual_seed(H * W)
+    N, C = 2, 64
+    d = lambda t: t.to(DEV)  # noqa: E731
+    x = d(torch.randn(N, C, H, W, generator=gen))
+    w2 = d(torch.randn(C, C, 3, 3, generator=gen) / (3 * C ** 0.5))
+    b2 = d(torch.randn(C, generator=gen))
+    w3 = d(torch.randn(C, C, 1, 1, generator=gen) / C ** 0.5)
+    b3 = d(torch.randn(C, generator=gen))
+    ident = d(torch.randn(N, C, H, W, generator=gen))
+    terms = [d(torch.randn(N, C, h, w, generator=gen)) for h, w in ups]
+    xin = x.contiguous(memory_format=torch.channels_last) if nhwc else x
+    args = (w2, ops.pack_weight(w2), b2, None, None, "relu", ops.pack_weight(w3), b3, ident, "relu",
+            1, 1, 1)
+    out, csa = ops.conv2d_pw(xin, *args, csa_up=terms)
+    ref_out = ops.conv2d_pw(xin, *args)
+    ref_csa = ops.csa_sum([ref_out] + terms, act="leaky")
+    assert torch.equal(out, ref_out)
+    err = (csa - ref_csa).abs().max().item()
+    assert err <= 1e-5 * (1 + ref_csa.abs().max().item()), err
+    # and against torch's own interpolate
+    t = ref_out.cpu()
+    for u in terms:
+        t = t + F.interpolate(u.cpu(), size=(H, W), mode="bilinear", align_corners=False)
+    err = (csa.cpu() - F.leaky_relu(t, 0.2)).abs().max().item()
+    assert err <= 2e-5 * (1 + t.abs().max().item()), err
+
+
+def test_mdcn_tail_csa_epilogue_matches_separate_sum():
+    gen = torch.Generator().manual_seed(3)
+    N, C, H, W, dg = 2, 64, 16, 52, 2
+    d = lambda t: t.to(DEV)  # noqa: E731
+    x = d(torch.randn(N, C, H, W, generator=gen)).contiguous(memory_format=torch.channels_last)
+    om = d(torch.randn(N, dg * 27, H, W, generator=gen))
+    w2 = d(torch.randn(C, C, 3, 3, generator=gen) / (3 * C ** 0.5))
+    sc, sh = d(torch.rand(C, generator=gen) + 0.5), d(torch.randn(C, generator=gen))
+    w3 = d(torch.randn(C, C, 1, 1, generator=gen) / C ** 0.5)
+    b3 = d(torch.randn(C, generator=gen))
+    ident = d(torch.randn(N, C, H, W, generator=gen))
+    terms = [d(torch.randn(N, C, H // 2, W // 2, generator=gen)),
+             d(torch.randn(N, C, H // 4, W // 4, generator=gen))]
+    args = (om, w2, ops.pack_weight(w2), None, sc, sh, "relu", ops.pack_weight(w3), b3, ident,
+            "relu", 1, 2, 2, dg, 2.0)
+    out, csa = ops.mdcn_pw(x, *args, csa_up=terms)
+    ref_out = ops.mdcn_pw(x, *args)
+    assert torch.equal(out, ref_out)
+    ref_csa = ops.csa_sum([ref_out] + terms, act="leaky")
+    err = (csa - ref_csa).abs().max().item()
+    assert err <= 1e-5 * (1 + ref_csa.abs().max().item()), err
+
+
+def test_tail_csa_epilogue_rejects_non_integer_ratio():
+    N, C, H, W = 1, 32, 8, 24
+    x = torch.randn(N, C, H, W, device=DEV)
+    w2 = torch.randn(C, C, 3, 3, device=DEV)
+    w3 = torch.randn(C, C, 1, 1, device=DEV)
+    with pytest.raises(Exception):
+        ops.conv2d_pw(x, w2, ops.pack_weight(w2), None, None, None, "relu", ops.pack_weight(w3),
+                      None, None, "relu", 1, 1, 1, csa_up=[torch.randn(N, C, 3, 9, device=DEV)])
