@@ -106,7 +106,8 @@ def kernel_rooflines(model, left, right, batch, iters):
     res["disp_regress_s0"] = dict(bound="hbm", ms=ms, algo=reg_bytes, unit="GB/s",
                                   achieved=reg_bytes / ms / 1e6, peak=HBM_PEAK_GBS)
     # modulated DCN as the hot path runs it (DeformSimpleBottleneck of the last fusion, scale 0):
-    # NHWC conv1 output in, DCN + BN2 + ReLU -> conv3 + BN3 + identity + ReLU in one kernel
+    # NHWC conv1 output in, DCN + BN2 + ReLU -> conv3 + BN3 + identity + ReLU -> block output and
+    # the scale-0 cross-scale sum, in one kernel
     blk = model.aggregation.fusions[5].branches[0][0]
     with torch.no_grad():
         x1 = conv_bn_act(vol, blk.conv1, blk.bn1, "relu", out_nhwc=True)
@@ -116,8 +117,11 @@ def kernel_rooflines(model, left, right, batch, iters):
         ps, psh = bn_affine(blk.bn2)
         wp = folded(dc, None)[2]
         w3, b3, p3 = folded(blk.conv3, blk.bn3)
+        # the CSA epilogue's coarser exchange terms (2x and 4x smaller), as in the module
+        ups = [torch.randn(B, w3.shape[0], H // r, W // r, device=vol.device) for r in (2, 4)]
         fn = lambda: ops.mdcn_pw(x1, om, dc.weight, wp, dc.bias, ps, psh, "relu", p3, b3, vol,  # noqa: E731
-                                 "relu", 1, dc.padding, dc.dilation, c2.deformable_groups, 2.0)
+                                 "relu", 1, dc.padding, dc.dilation, c2.deformable_groups, 2.0,
+                                 csa_up=ups)
         ms = time_events(fn, iters, stream)
     Co, Ci = dc.weight.shape[:2]
     Co2 = w3.shape[0]
