@@ -216,23 +216,26 @@ constexpr int SP = 40;  // LDS row pitch (floats) of both staging tiles: conflic
 
 typedef int i2v __attribute__((ext_vector_type(2)));
 
+// K chunk = (tap k, channels [c0, c1)); chunks of ck channels, cut at deformable-group
+// boundaries when `cut` (a chunk that spans groups carries one sampling state per group).
+template <int CK>
 struct ChunkIt {
   int k, c0, c1;
-  __device__ __forceinline__ static int next_end(int c0, int cend, int cpg, int mode) {
-    int e = min(c0 + KC, cend);
-    if (mode) e = min(e, (c0 / cpg + 1) * cpg);
+  __device__ __forceinline__ static int next_end(int c0, int cend, int cpg, int cut) {
+    int e = min(c0 + CK, cend);
+    if (cut) e = min(e, (c0 / cpg + 1) * cpg);
     return e;
   }
-  __device__ __forceinline__ void first(int cbeg, int cend, int cpg, int mode) {
+  __device__ __forceinline__ void first(int cbeg, int cend, int cpg, int cut) {
     k = 0;
     c0 = cbeg;
-    c1 = next_end(cbeg, cend, cpg, mode);
+    c1 = next_end(cbeg, cend, cpg, cut);
   }
-  __device__ __forceinline__ void advance(int K, int cend, int cpg, int mode) {
+  __device__ __forceinline__ void advance(int K, int cend, int cpg, int cut) {
     if (++k == K) {
       k = 0;
       c0 = c1;
-      c1 = next_end(c0, cend, cpg, mode);
+      c1 = next_end(c0, cend, cpg, cut);
     }
   }
 };
@@ -302,30 +305,39 @@ __device__ __forceinline__ void make_samp4(int o[4], f32x4 &wv, float h, float w
 // LAYOUT bit 0: input NHWC (channels-last; each staging item is one 16-byte load of 4 channels
 // at one position, so a DCN corner or a conv tap of 32 channels is 8 lanes x 16 B = one 128-B
 // line; needs FULL).  Bit 1: output NHWC.
-template <int MODE, int CO_T, int PTT, int PACKED, int TAIL, int SCHED, int FULL, int LAYOUT>
+// CFG: chunk shape.  0: 32 channels of one deformable group; 1: 16 channels (16-channel conv
+// groups: the second MFMA half of a chunk is skipped); 2: 32 channels spanning two 16-channel
+// deformable groups (one sampling state per (pixel, group)).
+template <int MODE, int CO_T, int PTT, int PACKED, int TAIL, int SCHED, int FULL, int LAYOUT,
+          int CFG = 0>
 __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
+  constexpr int CK = CFG == 1 ? 16 : 32;   // channels per K chunk
+  constexpr int GPC = CFG == 2 ? 2 : 1;    // deformable groups per chunk
   constexpr int WC = CO_T >= 32 ? 2 : 1;   // waves along the output channels
   constexpr int WP = FNT / 64 / WC;        // waves along the pixels
   constexpr int NCB = CO_T / 16 / WC;      // 16-row output-channel blocks per wave
   constexpr int NPB = PTT / 16 / WP;       // 16-col pixel blocks per wave
-  constexpr int CPT = KC * PTT / FNT;      // im2col values staged per thread per chunk
-  constexpr int WPT = KC * CO_T / FNT;     // weights staged per thread per chunk
+  constexpr int CPT = CK * PTT / FNT;      // im2col values staged per thread per chunk
+  constexpr int WPT = CK * CO_T / FNT;     // weights staged per thread per chunk
   static_assert(NCB >= 1 && NPB >= 1 && WPT >= 1 && CPT % 4 == 0, "tile shape");
+  static_assert(CFG == 0 || FULL, "chunk configurations 1/2 need full chunks");
   constexpr bool INH = (LAYOUT & 1) != 0, ONH = (LAYOUT & 2) != 0;
-  constexpr int NIT = INH ? PTT * (KC / 4) / FNT : 1;  // NHWC staging items per thread
-  static_assert(!INH || (FULL && NIT >= 1 && FNT % (KC / 4) == 0), "NHWC staging needs full chunks");
+  constexpr int NIT = INH ? PTT * (CK / 4) / FNT : 1;  // NHWC staging items per thread
+  static_assert(!INH || (FULL && NIT >= 1 && FNT % (CK / 4) == 0), "NHWC staging needs full chunks");
   static_assert(!(ONH && TAIL), "NHWC output with a pointwise tail is not instantiated");
   constexpr int BUF = (PTT + CO_T) * SP; // floats per LDS buffer
   constexpr int OP = PTT + 4;            // epilogue tile pitch
   static_assert(CO_T * OP <= 2 * BUF, "epilogue tile must fit the staging buffers");
   // DCN: the sampling state of a (pixel, tap, deformable group) is computed once, by the threads
-  // tid < PTT, and published through a double-buffered LDS slot to the FNT/PTT threads that
-  // stage channels of that pixel (the VALU it saves is matrix-pipe time).
-  constexpr int PSLOT = PTT * 8;
+  // tid < GPC*PTT (group gi = tid / PTT of the chunk), and published through a double-buffered
+  // LDS slot to the threads that stage channels of that pixel and group (the VALU it saves is
+  // matrix-pipe time).
+  constexpr int PSLOT = GPC * PTT * 8;
   __shared__ __attribute__((aligned(16))) float smem[2 * BUF + (MODE ? 2 * PSLOT : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool pwave = __builtin_amdgcn_readfirstlane(wave) < PTT / 64;  // tid < PTT, as an SGPR
+  const bool pwave = __builtin_amdgcn_readfirstlane(wave) < GPC * PTT / 64;  // tid < GPC*PTT
+  const int pgi = MODE ? __builtin_amdgcn_readfirstlane(wave / (PTT / 64)) : 0;  // param group
   const int wc0 = __builtin_amdgcn_readfirstlane((wave / WP) * NCB);  // first co block of the wave
   const int wp0 = __builtin_amdgcn_readfirstlane((wave % WP) * NPB);  // first px block of the wave
   const long P = (long)a.Ho * a.Wo;
@@ -354,12 +366,12 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   const int ho = pvalid ? (int)(p / a.Wo) : 0, wo = pvalid ? (int)(p % a.Wo) : 0;
   const long psafe = pvalid ? p : 0;
   // NHWC staging roles: lane quad nq = channels 4nq..4nq+3, pixels npx[i]
-  const int nq = tid & (KC / 4 - 1);
+  const int nq = tid & (CK / 4 - 1);
   int npx[NIT], nho[NIT], nwo[NIT];
   bool nval[NIT];
 #pragma unroll
   for (int i = 0; i < NIT; ++i) {
-    npx[i] = tid / (KC / 4) + (FNT / (KC / 4)) * i;
+    npx[i] = tid / (CK / 4) + (FNT / (CK / 4)) * i;
     const long pp = (long)tile * PTT + npx[i];
     nval[i] = pp < P;
     nho[i] = nval[i] ? (int)(pp / a.Wo) : 0;
@@ -387,29 +399,29 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   int wlane[WPT];  // per-lane weight byte offsets (chunk-invariant)
 #pragma unroll
   for (int i = 0; i < WPT; ++i) {
-    const int e = tid + FNT * i, co = e / KC, cl = e % KC;
+    const int e = tid + FNT * i, co = e / CK, cl = e % CK;
     // rows past the chunk read a neighbouring channel (multiplied by a zero im2col value);
     // reads past the tensor are out of range -> 0; co past co_end is never stored
     wlane[i] = PACKED ? (co * Cg + cl) * 4 : (co * Cg * K + cl * K) * 4;
   }
   const int pl4 = (int)psafe * 4;
 
-  auto load_params_raw = [&](const ChunkIt &c) {
-    const int g = c.c0 / cpg;
+  auto load_params_raw = [&](const ChunkIt<CK> &c) {
+    const int g = c.c0 / cpg + pgi;
     const int ob = __builtin_amdgcn_readfirstlane((int)(((long)g * 2 * K + 2 * c.k) * P * 4));
     const int mb = __builtin_amdgcn_readfirstlane((int)(((long)g * K + c.k) * P * 4));
     off_h = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, pl4, ob, 0));
     off_w = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, pl4, ob + (int)(P * 4), 0));
     mlog = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mskr, pl4, mb, 0));
   };
-  auto finish_params = [&](const ChunkIt &c, int slot) {
+  auto finish_params = [&](const ChunkIt<CK> &c, int slot) {
 #pragma clang fp contract(off)
     const int i = c.k / a.kw, j = c.k % a.kw;
     float m = a.mask_logits ? a.mask_scale * __builtin_amdgcn_rcpf(1.f + __expf(-mlog)) : mlog;
     if (!pvalid) m = 0.f;
     const float h = (float)(ho * a.stride - a.pad + i * a.dil) + off_h;
     const float w = (float)(wo * a.stride - a.pad + j * a.dil) + off_w;
-    float *d = smem + 2 * BUF + slot * PSLOT + spx * 8;
+    float *d = smem + 2 * BUF + slot * PSLOT + (pgi * PTT + spx) * 8;
     if constexpr (INH) {
       int o[4];
       f32x4 wv;
@@ -429,7 +441,8 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     if constexpr (INH) {
 #pragma unroll
       for (int i = 0; i < NIT; ++i) {
-        const float *d = smem + 2 * BUF + slot * PSLOT + npx[i] * 8;
+        const int gi = GPC == 2 ? nq >> 2 : 0;  // 16-channel group of this lane's quad
+        const float *d = smem + 2 * BUF + slot * PSLOT + (gi * PTT + npx[i]) * 8;
         const f32x4 q = *reinterpret_cast<const f32x4 *>(d);
         const float q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];  // see below
         noff[i][0] = __builtin_bit_cast(int, q0);
@@ -440,7 +453,8 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       }
       return;
     }
-    const float *d = smem + 2 * BUF + slot * PSLOT + spx * 8;
+    const int gi = GPC == 2 ? scb >> 4 : 0;  // scb: multiple of CPT (8) -> one group per thread
+    const float *d = smem + 2 * BUF + slot * PSLOT + (gi * PTT + spx) * 8;
     const f32x4 q = *reinterpret_cast<const f32x4 *>(d);
     // copy the elements to scalars first: __builtin_bit_cast of an ext-vector element lvalue
     // (q[1]) reads element 0 with this clang
@@ -450,7 +464,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     snext.wt = f2v{q[2], q[3]};
     snext.wb = *reinterpret_cast<const f2v *>(d + 4);
   };
-  auto issue_loads = [&](const ChunkIt &c) {
+  auto issue_loads = [&](const ChunkIt<CK> &c) {
     const int rows = c.c1 - c.c0;
     const int wbase = PACKED ? (((c.k * a.Co + co0) * Cg + (c.c0 - cbeg)) * 4)
                              : (((co0 * Cg + (c.c0 - cbeg)) * K + c.k) * 4);
@@ -500,13 +514,13 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       }
     }
   };
-  auto store_stage = [&](const ChunkIt &c, int buf) {
+  auto store_stage = [&](const ChunkIt<CK> &c, int buf) {
     float *sC = smem + buf * BUF, *sW = sC + PTT * SP;
     const int rows = c.c1 - c.c0;
 #pragma unroll
     for (int i = 0; i < WPT; ++i) {
       const int e = tid + FNT * i;
-      sW[(e / KC) * SP + e % KC] = wreg[i];
+      sW[(e / CK) * SP + e % CK] = wreg[i];
     }
     if constexpr (INH) {
 #pragma unroll
@@ -550,8 +564,9 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     for (int b = 0; b < NPB; ++b) acc[m][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int kr = lane >> 4, jj = lane & 15;
-  ChunkIt cur, nxt, nn;
-  cur.first(cbeg, cend, cpg, MODE);
+  constexpr int CUT = MODE && GPC == 1;  // chunks stop at deformable-group boundaries
+  ChunkIt<CK> cur, nxt, nn;
+  cur.first(cbeg, cend, cpg, CUT);
   if (MODE) {
     if (pwave) {
       load_params_raw(cur);
@@ -563,7 +578,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   issue_loads(cur);
   store_stage(cur, 0);
   nxt = cur;
-  nxt.advance(K, cend, cpg, MODE);
+  nxt.advance(K, cend, cpg, CUT);
   bool has_next = nxt.c0 < cend;
   if (MODE && has_next && pwave) {
     load_params_raw(nxt);
@@ -606,7 +621,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
 
   for (int buf = 0;; buf ^= 1) {
     nn = nxt;
-    nn.advance(K, cend, cpg, MODE);
+    nn.advance(K, cend, cpg, CUT);
     const bool has_nn = has_next && nn.c0 < cend;
     if (has_next) {
       if (MODE) get_params(slot);
@@ -619,9 +634,13 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       // The half-1 operands are read before the staging writes: LDS reads and writes of the two
       // buffers cannot be proven disjoint, so reads issued after the writes would hold every
       // MFMA of half 1 behind the whole staging store.
-      mfma_half(buf, 0);
       Frag f1;
-      read_frag(buf, 1, f1);
+      if (CK == 32) {
+        mfma_half(buf, 0);
+        read_frag(buf, 1, f1);
+      } else {  // 16-channel chunks: one half, which carries the staging interleave
+        read_frag(buf, 0, f1);
+      }
       if (!has_next) {
         mma(f1);
         break;
@@ -635,7 +654,8 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
         if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS_WRITE
       }
     } else {
-      mfma_chunk(buf);
+      mfma_half(buf, 0);
+      if (CK == 32) mfma_half(buf, 1);
       if (!has_next) break;
       store_stage(nxt, buf ^ 1);
     }
@@ -1126,33 +1146,47 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
   return a;
 }
 
-template <int MODE, int CO_T, int PTT, int FULL>
+template <int MODE, int CO_T, int PTT, int FULL, int CFG>
 void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
   const dim3 blk(FNT);
   if (a.tail_w) {
     if (FULL && a.layout == 1)
-      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1, FULL, FULL ? 1 : 0>), grid, blk, 0, st, a);
+      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1, FULL, FULL ? 1 : 0, CFG>), grid, blk, 0, st, a);
     else
-      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1, FULL, 0>), grid, blk, 0, st, a);
+      hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1, FULL, 0, CFG>), grid, blk, 0, st, a);
   } else if (packed) {
     switch (FULL ? a.layout : 0) {
-      case 1: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, FULL ? 1 : 0>), grid, blk, 0, st, a); break;
-      case 2: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 2>), grid, blk, 0, st, a); break;
-      case 3: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, FULL ? 3 : 2>), grid, blk, 0, st, a); break;
-      default: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 0>), grid, blk, 0, st, a); break;
+      case 1: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, FULL ? 1 : 0, CFG>), grid, blk, 0, st, a); break;
+      case 2: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 2, CFG>), grid, blk, 0, st, a); break;
+      case 3: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, FULL ? 3 : 2, CFG>), grid, blk, 0, st, a); break;
+      default: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, FULL, 0, CFG>), grid, blk, 0, st, a); break;
     }
   } else {
-    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 0, 0, 0, FULL, 0>), grid, blk, 0, st, a);
+    hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 0, 0, 0, FULL, 0, CFG>), grid, blk, 0, st, a);
   }
+}
+
+// Chunk configuration (conv_fwd_kernel CFG) for which every chunk is full, or -1.
+int full_cfg(const MdcnArgs &a, int mode, int co_t) {
+  const int Cg = a.C / a.groups, cpg = a.C / a.dg;
+  if (Cg % KC == 0 && (!mode || cpg % KC == 0)) return 0;
+  if (mode && Cg % KC == 0 && cpg == 16) return 2;
+  if (co_t >= 32 && Cg % 16 == 0 && (!mode || cpg % 16 == 0)) return 1;
+  return -1;
 }
 
 template <int MODE, int CO_T, int PTT>
 void launch_fwd_t(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
-  const int Cg = a.C / a.groups, cpg = a.C / a.dg;
-  if (Cg % KC == 0 && (!MODE || cpg % KC == 0))
-    launch_fwd_f<MODE, CO_T, PTT, 1>(a, packed, grid, st);
+  const int cfg = full_cfg(a, MODE, CO_T);
+  constexpr bool C1 = CO_T >= 32 && PTT == 128;  // 16-channel chunks: 4 staged values per thread
+  if (cfg == 0)
+    launch_fwd_f<MODE, CO_T, PTT, 1, 0>(a, packed, grid, st);
+  else if (cfg == 1 && C1)
+    launch_fwd_f<MODE, CO_T, PTT, 1, C1 ? 1 : 0>(a, packed, grid, st);
+  else if (cfg == 2 && MODE)
+    launch_fwd_f<MODE, CO_T, PTT, 1, MODE ? 2 : 0>(a, packed, grid, st);
   else
-    launch_fwd_f<MODE, CO_T, PTT, 0>(a, packed, grid, st);
+    launch_fwd_f<MODE, CO_T, PTT, 0, 0>(a, packed, grid, st);
 }
 
 template <int MODE>
@@ -1174,21 +1208,21 @@ int launch_fwd(const MdcnArgs &a, int packed, hipStream_t st) {
         return AANET_EUNSUPPORTED;
     }
   }
-  if (a.layout) {  // NHWC paths: packed weights, full 32-channel chunks, 4-channel quads
-    const int Cg = a.C / a.groups, cpg = a.C / a.dg;
-    if (!packed || Cg % KC || (MODE && cpg % KC) || a.C % 4) return AANET_EUNSUPPORTED;
-    if ((a.layout & 2) && (a.tail_w || Cog % 4)) return AANET_EUNSUPPORTED;
-  }
   int co_t = Cog <= 16 ? 16 : (Cog <= 32 ? 32 : 64);
   if (a.tail_w) {  // the whole conv output column of a pixel must sit in one workgroup
     if (a.groups != 1 || a.Co > 64 || a.Co2 <= 0 || a.Co2 > 64 || !packed) return AANET_EUNSUPPORTED;
     co_t = max(a.Co, a.Co2) <= 16 ? 16 : (max(a.Co, a.Co2) <= 32 ? 32 : 64);
+  }
+  if (a.layout) {  // NHWC paths: packed weights, full chunks (full_cfg), 4-channel quads
+    if (!packed || a.C % 4 || full_cfg(a, MODE, co_t) < 0) return AANET_EUNSUPPORTED;
+    if ((a.layout & 2) && (a.tail_w || Cog % 4)) return AANET_EUNSUPPORTED;
   }
   const int ncot = host_div_up(Cog, co_t);
   // 128-pixel tiles when they still give >= 4 workgroups per CU, else 64
   int ptt = co_t == 16 || (long)a.N * host_div_up(P, 128) * a.groups * ncot >= 1024 ? 128 : 64;
   static const int ptt_env = [] { const char *e = getenv("AANET_PTT"); return e ? atoi(e) : 0; }();
   if (ptt_env == 64 && co_t != 16) ptt = 64;  // A/B switch (tools/conv_microbench.py)
+  if (full_cfg(a, MODE, co_t) == 1) ptt = 128;  // 16-channel chunks are staged 4 per thread
   dim3 grid((unsigned)(a.N * host_div_up(P, ptt)), (unsigned)(a.groups * ncot));
   if (ptt == 128) {
     switch (co_t) {

@@ -115,7 +115,8 @@ class _BottleneckBase(nn.Module):
         c2 = self.conv2
         if deform:
             pw = c2.modulation and c2.deform_conv.stride == 1 and width <= 64 and w3.shape[0] <= 64
-            nhwc = pw and width % 32 == 0 and (width // c2.deformable_groups) % 32 == 0
+            cpg = width // c2.deformable_groups  # 32k-channel groups, or pairs of 16-channel ones
+            nhwc = pw and width % 32 == 0 and (cpg % 32 == 0 or cpg == 16)
         else:
             pw = c2.groups == 1 and width <= 64 and w3.shape[0] <= 64 and \
                 c2.stride[0] == c2.stride[1] and c2.padding[0] == c2.padding[1]

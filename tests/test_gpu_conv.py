@@ -129,6 +129,8 @@ NHWC_CASES = [
     (2, 64, 16, 52, 54, 3, 1, 2, 2, 2),      # offset_conv on the NHWC conv1 output
     (1, 64, 9, 27, 32, 3, 2, 1, 1, 1),       # strided, odd sizes, 64-px tiles
     (1, 128, 5, 11, 40, 3, 1, 1, 1, 4),      # 4 groups of 32, Co not a tile multiple
+    (2, 32, 9, 26, 54, 3, 1, 2, 2, 2),       # scale-1 offset_conv: 16-channel groups (CFG 1)
+    (1, 64, 7, 20, 80, 3, 1, 1, 1, 4),       # 16-channel groups, Cog 20
 ]
 
 
@@ -163,9 +165,14 @@ def test_conv2d_fused_nhwc_vs_torch_cpu(case, layout):
 
 
 def test_conv2d_nhwc_requires_full_chunks():
+    from aanet_amd._lib import AanetError
     x = torch.randn(1, 16, 8, 8, device=DEV).contiguous(memory_format=torch.channels_last)
     w = torch.randn(16, 16, 3, 3, device=DEV)
-    with pytest.raises(Exception):
+    with pytest.raises(AanetError):  # 16-channel chunks need >= 32-wide output tiles
+        ops.conv2d_fused(x, w, None, 1, 1, 1, 1, packed_weight=ops.pack_weight(w))
+    x = torch.randn(1, 24, 8, 8, device=DEV).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(32, 24, 3, 3, device=DEV)
+    with pytest.raises(AanetError):  # 24 channels: no full-chunk configuration
         ops.conv2d_fused(x, w, None, 1, 1, 1, 1, packed_weight=ops.pack_weight(w))
 
 
@@ -188,12 +195,15 @@ def test_conv2d_pw_tail_nhwc_input(C, H, W):
     assert err <= 3e-5 * (1 + ref.abs().max().item()), err
 
 
-@pytest.mark.parametrize("C,H,W,off_scale", [(64, 16, 52, 1.0), (64, 9, 26, 3.0), (32, 7, 19, 1.0)])
-def test_mdcn_pw_tail_nhwc_input_vs_oracle(C, H, W, off_scale):
-    """DCN with NHWC corner loads (+BN2+ReLU, mask = 2*sigmoid) -> conv3 + identity + ReLU."""
+@pytest.mark.parametrize("C,H,W,off_scale,dg", [(64, 16, 52, 1.0, 2), (64, 9, 26, 3.0, 2),
+                                                (32, 7, 19, 1.0, 1), (32, 9, 26, 1.5, 2),
+                                                (64, 6, 17, 2.0, 4)])
+def test_mdcn_pw_tail_nhwc_input_vs_oracle(C, H, W, off_scale, dg):
+    """DCN with NHWC corner loads (+BN2+ReLU, mask = 2*sigmoid) -> conv3 + identity + ReLU.
+    dg with 16-channel groups: chunks span two groups, one sampling state each (CFG 2)."""
     from oracle import oracle
     rng = np.random.default_rng(C + W)
-    N, dg = 2, C // 32
+    N = 2
     x = rng.standard_normal((N, C, H, W)).astype(np.float32)
     om = rng.standard_normal((N, dg * 27, H, W)).astype(np.float32)
     om[:, :dg * 18] *= off_scale

@@ -165,3 +165,20 @@ def test_deform_conv_cuda_shim_matches_reference_call_sequence():
     rx, roff, rm, rw, rb = oracle.mdcn_backward(x, off, msk, w, go, True, 1, 2, 2, 1, 2)
     for got, r in ((gi, rx), (goff, roff), (gm, rm), (gw, rw + 1), (gb, rb + 1)):
         assert np.abs(t2n(got) - r).max() <= 1e-4 * (np.abs(r).max() + 1)
+
+
+@pytest.mark.parametrize("C,dg,Co", [(32, 2, 32), (64, 4, 64), (32, 2, 48)])
+@pytest.mark.parametrize("packed", [False, True])
+def test_mdcn_fused_sixteen_channel_groups_vs_oracle(C, dg, Co, packed):
+    """16-channel deformable groups: 32-channel chunks spanning two groups (conv engine CFG 2)."""
+    rng = np.random.default_rng(C * dg)
+    N, H, W = 2, 9, 26
+    x = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    om = (rng.standard_normal((N, dg * 27, H, W)) * 1.5).astype(np.float32)
+    w = (rng.standard_normal((Co, C, 3, 3)) / (3 * C ** 0.5)).astype(np.float32)
+    mask = (2.0 / (1.0 + np.exp(-om[:, dg * 18:].astype(np.float64)))).astype(np.float32)
+    ref = oracle.mdcn_forward(x, om[:, :dg * 18], mask, w, None, 1, 2, 2, 1, dg)
+    wd = g2t(w)
+    got = ops.mdcn_forward_fused(g2t(x), g2t(om), wd, None, None, None, None, 1, 2, 2, dg, 2.0,
+                                 packed_weight=ops.pack_weight(wd) if packed else None)
+    assert np.abs(t2n(got) - ref).max() <= 2e-5 * (1 + np.abs(ref).max())
