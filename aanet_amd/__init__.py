@@ -1,10 +1,12 @@
 """aanet_amd -- MI355X-native (gfx950) AANet cost-volume hot path.
 
 Layers: include/aanet_mi355x.h (C ABI, HIP kernels in aanet_amd/csrc) -> aanet_amd._lib (ctypes)
--> aanet_amd.ops (autograd ops) -> aanet_amd.nets (drop-in modules mirroring the reference's
+-> aanet_amd.ops (autograd ops; also registered as torch.ops.aanet.*, aanet_amd.torch_ops)
+-> aanet_amd.nets (drop-in modules mirroring the reference's
 nets/ API).  No CPU fallback: ops raise on non-HIP tensors or a missing library.
 """
 from . import _lib, ops  # noqa: F401
+from . import torch_ops  # noqa: F401  (registers torch.ops.aanet.*)
 
 __version__ = "0.1.0"
 

@@ -90,3 +90,25 @@ def test_hot_path_module_api_mirrors_aanet():
 def test_package_exposes_native_library_path():
     assert aanet_amd.native_library_path().endswith("libaanet_mi355x.so")
     assert os.path.exists(aanet_amd.native_library_path())
+
+
+def test_torch_ops_registered_and_refuse_cpu():
+    """torch.ops.aanet.* exist (SURVEY §8b op-level API), shape-propagate through fake kernels,
+    and have no CPU kernel (the reference DCN is CUDA-only)."""
+    import torch
+    import aanet_amd  # noqa: F401  (registers the ops)
+    from aanet_amd.torch_ops import OPS
+    for name in OPS:
+        assert hasattr(torch.ops.aanet, name), name
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    with FakeTensorMode():
+        x = torch.empty(2, 8, 10, 12)
+        w = torch.empty(6, 8, 3, 3)
+        off, msk = torch.empty(2, 18, 10, 12), torch.empty(2, 9, 10, 12)
+        y = torch.ops.aanet.mdcn_forward(x, off, msk, w, None, 1, 2, 2, 1, 1)
+        assert tuple(y.shape) == (2, 6, 10, 12)
+        v = torch.ops.aanet.corr_volume(x, x, 5)
+        assert tuple(v.shape) == (2, 5, 10, 12)
+        assert tuple(torch.ops.aanet.disp_regress(v, False).shape) == (2, 10, 12)
+    with pytest.raises(NotImplementedError):
+        torch.ops.aanet.corr_volume(torch.randn(1, 4, 3, 5), torch.randn(1, 4, 3, 5), 2)

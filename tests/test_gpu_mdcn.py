@@ -182,3 +182,36 @@ def test_mdcn_fused_sixteen_channel_groups_vs_oracle(C, dg, Co, packed):
     got = ops.mdcn_forward_fused(g2t(x), g2t(om), wd, None, None, None, None, 1, 2, 2, dg, 2.0,
                                  packed_weight=ops.pack_weight(wd) if packed else None)
     assert np.abs(t2n(got) - ref).max() <= 2e-5 * (1 + np.abs(ref).max())
+
+
+def test_torch_ops_match_functional_ops_and_autograd():
+    """torch.ops.aanet.* (custom operators) == aanet_amd.ops, gradients included."""
+    import aanet_amd  # noqa: F401
+    rng = np.random.default_rng(11)
+    N, C, H, W, Co, dg = 2, 16, 9, 13, 8, 2
+    x = g2t(rng.standard_normal((N, C, H, W)).astype(np.float32)).requires_grad_()
+    off = g2t(rng.standard_normal((N, dg * 18, H, W)).astype(np.float32)).requires_grad_()
+    msk = g2t(rng.uniform(0, 1, (N, dg * 9, H, W)).astype(np.float32)).requires_grad_()
+    w = g2t((rng.standard_normal((Co, C, 3, 3)) * 0.1).astype(np.float32)).requires_grad_()
+    b = g2t(rng.standard_normal(Co).astype(np.float32)).requires_grad_()
+    y1 = torch.ops.aanet.mdcn_forward(x, off, msk, w, b, 1, 2, 2, 1, dg)
+    y2 = ops.modulated_deform_conv(x, off, msk, w, b, 1, 2, 2, 1, dg)
+    assert torch.equal(y1, y2)
+    gy = torch.randn_like(y1)
+    g1 = torch.autograd.grad(y1, (x, off, msk, w, b), gy)
+    g2 = torch.autograd.grad(y2, (x, off, msk, w, b), gy)
+    for a, c in zip(g1, g2):
+        assert torch.allclose(a, c, rtol=1e-5, atol=1e-5 * (1 + c.abs().max().item()))
+    L = torch.randn(2, 32, 6, 20, device="cuda", requires_grad=True)
+    R = torch.randn(2, 32, 6, 20, device="cuda", requires_grad=True)
+    v1 = torch.ops.aanet.corr_volume(L, R, 8)
+    v2 = ops.CorrelationVolumeFunction.apply(L, R, 8)
+    assert torch.equal(v1, v2)
+    d1 = torch.ops.aanet.disp_regress(v1, False)
+    d2 = ops.DisparityRegressionFunction.apply(v2, False)
+    assert torch.equal(d1, d2)
+    gd = torch.randn_like(d1)
+    ga = torch.autograd.grad(d1, (L, R), gd)
+    gb = torch.autograd.grad(d2, (L, R), gd)
+    for a, c in zip(ga, gb):
+        assert torch.equal(a, c)
