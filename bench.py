@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="time eager launches, not a HIP graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=20)
+    ap.add_argument("--features", default="randn", choices=sorted(FEATURE_KINDS),
+                    help="synthetic feature variant (SURVEY.md §8d)")
     ap.add_argument("--only", default=None,
                     help="profiling mode: run only one kernel family (corr|mdcn|regress|step)")
     return ap.parse_args()
@@ -67,11 +69,37 @@ def build_model(device):
     return m.to(device).eval()
 
 
-def make_features(batch, rank, device):
+FEATURE_KINDS = {
+    "randn": "N(0,1) feature pyramids",
+    "relu": "post-ReLU |N(0,1)| feature pyramids",
+    "structured": "random texture, right = left shifted by a known per-row disparity in [0,63] "
+                  "at 1/3 scale (2x2-average-pooled for 1/6, 1/12), so the softmax is peaked",
+}
+
+
+def make_features(batch, rank, device, kind="randn"):
+    """SURVEY.md §8(d) primary timed unit: seeded (1234 + rank) on-device feature pyramids."""
     gen = torch.Generator(device=device).manual_seed(1234 + rank)
     shapes = [(batch, FEAT_C, (H_IMG // 3) >> s, (W_IMG // 3) >> s) for s in range(3)]
-    left = [torch.randn(s, device=device, generator=gen) for s in shapes]
-    right = [torch.randn(s, device=device, generator=gen) for s in shapes]
+    if kind in ("randn", "relu"):
+        left = [torch.randn(s, device=device, generator=gen) for s in shapes]
+        right = [torch.randn(s, device=device, generator=gen) for s in shapes]
+        if kind == "relu":
+            left, right = [t.abs_() for t in left], [t.abs_() for t in right]
+        return left, right
+    if kind != "structured":
+        raise SystemExit(f"unknown --features {kind}")
+    B, C, H, W = shapes[0]
+    tex = torch.randn((B, C, H, W + MAXD), device=device, generator=gen)
+    d = torch.randint(0, MAXD, (B, 1, H, 1), device=device, generator=gen)
+    x = torch.arange(W, device=device).view(1, 1, 1, W)
+    left0 = tex[..., MAXD:].contiguous()                       # L(x) = T(x + MAXD)
+    idx = (x + MAXD - d).expand(B, C, H, W)                    # R(x) = T(x + MAXD - d) = L(x - d)
+    right0 = torch.gather(tex, 3, idx).contiguous()
+    left, right = [left0], [right0]
+    for _ in range(2):
+        left.append(torch.nn.functional.avg_pool2d(left[-1], 2).contiguous())
+        right.append(torch.nn.functional.avg_pool2d(right[-1], 2).contiguous())
     return left, right
 
 
@@ -164,7 +192,7 @@ def main():
         dist.init_process_group("nccl", device_id=device)
 
     model = build_model(device)
-    left, right = make_features(args.batch, rank, device)
+    left, right = make_features(args.batch, rank, device, args.features)
 
     def step():
         with torch.no_grad():
@@ -232,7 +260,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (N(0,1) feature pyramids on device, seeded per rank; random-init weights)",
+            "data": f"synthetic ({FEATURE_KINDS[args.features]} on device, seeded per rank; "
+                    "random-init weights)",
             "config": {
                 "workload": "C2: KITTI 384x1248 stereo pairs, features 128ch at 1/3,1/6,1/12, "
                             "correlation volume D=64/32/16 -> AdaptiveAggregation (6 fusions, 3 "
