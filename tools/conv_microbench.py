@@ -24,6 +24,9 @@ p1, p3, po = ops.pack_weight(w1), ops.pack_weight(w3), ops.pack_weight(wo)
 om = ops.conv2d_fused(x, wo, bo, 1, 2, 2, 2, packed_weight=po)
 xn = x.contiguous(memory_format=torch.channels_last)
 up1, up2 = res[:, :, :64, :208].contiguous(), res[:, :, :32, :104].contiguous()
+fl = torch.randn(B, 128, H, W, device=dev, generator=g)
+fr = torch.randn(B, 128, H, W, device=dev, generator=g)
+vol64 = torch.randn(B, 64, H, W, device=dev, generator=g)
 cases = {
     "conv1x1": (lambda: ops.conv2d_fused(x, w1, b, act="relu", packed_weight=p1), 2 * B * H * W * C * C),
     "conv1x1_res": (lambda: ops.conv2d_fused(x, w1, b, act="relu", residual=res, packed_weight=p1),
@@ -51,6 +54,8 @@ cases = {
     "conv3x3_pw_nhwc": (lambda: ops.conv2d_pw(xn, w3, p3, b, None, None, "relu", p1, b, res, "relu", 1, 1, 1),
                         2 * B * H * W * C * C * 10),
     "csa_sum": (lambda: ops.csa_sum([x, up1, up2]), 0),
+    "corr": (lambda: ops.corr_volume(fl, fr, 64), 0),
+    "regress": (lambda: ops.disp_regress(vol64), 0),
 }
 for name, (fn, flops) in cases.items():
     if names and name not in names:
@@ -64,4 +69,7 @@ for name, (fn, flops) in cases.items():
     e.record()
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / iters
-    print(f"{name:12s} {ms * 1e3:8.1f} us  {flops / ms / 1e9 if flops else 0:6.1f} TF/s")
+    gbs = {"corr": 4 * (2 * B * 128 * H * W + B * 64 * H * W), "regress": 4 * (B * 64 * H * W + B * H * W),
+           "csa_sum": 4 * (2 * B * C * H * W + B * C * H * W * 5 // 16)}.get(name)
+    rate = f"{gbs / ms / 1e6:6.0f} GB/s" if gbs else f"{flops / ms / 1e9:6.1f} TF/s"
+    print(f"{name:12s} {ms * 1e3:8.1f} us  {rate}")
