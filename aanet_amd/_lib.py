@@ -31,6 +31,7 @@ _SIGNATURES = {
     "aanet_mdcn_fwd_f32": [_P, _P, _P, _P, _P, _P] + [_I] * 12 + [_P],
     "aanet_mdcn_fwd_fused_f32": [_P, _P, _L, _P, _L, _I, _F, _P, _I, _P, _P, _P, _I, _P] + [_I] * 13 + [_P],
     "aanet_mdcn_bwd_f32": [_P] * 10 + [_I] * 12 + [_P],
+    "aanet_mdcn_bwd_det_f32": [_P] * 10 + [_I] * 12 + [_P, ctypes.c_size_t, _P],
     "aanet_conv2d_fused_f32": [_P] * 6 + [_I, _I, _P] + [_I] * 12 + [_P],
     "aanet_conv_weight_pack_f32": [_P, _P, _I, _I, _I, _I, _P],
     "aanet_conv2d_pw_f32": [_P] * 5 + [_I] + [_P] * 3 + [_I, _I, _P] + [_I] * 10 + [_P, _I, _P],
@@ -63,13 +64,16 @@ def lib():
             f.restype = _I
         L.aanet_status_string.argtypes = [_I]
         L.aanet_status_string.restype = ctypes.c_char_p
+        L.aanet_mdcn_bwd_det_workspace_size.argtypes = [_I] * 12
+        L.aanet_mdcn_bwd_det_workspace_size.restype = ctypes.c_size_t
         L.aanet_version.restype = _I
         _lib = L
     return _lib
 
 
 def exported_symbols():
-    return ["aanet_version", "aanet_status_string"] + list(_SIGNATURES)
+    return (["aanet_version", "aanet_status_string", "aanet_mdcn_bwd_det_workspace_size"]
+            + list(_SIGNATURES))
 
 
 def call(name, *args):

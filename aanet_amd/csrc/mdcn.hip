@@ -896,11 +896,18 @@ __global__ void mdcn_sample_index_kernel(MdcnArgs a, int *__restrict__ hl, int *
 // then each thread (pixel, channel subset) accumulates grad_mask / grad_offset partials
 // (kernel.cu:695-767) and scatters grad_x to the 4 bilinear corners (kernel.cu:635-693,
 // float atomics like the reference).
+// DET: grad_x is accumulated in 64-bit fixed point (value * scale, scale a power of two chosen
+// on the device from a bound on any single contribution, det_bound_kernel).  Integer adds are
+// associative, so the sum -- and the fp32 grad_x converted from it -- does not depend on the
+// order in which the atomics land: the deterministic backward of torch's
+// use_deterministic_algorithms (the reference's col2im atomics, kernel.cu:688, are not).
+template <int DET>
 __global__ __launch_bounds__(NT) void mdcn_bwd_data_kernel(MdcnArgs a, const float *__restrict__ gout,
                                                            float *__restrict__ gx,
                                                            float *__restrict__ goff,
                                                            float *__restrict__ gmask, int GP,
-                                                           int WTP) {
+                                                           int WTP, long long *__restrict__ gxi,
+                                                           const double *__restrict__ det_scale) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int Co = a.Co;
   float *sG = sm;                       // [Co][GP]      gOut tile
@@ -919,6 +926,15 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_kernel(MdcnArgs a, const flo
   const long HW = (long)a.H * a.W;
   const float *xn = a.x + (long)n * C * HW;
   float *gxn = gx + (long)n * C * HW;
+  long long *gxin = DET ? gxi + (long)n * C * HW : nullptr;
+  const double scale = DET ? *det_scale : 1.0;
+  auto scatter = [&](long idx, float v) {
+    if (DET)
+      atomicAdd(reinterpret_cast<unsigned long long *>(gxin + idx),
+                (unsigned long long)__double2ll_rn((double)v * scale));
+    else
+      atomicAdd(gxn + idx, v);
+  };
 
   for (int e = tid; e < Co * PT; e += NT) {
     const int co = e / PT, pl = e % PT;
@@ -972,11 +988,11 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_kernel(MdcnArgs a, const flo
           const float top = cg * s.m;
           goh += wh * top;
           gow += ww * top;
-          float *gim = gxn + (long)c * HW;
-          if (s.ok & 1) atomicAdd(gim + s.i1, hh * hw * top);
-          if (s.ok & 2) atomicAdd(gim + s.i2, hh * s.lw * top);
-          if (s.ok & 4) atomicAdd(gim + s.i3, s.lh * hw * top);
-          if (s.ok & 8) atomicAdd(gim + s.i4, s.lh * s.lw * top);
+          const long cb = (long)c * HW;
+          if (s.ok & 1) scatter(cb + s.i1, hh * hw * top);
+          if (s.ok & 2) scatter(cb + s.i2, hh * s.lw * top);
+          if (s.ok & 4) scatter(cb + s.i3, s.lh * hw * top);
+          if (s.ok & 8) scatter(cb + s.i4, s.lh * s.lw * top);
         }
       }
     }
@@ -1006,9 +1022,12 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_kernel(MdcnArgs a, const flo
 // images flattened) x one 64-wide output-channel tile.  The col chunk is re-sampled into LDS
 // per 64-pixel sub-tile, the [co][c] tile accumulates in MFMA registers across the whole
 // pixel range, then one float atomic per element (grad accumulates, cpp:660-669).
+// DET: each pixel-range split writes its partial sums to part[split][co][c][k] (no atomics);
+// det_weight_reduce_kernel adds them to grad_weight in split order.
+template <int DET>
 __global__ __launch_bounds__(NT) void mdcn_bwd_weight_kernel(MdcnArgs a, const float *__restrict__ gout,
                                                              float *__restrict__ gw, int npieces,
-                                                             long range) {
+                                                             long range, float *__restrict__ part) {
   constexpr int GP2 = PT + 2;  // A/B reads (16 rows x 4 cols per 16 lanes) conflict-free
   __shared__ __attribute__((aligned(16))) float sG[64 * GP2];
   __shared__ __attribute__((aligned(16))) float sC[KC * GP2];
@@ -1066,7 +1085,13 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_weight_kernel(MdcnArgs a, const f
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int co = co0 + 16 * wave + 4 * kr + r, cl = 16 * cb + jj;
-      if (co < Co && cl < rows) atomicAdd(gw + ((long)co * C + c0 + cl) * K + k, acc[cb][r]);
+      if (co < Co && cl < rows) {
+        const long e = ((long)co * C + c0 + cl) * K + k;
+        if (DET)
+          part[(long)blockIdx.y * Co * C * K + e] = acc[cb][r];
+        else
+          atomicAdd(gw + e, acc[cb][r]);
+      }
     }
 }
 
@@ -1240,6 +1265,55 @@ int launch_fwd(const MdcnArgs &a, int packed, hipStream_t st) {
   return aanet_launch_status();
 }
 
+// ---- deterministic-backward helpers ---------------------------------------------------------
+// bounds[0] = max_{c,k} sum_co |W[co][c][k]|, bounds[1] = max|gOut|, bounds[2] = max|mask|, as
+// float bits (non-negative floats order like their bit patterns).  Every grad_x contribution is
+// colg * w_corner * m with |colg| <= bounds[0]*bounds[1] and |w_corner| <= 1.
+__global__ __launch_bounds__(256) void det_wbound_kernel(const float *__restrict__ w, int Co, int CK,
+                                                         unsigned *__restrict__ bounds) {
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < CK; e += gridDim.x * 256) {
+    float s = 0.f;
+    for (int co = 0; co < Co; ++co) s += fabsf(w[(long)co * CK + e]);
+    atomicMax(bounds, __float_as_uint(s));
+  }
+}
+
+__global__ __launch_bounds__(256) void det_absmax_kernel(const float *__restrict__ v, long n,
+                                                         unsigned *__restrict__ slot) {
+  float m = 0.f;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256)
+    m = fmaxf(m, fabsf(v[e]));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(slot, __float_as_uint(m));
+}
+
+// scale = 2^(38 - ceil(log2 bound)): a single contribution stays below 2^38, so up to 2^25 of
+// them can meet in one element before the int64 sum could overflow; the fixed-point step
+// (2^-38 of the largest possible contribution) is far below fp32 rounding of typical sums.
+__global__ void det_scale_kernel(const unsigned *__restrict__ bounds, double *__restrict__ scale) {
+  const double b = (double)__uint_as_float(bounds[0]) * (double)__uint_as_float(bounds[1]) *
+                   (double)__uint_as_float(bounds[2]);
+  *scale = (b > 0.0 && isfinite(b)) ? ldexp(1.0, 38 - (int)ceil(log2(b))) : 1.0;
+}
+
+__global__ __launch_bounds__(256) void det_convert_kernel(const long long *__restrict__ gxi,
+                                                          float *__restrict__ gx, long n,
+                                                          const double *__restrict__ scale) {
+  const double inv = 1.0 / *scale;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256)
+    gx[e] = (float)((double)gxi[e] * inv);
+}
+
+__global__ __launch_bounds__(256) void det_weight_reduce_kernel(const float *__restrict__ part,
+                                                                float *__restrict__ gw, long n,
+                                                                int nsplit) {
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int y = 0; y < nsplit; ++y) s += part[(long)y * n + e];
+    gw[e] += s;
+  }
+}
+
 __global__ void pack_weight_kernel(const float *__restrict__ w, float *__restrict__ wp, int Co,
                                    int Cg, int K) {
   const long total = (long)Co * Cg * K;
@@ -1402,12 +1476,52 @@ extern "C" int aanet_mdcn_sample_index(const float *offset, int *h_low, int *w_l
   return aanet_launch_status();
 }
 
-extern "C" int aanet_mdcn_bwd_f32(const float *x, const float *offset, const float *mask,
-                                  const float *weight, const float *grad_out, float *grad_x,
-                                  float *grad_offset, float *grad_mask, float *grad_weight,
-                                  float *grad_bias, int n, int c, int h, int w, int co, int kh,
-                                  int kw, int stride, int pad, int dil, int groups, int dg,
-                                  aanet_stream_t stream) {
+namespace {
+
+struct BwdPlan {
+  int npieces, nchunks, nsplit;
+  long range;
+};
+
+BwdPlan bwd_plan(const MdcnArgs &a) {
+  BwdPlan pl;
+  const long P = (long)a.Ho * a.Wo, T = (long)a.N * P;
+  const int K = a.kh * a.kw, cpg = a.C / a.dg;
+  pl.npieces = host_div_up(cpg, KC);
+  pl.nchunks = K * a.dg * pl.npieces;
+  // ~2048 workgroups in total; each covers `range` flattened pixels
+  long nsplit = 2048 / pl.nchunks;
+  if (nsplit < 1) nsplit = 1;
+  long range = (T + nsplit - 1) / nsplit;
+  range = ((range + PT - 1) / PT) * PT;
+  pl.nsplit = (int)((T + range - 1) / range);
+  pl.range = range;
+  return pl;
+}
+
+// Deterministic-backward workspace: [grad_x as int64][weight partials][bounds, scale]
+struct DetLayout {
+  size_t gxi, part, bounds, scale, total;
+};
+
+DetLayout det_layout(const MdcnArgs &a, const BwdPlan &pl) {
+  auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+  DetLayout L;
+  const size_t nx = (size_t)a.N * a.C * a.H * a.W;
+  const size_t nw = (size_t)a.Co * a.C * a.kh * a.kw;
+  L.gxi = 0;
+  L.part = up(L.gxi + nx * 8);
+  L.bounds = up(L.part + (size_t)pl.nsplit * nw * 4);
+  L.scale = L.bounds + 16;
+  L.total = up(L.scale + 8);
+  return L;
+}
+
+int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const float *weight,
+                  const float *grad_out, float *grad_x, float *grad_offset, float *grad_mask,
+                  float *grad_weight, float *grad_bias, int n, int c, int h, int w, int co,
+                  int kh, int kw, int stride, int pad, int dil, int groups, int dg, int det,
+                  void *ws, size_t ws_bytes, hipStream_t st) {
   MdcnArgs a = make_args(x, offset, -1, mask, -1, 0, 1.f, weight, nullptr, nullptr, nullptr, 0,
                          nullptr, n, c, h, w, co, kh, kw, stride, pad, dil, groups, dg);
   int rc = check_shapes(a);
@@ -1417,34 +1531,106 @@ extern "C" int aanet_mdcn_bwd_f32(const float *x, const float *offset, const flo
     return AANET_EINVAL;
   if (groups != 1) return AANET_EUNSUPPORTED;  // AANet uses groups=1 (nets/deform.py:25)
   if (co % 4 || co > 256) return AANET_EUNSUPPORTED;
-  hipStream_t st = as_hip(stream);
   const long P = (long)a.Ho * a.Wo;
-  const int K = kh * kw, cpg = c / dg;
-  hipError_t e = hipMemsetAsync(grad_x, 0, sizeof(float) * (size_t)n * c * h * w, st);
-  if (e != hipSuccess) return (int)e;
+  const int K = kh * kw;
+  const BwdPlan pl = bwd_plan(a);
+  DetLayout L{};
+  char *wb = static_cast<char *>(ws);
+  if (det) {
+    L = det_layout(a, pl);
+    if (!ws || ws_bytes < L.total) return AANET_EINVAL;
+  }
+  long long *gxi = det ? reinterpret_cast<long long *>(wb + L.gxi) : nullptr;
+  float *part = det ? reinterpret_cast<float *>(wb + L.part) : nullptr;
+  unsigned *bounds = det ? reinterpret_cast<unsigned *>(wb + L.bounds) : nullptr;
+  double *scale = det ? reinterpret_cast<double *>(wb + L.scale) : nullptr;
+  const size_t nx = (size_t)n * c * h * w;
+  hipError_t e;
+  if (det) {
+    e = hipMemsetAsync(gxi, 0, nx * 8, st);
+    if (e == hipSuccess) e = hipMemsetAsync(bounds, 0, 16, st);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(det_wbound_kernel, dim3(host_div_up((long)c * K, 256)), dim3(256), 0, st,
+                       weight, co, c * K, bounds);
+    const long ng = (long)n * co * P, nm = (long)n * dg * K * P;
+    hipLaunchKernelGGL(det_absmax_kernel, dim3(host_div_up(ng, 256) > 2048 ? 2048 : host_div_up(ng, 256)),
+                       dim3(256), 0, st, grad_out, ng, bounds + 1);
+    hipLaunchKernelGGL(det_absmax_kernel, dim3(host_div_up(nm, 256) > 2048 ? 2048 : host_div_up(nm, 256)),
+                       dim3(256), 0, st, mask, nm, bounds + 2);
+    hipLaunchKernelGGL(det_scale_kernel, dim3(1), dim3(1), 0, st, bounds, scale);
+  } else {
+    e = hipMemsetAsync(grad_x, 0, sizeof(float) * nx, st);
+    if (e != hipSuccess) return (int)e;
+  }
   const int GP = round_pitch(PT, 16), WTP = round_pitch(co, 2);
   const size_t smem = sizeof(float) * ((size_t)co * GP + (size_t)KC * WTP + (size_t)KC * CP + 3 * 4 * 64);
   if (smem > 64 * 1024) return AANET_EUNSUPPORTED;
-  hipLaunchKernelGGL(mdcn_bwd_data_kernel, dim3((unsigned)(n * host_div_up(P, PT)), (unsigned)dg),
-                     dim3(NT), smem, st, a, grad_out, grad_x, grad_offset, grad_mask, GP, WTP);
+  const dim3 gdata((unsigned)(n * host_div_up(P, PT)), (unsigned)dg);
+  if (det)
+    hipLaunchKernelGGL(mdcn_bwd_data_kernel<1>, gdata, dim3(NT), smem, st, a, grad_out, grad_x,
+                       grad_offset, grad_mask, GP, WTP, gxi, scale);
+  else
+    hipLaunchKernelGGL(mdcn_bwd_data_kernel<0>, gdata, dim3(NT), smem, st, a, grad_out, grad_x,
+                       grad_offset, grad_mask, GP, WTP, nullptr, nullptr);
   rc = aanet_launch_status();
   if (rc) return rc;
-  const int npieces = host_div_up(cpg, KC);
-  const long T = (long)n * P;
-  const int nchunks = K * dg * npieces;
-  // ~2048 workgroups in total; each covers `range` flattened pixels
-  long nsplit = 2048 / nchunks;
-  if (nsplit < 1) nsplit = 1;
-  long range = (T + nsplit - 1) / nsplit;
-  range = ((range + PT - 1) / PT) * PT;
-  nsplit = (T + range - 1) / range;
-  hipLaunchKernelGGL(mdcn_bwd_weight_kernel, dim3(nchunks, (unsigned)nsplit, host_div_up(co, 64)),
-                     dim3(NT), 0, st, a, grad_out, grad_weight, npieces, range);
+  if (det) {
+    hipLaunchKernelGGL(det_convert_kernel, dim3(host_div_up((long)nx, 256) > 8192 ? 8192 : host_div_up((long)nx, 256)),
+                       dim3(256), 0, st, gxi, grad_x, (long)nx, scale);
+  }
+  const dim3 gw3(pl.nchunks, (unsigned)pl.nsplit, host_div_up(co, 64));
+  if (det)
+    hipLaunchKernelGGL(mdcn_bwd_weight_kernel<1>, gw3, dim3(NT), 0, st, a, grad_out, grad_weight,
+                       pl.npieces, pl.range, part);
+  else
+    hipLaunchKernelGGL(mdcn_bwd_weight_kernel<0>, gw3, dim3(NT), 0, st, a, grad_out, grad_weight,
+                       pl.npieces, pl.range, nullptr);
   rc = aanet_launch_status();
   if (rc) return rc;
+  if (det) {
+    const long nw = (long)co * c * K;
+    hipLaunchKernelGGL(det_weight_reduce_kernel, dim3(host_div_up(nw, 256)), dim3(256), 0, st,
+                       part, grad_weight, nw, pl.nsplit);
+    rc = aanet_launch_status();
+    if (rc) return rc;
+  }
   if (grad_bias) {
     hipLaunchKernelGGL(bias_grad_kernel, dim3(co), dim3(256), 0, st, grad_out, grad_bias, n, co, P);
     rc = aanet_launch_status();
   }
   return rc;
+}
+
+}  // namespace
+
+extern "C" int aanet_mdcn_bwd_f32(const float *x, const float *offset, const float *mask,
+                                  const float *weight, const float *grad_out, float *grad_x,
+                                  float *grad_offset, float *grad_mask, float *grad_weight,
+                                  float *grad_bias, int n, int c, int h, int w, int co, int kh,
+                                  int kw, int stride, int pad, int dil, int groups, int dg,
+                                  aanet_stream_t stream) {
+  return mdcn_bwd_impl(x, offset, mask, weight, grad_out, grad_x, grad_offset, grad_mask,
+                       grad_weight, grad_bias, n, c, h, w, co, kh, kw, stride, pad, dil, groups,
+                       dg, 0, nullptr, 0, as_hip(stream));
+}
+
+extern "C" size_t aanet_mdcn_bwd_det_workspace_size(int n, int c, int h, int w, int co, int kh,
+                                                    int kw, int stride, int pad, int dil,
+                                                    int groups, int dg) {
+  MdcnArgs a = make_args(nullptr, nullptr, -1, nullptr, -1, 0, 1.f, nullptr, nullptr, nullptr,
+                         nullptr, 0, nullptr, n, c, h, w, co, kh, kw, stride, pad, dil, groups, dg);
+  if (check_shapes(a)) return 0;
+  return det_layout(a, bwd_plan(a)).total;
+}
+
+extern "C" int aanet_mdcn_bwd_det_f32(const float *x, const float *offset, const float *mask,
+                                      const float *weight, const float *grad_out, float *grad_x,
+                                      float *grad_offset, float *grad_mask, float *grad_weight,
+                                      float *grad_bias, int n, int c, int h, int w, int co,
+                                      int kh, int kw, int stride, int pad, int dil, int groups,
+                                      int dg, void *workspace, size_t workspace_bytes,
+                                      aanet_stream_t stream) {
+  return mdcn_bwd_impl(x, offset, mask, weight, grad_out, grad_x, grad_offset, grad_mask,
+                       grad_weight, grad_bias, n, c, h, w, co, kh, kw, stride, pad, dil, groups,
+                       dg, 1, workspace, workspace_bytes, as_hip(stream));
 }

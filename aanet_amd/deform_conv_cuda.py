@@ -12,6 +12,8 @@ Only stride_h == stride_w, pad_h == pad_w, dilation_h == dilation_w are supporte
 form deform_conv.py ever passes, :143-147).  The DCNv1 entry points (deform_conv_forward_cuda,
 deform_conv_backward_*) are dead code for AANet and raise.
 """
+import torch
+
 from . import ops
 from ._lib import call, ptr, require_gpu, stream_of
 
@@ -55,6 +57,17 @@ def modulated_deform_conv_cuda_backward(input, weight, bias, ones, offset, mask,
                 names=("input", "weight", "offset", "mask", "grad_input", "grad_weight",
                        "grad_offset", "grad_mask"))
     go = grad_output.contiguous()
+    if torch.are_deterministic_algorithms_enabled():
+        # bit-reproducible form (aanet_mdcn_bwd_det_f32); same in-place / accumulate contract
+        gx, goff, gm, gw, gb = ops.mdcn_backward(input, offset, mask, weight, go, with_bias, s, p,
+                                                 d, group, deformable_group, deterministic=True)
+        grad_input.copy_(gx)
+        grad_offset.copy_(goff)
+        grad_mask.copy_(gm)
+        grad_weight.add_(gw)
+        if with_bias:
+            grad_bias.add_(gb)
+        return
     N, C, H, W = input.shape
     Co = weight.shape[0]
     call("aanet_mdcn_bwd_f32", ptr(input), ptr(offset), ptr(mask), ptr(weight), ptr(go),

@@ -286,8 +286,12 @@ def csa_sum(inputs, act="leaky"):
 
 
 def mdcn_backward(x, offset, mask, weight, grad_out, with_bias, stride, padding, dilation, groups,
-                  deformable_groups):
-    """deform_conv_cuda.cpp:571-685 -> (gX, gOffset, gMask, gW, gB or None)."""
+                  deformable_groups, deterministic=None):
+    """deform_conv_cuda.cpp:571-685 -> (gX, gOffset, gMask, gW, gB or None).
+
+    deterministic (default: torch.are_deterministic_algorithms_enabled()): the bit-reproducible
+    form (aanet_mdcn_bwd_det_f32: fixed-point grad_x accumulation, ordered grad_W reduction)
+    instead of float atomics."""
     require_gpu(x, offset, mask, weight, grad_out,
                 names=("input", "offset", "mask", "weight", "grad_output"))
     N, C, H, W = x.shape
@@ -295,6 +299,19 @@ def mdcn_backward(x, offset, mask, weight, grad_out, with_bias, stride, padding,
     gx, goff, gm = torch.empty_like(x), torch.empty_like(offset), torch.empty_like(mask)
     gw = torch.zeros_like(weight)
     gb = x.new_zeros((Co,)) if with_bias else None
+    if deterministic is None:
+        deterministic = torch.are_deterministic_algorithms_enabled()
+    if deterministic:
+        nbytes = _lib.lib().aanet_mdcn_bwd_det_workspace_size(N, C, H, W, Co, kh, kw, stride,
+                                                               padding, dilation, groups,
+                                                               deformable_groups)
+        if nbytes == 0:
+            raise ValueError("aanet_mdcn_bwd_det_workspace_size: invalid shape")
+        ws = torch.empty((nbytes,), device=x.device, dtype=torch.uint8)
+        call("aanet_mdcn_bwd_det_f32", ptr(x), ptr(offset), ptr(mask), ptr(weight), ptr(grad_out),
+             ptr(gx), ptr(goff), ptr(gm), ptr(gw), ptr(gb), N, C, H, W, Co, kh, kw, stride,
+             padding, dilation, groups, deformable_groups, ptr(ws), nbytes, stream_of(x))
+        return gx, goff, gm, gw, gb
     call("aanet_mdcn_bwd_f32", ptr(x), ptr(offset), ptr(mask), ptr(weight), ptr(grad_out), ptr(gx),
          ptr(goff), ptr(gm), ptr(gw), ptr(gb), N, C, H, W, Co, kh, kw, stride, padding, dilation,
          groups, deformable_groups, stream_of(x))

@@ -1,0 +1,127 @@
+"""Training step of the hot path with data-parallel gradient all-reduce.
+
+What the reference's training loop does around the path, restated on the drop-in modules:
+
+* loss -- model.py:97-134: every disparity in the pyramid is bilinearly upsampled to the
+  ground-truth size (align_corners=False) and scaled by W_gt / W_pred, then
+  smooth-L1 over the valid mask (mean), weighted by the pyramid weights of model.py:98-107;
+  the optional pseudo-ground-truth term (model.py:126-134) is added the same way;
+* parameter groups -- train.py:199-215 with utils/utils.py:156-169: `offset_conv.weight` /
+  `offset_conv.bias` train at 0.1x the base learning rate (Adam);
+* data parallelism -- train.py:184-190: SyncBatchNorm conversion, then DistributedDataParallel;
+  micro-steps that are not on an accumulation boundary run under `no_sync()` (model.py:82-85),
+  the loss is divided by the accumulation count (model.py:136) and the optimizer steps on
+  boundaries (model.py:151-153).
+
+MI355X specifics: one process per GPU over RCCL (torch.distributed backend "nccl").  The
+gradient of the path is ~16 MB (AANet) -- one or two buckets: the bucket cap is raised to 32 MB
+so the all-reduce is a single large ring over xGMI instead of the default 25 MB split, and
+gradients are bucket views (no extra copy).  The DCN backward is the HIP one; with
+torch.use_deterministic_algorithms(True) it is the bit-reproducible form
+(aanet_mdcn_bwd_det_f32) -- the HIP cost-volume and regression backwards are gathers and are
+reproducible either way; the loss's bilinear upsampling backward is torch's and follows torch's
+own deterministic-algorithms rules.
+"""
+import contextlib
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+# model.py:98-107: pyramid weights by pyramid length
+PYRAMID_WEIGHTS = {5: [1 / 3, 2 / 3, 1.0, 1.0, 1.0],  # AANet and AANet+
+                   4: [1 / 3, 2 / 3, 1.0, 1.0],
+                   3: [1.0, 1.0, 1.0],
+                   1: [1.0]}
+
+SPECIFIC_PARAMS = ("offset_conv.weight", "offset_conv.bias")  # utils/utils.py:156-169
+
+
+def pyramid_weights(n, highest_loss_only=False):
+    if highest_loss_only:
+        return [1.0]
+    if n not in PYRAMID_WEIGHTS:
+        raise NotImplementedError(f"no pyramid weights for {n} predictions")
+    return PYRAMID_WEIGHTS[n]
+
+
+def disparity_loss(pred_pyramid, gt_disp, mask, weights=None, pseudo_gt=None, pseudo_mask=None):
+    """model.py:109-134 -> (weighted total, per-scale losses).  pred_pyramid: coarse-to-fine
+    list of [B, h, w]; gt_disp, mask: [B, H, W] (mask bool); pseudo_gt / pseudo_mask the
+    optional pseudo ground truth (args.load_pseudo_gt)."""
+    if weights is None:
+        weights = pyramid_weights(len(pred_pyramid))
+    if len(weights) != len(pred_pyramid):
+        raise ValueError("one weight per prediction")
+    total, per_scale = 0.0, []
+    for pred, w in zip(pred_pyramid, weights):
+        if pred.size(-1) != gt_disp.size(-1):
+            pred = F.interpolate(pred.unsqueeze(1), size=gt_disp.shape[-2:], mode="bilinear",
+                                 align_corners=False) * (gt_disp.size(-1) / pred.size(-1))
+            pred = pred.squeeze(1)
+        loss = F.smooth_l1_loss(pred[mask], gt_disp[mask], reduction="mean")
+        total = total + w * loss
+        per_scale.append(loss)
+        if pseudo_gt is not None:
+            total = total + w * F.smooth_l1_loss(pred[pseudo_mask], pseudo_gt[pseudo_mask],
+                                                 reduction="mean")
+    return total, per_scale
+
+
+def param_groups(model, lr):
+    """Base parameters at lr, offset_conv at 0.1 * lr (train.py:199-215)."""
+    base, specific = [], []
+    for name, p in model.named_parameters():
+        (specific if any(s in name for s in SPECIFIC_PARAMS) else base).append(p)
+    return [{"params": base, "lr": lr}, {"params": specific, "lr": lr * 0.1}]
+
+
+def wrap_data_parallel(model, device, sync_bn=True, bucket_cap_mb=32):
+    """SyncBN + DDP (train.py:184-190) when torch.distributed is initialised with >1 rank;
+    otherwise the module itself."""
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return model
+    if sync_bn:
+        model = nn.SyncBatchNorm.convert_sync_batchnorm(model)
+    dev_ids = [device.index] if device.type == "cuda" and dist.get_backend() == "nccl" else None
+    return nn.parallel.DistributedDataParallel(model, device_ids=dev_ids,
+                                               bucket_cap_mb=bucket_cap_mb,
+                                               gradient_as_bucket_view=True)
+
+
+class Trainer:
+    """One optimizer step per `accumulation_steps` micro-batches (model.py:64-153)."""
+
+    def __init__(self, model, lr=1e-3, weight_decay=1e-4, accumulation_steps=1,
+                 highest_loss_only=False):
+        self.model = model
+        self.accumulation_steps = accumulation_steps
+        self.highest_loss_only = highest_loss_only
+        self.optimizer = torch.optim.Adam(param_groups(model, lr), weight_decay=weight_decay)
+        self.micro = 0
+
+    def step(self, left_feature, right_feature, gt_disp, mask=None, pseudo_gt=None,
+             pseudo_mask=None):
+        """Forward + backward of one micro-batch; returns the (unscaled) total loss.  The
+        optimizer steps (and DDP all-reduces) on accumulation boundaries only."""
+        self.model.train()
+        if mask is None:
+            mask = gt_disp > 0
+        self.micro += 1
+        boundary = self.micro % self.accumulation_steps == 0
+        sync_ctx = contextlib.nullcontext()
+        if not boundary and isinstance(self.model, nn.parallel.DistributedDataParallel):
+            sync_ctx = self.model.no_sync()
+        with sync_ctx:
+            pyramid = self.model(left_feature, right_feature)
+            if self.highest_loss_only:
+                pyramid = [pyramid[-1]]
+            total, _ = disparity_loss(pyramid, gt_disp, mask,
+                                      pyramid_weights(len(pyramid), self.highest_loss_only),
+                                      pseudo_gt, pseudo_mask)
+            (total / self.accumulation_steps).backward()
+        if boundary:
+            self.optimizer.step()
+            self.optimizer.zero_grad(set_to_none=True)
+        return total.detach()

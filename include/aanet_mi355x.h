@@ -185,6 +185,22 @@ int aanet_mdcn_bwd_f32(const float *x, const float *offset, const float *mask, c
                        int kh, int kw, int stride, int pad, int dil, int groups, int dg,
                        aanet_stream_t stream);
 
+/* Deterministic form of aanet_mdcn_bwd_f32 (same contract, bit-reproducible run to run):
+ *   - grad_x: 64-bit fixed-point atomics. Integer adds are associative, so the sum does not
+ *     depend on atomic ordering. The fixed-point scale is a power of two chosen on the device from
+ *     max_{c,k} sum_co |W| * max|grad_out| * max|mask|, so there is no host synchronisation.
+ *   - grad_weight: per-split partial sums reduced in a fixed order.
+ * `workspace` (device, caller-owned) must hold aanet_mdcn_bwd_det_workspace_size(...) bytes.
+ * The atomic col2im of the reference (kernel.cu:688) has no such guarantee. */
+size_t aanet_mdcn_bwd_det_workspace_size(int n, int c, int h, int w, int co, int kh, int kw,
+                                         int stride, int pad, int dil, int groups, int dg);
+int aanet_mdcn_bwd_det_f32(const float *x, const float *offset, const float *mask,
+                           const float *weight, const float *grad_out, float *grad_x,
+                           float *grad_offset, float *grad_mask, float *grad_weight,
+                           float *grad_bias, int n, int c, int h, int w, int co, int kh, int kw,
+                           int stride, int pad, int dil, int groups, int dg, void *workspace,
+                           size_t workspace_bytes, aanet_stream_t stream);
+
 /* Debug exports for bit-exact checks (SURVEY.md §8c pin 6):
  * im2col of ONE image, kernel.cu:570-633: col [c*kh*kw, ho*wo]. */
 int aanet_mdcn_im2col_f32(const float *x, const float *offset, const float *mask, float *col,

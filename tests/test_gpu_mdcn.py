@@ -125,15 +125,21 @@ BWD_CASES = [
 
 @pytest.mark.parametrize("case", BWD_CASES)
 @pytest.mark.parametrize("off_scale", [0.7, 2.0])
-def test_mdcn_backward_vs_oracle(case, off_scale):
+@pytest.mark.parametrize("deterministic", [False, True])
+def test_mdcn_backward_vs_oracle(case, off_scale, deterministic):
     N, C, H, W, Co, k, s, p, d, dg = case
     x, off, msk, w, b = make_case(5, N, C, H, W, Co, k, s, p, d, dg, off_scale=off_scale)
     Ho, Wo = off.shape[2:]
     go = np.random.default_rng(6).standard_normal((N, Co, Ho, Wo)).astype(np.float32)
     xt, ot, mt = g2t(x).requires_grad_(), g2t(off).requires_grad_(), g2t(msk).requires_grad_()
     wt, bt = g2t(w).requires_grad_(), g2t(b).requires_grad_()
-    out = ops.modulated_deform_conv(xt, ot, mt, wt, bt, s, p, d, 1, dg)
-    out.backward(g2t(go))
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(deterministic)
+    try:
+        out = ops.modulated_deform_conv(xt, ot, mt, wt, bt, s, p, d, 1, dg)
+        out.backward(g2t(go))
+    finally:
+        torch.use_deterministic_algorithms(prev)
     gx, goff, gm, gw, gb = oracle.mdcn_backward(x, off, msk, w, go, True, s, p, d, 1, dg)
     for name, got, ref in (("grad_input", xt.grad, gx), ("grad_offset", ot.grad, goff),
                            ("grad_mask", mt.grad, gm), ("grad_weight", wt.grad, gw),
@@ -215,3 +221,48 @@ def test_torch_ops_match_functional_ops_and_autograd():
     gb = torch.autograd.grad(d2, (L, R), gd)
     for a, c in zip(ga, gb):
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("case", [(2, 64, 16, 52, 64, 3, 1, 2, 2, 2), (1, 32, 9, 26, 32, 3, 2, 1, 1, 2)])
+def test_mdcn_backward_deterministic_is_bit_reproducible(case):
+    """aanet_mdcn_bwd_det_f32: identical bits on every run (the atomic form need not be)."""
+    N, C, H, W, Co, k, s, p, d, dg = case
+    x, off, msk, w, b = make_case(9, N, C, H, W, Co, k, s, p, d, dg, off_scale=2.0)
+    Ho, Wo = off.shape[2:]
+    go = g2t(np.random.default_rng(3).standard_normal((N, Co, Ho, Wo)).astype(np.float32))
+    args = (g2t(x), g2t(off), g2t(msk), g2t(w), go, True, s, p, d, 1, dg)
+    runs = [ops.mdcn_backward(*args, deterministic=True) for _ in range(3)]
+    for r in runs[1:]:
+        for a_, b_ in zip(runs[0], r):
+            assert torch.equal(a_, b_)
+    atomic = ops.mdcn_backward(*args, deterministic=False)
+    for a_, b_ in zip(runs[0], atomic):
+        scale = b_.abs().max().item() + 1e-12
+        assert (a_ - b_).abs().max().item() <= 1e-5 * scale
+
+
+def test_deterministic_mode_reaches_shim_and_torch_ops():
+    """torch.use_deterministic_algorithms(True) selects the deterministic kernels in every entry
+    point: the autograd Function, torch.ops.aanet.mdcn_backward and the deform_conv_cuda shim."""
+    import aanet_amd  # noqa: F401
+    from aanet_amd import deform_conv_cuda
+    x, off, msk, w, b = make_case(4, 2, 32, 9, 26, 32, off_scale=1.5)
+    xt, ot, mt, wt, bt = (g2t(a) for a in (x, off, msk, w, b))
+    go = g2t(np.random.default_rng(2).standard_normal((2, 32, 9, 26)).astype(np.float32))
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True)
+    try:
+        ref = ops.mdcn_backward(xt, ot, mt, wt, go, True, 1, 2, 2, 1, 2, deterministic=True)
+        got = torch.ops.aanet.mdcn_backward(xt, ot, mt, wt, go, True, 1, 2, 2, 1, 2)
+        for a_, b_ in zip(ref, got):
+            assert torch.equal(a_, b_)
+        gi, goff, gm = torch.zeros_like(xt), torch.zeros_like(ot), torch.zeros_like(mt)
+        gw, gb = torch.zeros_like(wt), torch.zeros_like(bt)
+        e = xt.new_empty(0)
+        deform_conv_cuda.modulated_deform_conv_cuda_backward(xt, wt, bt, e, ot, mt, e, gi, gw, gb,
+                                                             goff, gm, go, 3, 3, 1, 1, 2, 2, 2, 2,
+                                                             1, 2, True)
+        for a_, b_ in zip(ref, (gi, goff, gm, gw, gb)):
+            assert torch.equal(a_, b_)
+    finally:
+        torch.use_deterministic_algorithms(prev)

@@ -1,0 +1,136 @@
+"""GPU tests of the training step on the drop-in path: the Trainer over
+AANetHotPath (HIP forward + backward kernels, Adam with the offset_conv 0.1x group), and
+data parallelism with SyncBatchNorm -- two ranks sharing cuda:0 over gloo (one GPU on the test
+box; the production backend is nccl=RCCL, one process per GPU) against one process on the full
+batch with plain BatchNorm."""
+import copy
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from aanet_amd import nets, train
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _inputs(B, seed):
+    g = torch.Generator().manual_seed(seed)
+    sizes = [(24, 48), (12, 24), (6, 12)]
+    left = [torch.randn(B, 16, h, w, generator=g).to(DEV) for h, w in sizes]
+    right = [torch.randn(B, 16, h, w, generator=g).to(DEV) for h, w in sizes]
+    gt = (torch.rand(B, 48, 96, generator=g) * 12 + 1).to(DEV)   # 2x the scale-0 resolution
+    return left, right, gt
+
+
+def _model(seed=0):
+    torch.manual_seed(seed)
+    return nets.AANetHotPath(16, no_intermediate_supervision=False, num_deform_blocks=3).to(DEV)
+
+
+def test_trainer_steps_hot_path():
+    m = _model()
+    t = train.Trainer(m, lr=1e-3)
+    off0 = {n: p.detach().clone() for n, p in m.named_parameters() if "offset_conv" in n}
+    base0 = {n: p.detach().clone() for n, p in m.named_parameters() if "offset_conv" not in n}
+    assert off0 and base0
+    l, r, gt = _inputs(2, 0)
+    losses = [float(t.step(l, r, gt)) for _ in range(4)]
+    assert all(torch.isfinite(torch.tensor(losses)))
+    assert losses[-1] < losses[0], losses
+    # both groups moved; Adam's first step moves each weight by ~lr, so the offset group (0.1 lr)
+    # moves about a tenth as far
+    named = {n: p.detach() for n, p in m.named_parameters()}
+    d_off = max(float((named[n] - p).abs().max()) for n, p in off0.items())
+    d_base = max(float((named[n] - p).abs().max()) for n, p in base0.items())
+    assert 0 < d_off < 0.5 * d_base, (d_off, d_base)
+
+
+def test_deterministic_training_step_is_bit_reproducible():
+    """Same seed and data, deterministic algorithms on: every gradient of the path is
+    bit-identical across two runs (the DCN weight/input gradients come from the fixed-point
+    aanet_mdcn_bwd_det_f32).  The loss is taken on the pyramid directly -- torch's bilinear
+    upsample backward (the loss's resizing) has no deterministic CUDA kernel."""
+    grads = []
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True)
+    try:
+        for _ in range(2):
+            m = _model(5).train()
+            l, r, _ = _inputs(2, 1)
+            loss = sum((d * (i + 1)).mean() for i, d in enumerate(m(l, r)))
+            loss.backward()
+            grads.append({n: p.grad.clone() for n, p in m.named_parameters()
+                          if p.grad is not None})
+    finally:
+        torch.use_deterministic_algorithms(prev)
+    a, b = grads
+    assert a.keys() == b.keys() and len(a) > 100
+    diff = [n for n in a if not torch.equal(a[n], b[n])]
+    assert not diff, diff[:20]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _ddp_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        m = _model(11)
+        ref = copy.deepcopy(m)
+        ddp = train.wrap_data_parallel(m, torch.device(DEV), sync_bn=True)
+        assert isinstance(ddp, torch.nn.parallel.DistributedDataParallel)
+        assert any(isinstance(x, torch.nn.SyncBatchNorm) for x in ddp.modules())
+        l, r, gt = _inputs(2 * world, 3)
+        sl = slice(2 * rank, 2 * rank + 2)
+        ddp.train()
+        tot, _ = train.disparity_loss(ddp([x[sl] for x in l], [x[sl] for x in r]), gt[sl],
+                                      gt[sl] > 0)
+        tot.backward()
+        # reference: one process, full batch, plain BatchNorm (batch statistics over all ranks)
+        ref.train()
+        rtot, _ = train.disparity_loss(ref(l, r), gt, gt > 0)
+        rtot.backward()
+        got = torch.cat([p.grad.flatten() for p in m.parameters() if p.grad is not None])
+        want = torch.cat([p.grad.flatten() for p in ref.parameters() if p.grad is not None])
+        cos = float(got @ want / (got.norm() * want.norm()))
+        rel = float((got - want).norm() / want.norm())
+        sums = [torch.zeros(1) for _ in range(world)]
+        dist.all_gather(sums, torch.tensor([float(got.double().sum())]))
+        if rank == 0:
+            q.put(("ok", cos, rel, [float(s) for s in sums]))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent on q.get
+        q.put(("error", repr(e), 0.0, []))
+        raise
+
+
+def test_ddp_syncbn_two_ranks_match_full_batch():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        status, cos, rel, sums = q.get(timeout=300)
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+            if p.is_alive():
+                p.kill()
+    assert status == "ok", cos
+    for p in procs:
+        assert p.exitcode == 0
+    assert sums[0] == sums[1]                 # all-reduced gradients identical on both ranks
+    assert cos > 0.9999 and rel < 1e-2, (cos, rel)
