@@ -11,6 +11,7 @@ into the 1x1/3x3 convs, and the deformable conv2 -> bn2 -> ReLU done by ONE kern
 the offset_conv output in place (offset slice + 2*sigmoid(mask logits)) and applies BN+ReLU
 in its epilogue.
 """
+import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
@@ -60,9 +61,22 @@ class DeformConv2d(nn.Module):
         nn.init.constant_(self.offset_conv.weight, 0.)
         nn.init.constant_(self.offset_conv.bias, 0.)
 
+    def _offset_conv(self, x):
+        """offset_conv (groups = deformable_groups, dilated).  MIOpen has no dilated grouped
+        convolution, so torch would fall back to a per-image im2col loop (the largest cost of a
+        training step); on the GPU each deformable group runs as its own ungrouped conv."""
+        oc = self.offset_conv
+        g = oc.groups
+        if g == 1 or not x.is_cuda or oc.dilation == (1, 1):
+            return oc(x)
+        cin, cout = x.shape[1] // g, oc.out_channels // g
+        return torch.cat([F.conv2d(x[:, i * cin:(i + 1) * cin], oc.weight[i * cout:(i + 1) * cout],
+                                   oc.bias[i * cout:(i + 1) * cout], oc.stride, oc.padding,
+                                   oc.dilation) for i in range(g)], 1)
+
     def forward(self, x):
         if self.modulation:
-            offset_mask = self.offset_conv(x)
+            offset_mask = self._offset_conv(x)
             offset_channel = self.deformable_groups * 2 * self.kernel_size * self.kernel_size
             offset = offset_mask[:, :offset_channel, :, :]
             mask = offset_mask[:, offset_channel:, :, :]
@@ -70,7 +84,7 @@ class DeformConv2d(nn.Module):
             if self.double_mask:
                 mask = mask * 2
             return self.deform_conv(x, offset, mask)
-        offset = self.offset_conv(x)
+        offset = self._offset_conv(x)
         return self.deform_conv(x, offset)
 
     def forward_fused(self, x, bn=None, act=None):

@@ -54,18 +54,29 @@ def disparity_loss(pred_pyramid, gt_disp, mask, weights=None, pseudo_gt=None, ps
         weights = pyramid_weights(len(pred_pyramid))
     if len(weights) != len(pred_pyramid):
         raise ValueError("one weight per prediction")
+    # mean over the mask as a masked sum / count: the same value as smooth_l1(pred[mask], ...)
+    # (model.py:121) without the boolean gather, whose nonzero() syncs the host every scale
+    # (masked-out ground truth may be inf/nan in real data: zero it so 0 * term stays 0)
+    maskf = mask.to(gt_disp.dtype)
+    count = maskf.sum()
+    gt_disp = torch.where(mask, gt_disp, torch.zeros_like(gt_disp))
+    pmaskf = pcount = None
+    if pseudo_gt is not None:
+        pmaskf = pseudo_mask.to(gt_disp.dtype)
+        pcount = pmaskf.sum()
+        pseudo_gt = torch.where(pseudo_mask, pseudo_gt, torch.zeros_like(pseudo_gt))
     total, per_scale = 0.0, []
     for pred, w in zip(pred_pyramid, weights):
         if pred.size(-1) != gt_disp.size(-1):
             pred = F.interpolate(pred.unsqueeze(1), size=gt_disp.shape[-2:], mode="bilinear",
                                  align_corners=False) * (gt_disp.size(-1) / pred.size(-1))
             pred = pred.squeeze(1)
-        loss = F.smooth_l1_loss(pred[mask], gt_disp[mask], reduction="mean")
+        loss = (F.smooth_l1_loss(pred, gt_disp, reduction="none") * maskf).sum() / count
         total = total + w * loss
         per_scale.append(loss)
         if pseudo_gt is not None:
-            total = total + w * F.smooth_l1_loss(pred[pseudo_mask], pseudo_gt[pseudo_mask],
-                                                 reduction="mean")
+            ploss = (F.smooth_l1_loss(pred, pseudo_gt, reduction="none") * pmaskf).sum() / pcount
+            total = total + w * ploss
     return total, per_scale
 
 

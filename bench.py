@@ -46,16 +46,22 @@ def parse():
     ap.add_argument("--kernel-iters", type=int, default=20)
     ap.add_argument("--features", default="randn", choices=sorted(FEATURE_KINDS),
                     help="synthetic feature variant (SURVEY.md §8d)")
+    ap.add_argument("--train", action="store_true",
+                    help="time the training step (fwd+bwd+Adam, SyncBN+DDP for N>1) instead")
+    ap.add_argument("--train-batch", type=int, default=4, help="training pairs per GPU")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="--train with torch.use_deterministic_algorithms (det DCN backward)")
     ap.add_argument("--only", default=None,
                     help="profiling mode: run only one kernel family (corr|mdcn|regress|step)")
     return ap.parse_args()
 
 
-def build_model(device):
+def build_model(device, intermediate_supervision=False):
     from aanet_amd.nets import AANetHotPath
     torch.manual_seed(0)  # identical weights on every rank
     m = AANetHotPath(MAXD, feature_similarity="correlation", num_scales=3, num_fusions=6,
-                     deformable_groups=2, mdconv_dilation=2, no_intermediate_supervision=True,
+                     deformable_groups=2, mdconv_dilation=2,
+                     no_intermediate_supervision=not intermediate_supervision,
                      num_stage_blocks=1, num_deform_blocks=3)
     g = torch.Generator().manual_seed(1)
     with torch.no_grad():
@@ -77,10 +83,10 @@ FEATURE_KINDS = {
 }
 
 
-def make_features(batch, rank, device, kind="randn"):
+def make_features(batch, rank, device, kind="randn", img=(H_IMG, W_IMG)):
     """SURVEY.md §8(d) primary timed unit: seeded (1234 + rank) on-device feature pyramids."""
     gen = torch.Generator(device=device).manual_seed(1234 + rank)
-    shapes = [(batch, FEAT_C, (H_IMG // 3) >> s, (W_IMG // 3) >> s) for s in range(3)]
+    shapes = [(batch, FEAT_C, (img[0] // 3) >> s, (img[1] // 3) >> s) for s in range(3)]
     if kind in ("randn", "relu"):
         left = [torch.randn(s, device=device, generator=gen) for s in shapes]
         right = [torch.randn(s, device=device, generator=gen) for s in shapes]
@@ -191,6 +197,9 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
 
+    if args.train:
+        train_main(args, device, rank, world)
+        return
     model = build_model(device)
     left, right = make_features(args.batch, rank, device, args.features)
 
@@ -284,6 +293,64 @@ def main():
             line["epe_vs_ref"] = epe
             line["max_abs_disp_err_vs_ref"] = mx
         print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+TRAIN_IMG = (288, 576)   # scripts/aanet_train.sh (Scene Flow): --img_height 288 --img_width 576
+TRAIN_METRIC = "training stereo-pairs/s @288x576 D=64 fp32 (hot path fwd+bwd+Adam)"
+
+
+def train_main(args, device, rank, world):
+    """--train: the training step of the path (aanet_amd/train.py) -- forward in train mode
+    (batch-statistics BN, intermediate supervision: 3 disparities), pyramid smooth-L1 against a
+    full-resolution synthetic ground truth, HIP backward kernels, Adam with the offset_conv
+    0.1x group; SyncBN + DDP over RCCL when N>1 (the gradient all-reduce is the one data-path
+    collective).  Secondary line: not the headline metric."""
+    from aanet_amd import train as atrain
+    if args.deterministic:
+        torch.use_deterministic_algorithms(True, warn_only=True)  # torch's upsample bwd: warn
+    model = build_model(device, intermediate_supervision=True).train()
+    model = atrain.wrap_data_parallel(model, device)
+    trainer = atrain.Trainer(model, lr=1e-3)
+    left, right = make_features(args.train_batch, rank, device, args.features, TRAIN_IMG)
+    gen = torch.Generator(device=device).manual_seed(99 + rank)
+    gt = torch.rand((args.train_batch,) + TRAIN_IMG, device=device, generator=gen) * (MAXD_IMG - 1)
+    mask = (gt > 0) & (gt < MAXD_IMG)
+    for _ in range(args.warmup):
+        loss = trainer.step(left, right, gt, mask)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = trainer.step(left, right, gt, mask)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    from aanet_amd import dist as adist
+    rec = adist.make_record(device, pairs=args.train_batch * args.steps, elapsed_s=elapsed)
+    summary = adist.summarize(adist.gather_records(rec))
+    if rank == 0:
+        print(json.dumps({
+            "metric": TRAIN_METRIC,
+            "value": summary["pairs"] / summary["elapsed_max_s"],
+            "unit": "stereo-pairs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1000.0 * summary["elapsed_max_s"] / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (N(0,1) feature pyramids, uniform ground truth; random-init "
+                    "weights)",
+            "config": {"workload": "Scene Flow training crop 288x576: features 128ch at "
+                                   "1/3,1/6,1/12, D=64/32/16, AdaptiveAggregation train mode "
+                                   "with intermediate supervision, pyramid smooth-L1, Adam",
+                       "batch_per_gpu": args.train_batch,
+                       "global_batch": args.train_batch * world,
+                       "parallelism": f"dp{world} (SyncBN + DDP all-reduce)" if world > 1
+                       else "dp1", "deterministic": bool(args.deterministic)},
+            "final_loss": float(loss)}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

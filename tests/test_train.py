@@ -68,6 +68,14 @@ def test_disparity_loss_upsamples_and_scales():
     assert len(per) == 2
     with pytest.raises(ValueError):
         train.disparity_loss([p0, p1], gt, mask, [1.0])
+    # non-finite ground truth outside the mask does not leak into the loss or its gradient
+    gt_bad = torch.where(mask, gt, torch.full_like(gt, float("inf")))
+    gt_bad[0, 0, 0] = float("nan") if not mask[0, 0, 0] else gt_bad[0, 0, 0]
+    p1g = p1.clone().requires_grad_()
+    bad, _ = train.disparity_loss([p1g], gt_bad, mask, [1.0])
+    bad.backward()
+    assert torch.allclose(bad, F.smooth_l1_loss(p1[mask], gt[mask]))
+    assert torch.isfinite(p1g.grad).all()
     # pseudo ground truth adds a second weighted term over its own mask
     got2, _ = train.disparity_loss([p1], gt, mask, [1.0], pseudo_gt=gt * 0, pseudo_mask=mask)
     assert torch.allclose(got2, F.smooth_l1_loss(p1[mask], gt[mask])
