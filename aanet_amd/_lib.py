@@ -28,6 +28,8 @@ _SIGNATURES = {
     "aanet_corr_pyramid_f32": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _P],
     "aanet_disp_regress_f32": [_P, _P, _I, _I, _I, _I, _I, _P],
     "aanet_disp_regress_bwd_f32": [_P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "aanet_disp_warp_f32": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
+    "aanet_disp_warp_bwd_f32": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P],
     "aanet_mdcn_fwd_f32": [_P, _P, _P, _P, _P, _P] + [_I] * 12 + [_P],
     "aanet_mdcn_fwd_fused_f32": [_P, _P, _L, _P, _L, _I, _F, _P, _I, _P, _P, _P, _I, _P] + [_I] * 13 + [_P],
     "aanet_mdcn_bwd_f32": [_P] * 10 + [_I] * 12 + [_P],
@@ -80,7 +82,8 @@ def call(name, *args):
     rc = getattr(lib(), name)(*args)
     if rc != 0:
         msg = lib().aanet_status_string(rc).decode()
-        raise AanetError(f"{name} failed: {msg} (status {rc})")
+        ints = [a for a in args if isinstance(a, int)]
+        raise AanetError(f"{name} failed: {msg} (status {rc}); integer args {ints}")
 
 
 def ptr(t):

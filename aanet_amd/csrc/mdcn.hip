@@ -1564,7 +1564,17 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
   }
   const int GP = round_pitch(PT, 16), WTP = round_pitch(co, 2);
   const size_t smem = sizeof(float) * ((size_t)co * GP + (size_t)KC * WTP + (size_t)KC * CP + 3 * 4 * 64);
-  if (smem > 64 * 1024) return AANET_EUNSUPPORTED;
+  // sG grows with Co (Co = 128 in the feature extractor's DCNs: ~69 KB); a gfx950 workgroup may
+  // use the CU's whole 160 KiB of LDS
+  if (smem > 160 * 1024) return AANET_EUNSUPPORTED;
+  static const bool lds_attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_kernel<0>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_kernel<1>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)lds_attr;
   const dim3 gdata((unsigned)(n * host_div_up(P, PT)), (unsigned)dg);
   if (det)
     hipLaunchKernelGGL(mdcn_bwd_data_kernel<1>, gdata, dim3(NT), smem, st, a, grad_out, grad_x,

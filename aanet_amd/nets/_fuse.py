@@ -5,6 +5,7 @@ residual add in its epilogue.  Training mode never uses these: modules then run 
 op sequence with autograd.
 """
 import torch
+import torch.nn as nn
 
 from .. import ops
 from .._lib import is_nhwc
@@ -78,3 +79,64 @@ def use_fused(module, x):
     """Fast path only in eval mode, without autograd, on the HIP device."""
     return (not module.training) and x.is_cuda and not torch.is_grad_enabled() and \
         getattr(module, "aanet_fuse", True)
+
+
+def act_name(m):
+    """Engine epilogue name of an activation module (None: identity; False: not expressible)."""
+    if m is None:
+        return None
+    if isinstance(m, nn.ReLU):
+        return "relu"
+    if isinstance(m, nn.LeakyReLU) and m.negative_slope == 0.2:
+        return "leaky"
+    return False
+
+
+def engine_conv(conv):
+    """A conv the HIP implicit-GEMM engine runs (plain 2-D, zero padding, square parameters)."""
+    if type(conv) is not nn.Conv2d or conv.padding_mode != "zeros" or isinstance(conv.padding, str):
+        return False
+    return all(v[0] == v[1] for v in (conv.stride, conv.padding, conv.dilation, conv.kernel_size))
+
+
+def _leaves(seq):
+    for m in seq:
+        if isinstance(m, nn.Sequential):
+            yield from _leaves(m)
+        else:
+            yield m
+
+
+def run_fused_chain(mods, x):
+    """Run a flat module list in eval: each conv [+ BatchNorm2d] [+ ReLU | LeakyReLU(0.2)] run of
+    it is ONE HIP engine kernel; anything else (pooling, transposed convs, ...) runs as is."""
+    i, n = 0, len(mods)
+    while i < n:
+        m = mods[i]
+        if engine_conv(m):
+            bn = act = None
+            j = i + 1
+            if j < n and isinstance(mods[j], nn.BatchNorm2d):
+                bn, j = mods[j], j + 1
+            if j < n and act_name(mods[j]) not in (None, False):
+                act, j = act_name(mods[j]), j + 1
+            x = conv_bn_act(x, m, bn, act)
+            i = j
+        else:
+            x = m(x)
+            i += 1
+    return x
+
+
+class FusedSequential(nn.Sequential):
+    """nn.Sequential with the reference's children (same state-dict keys, nesting allowed) that
+    in eval mode without autograd runs its conv/BN/activation runs as HIP engine kernels
+    (run_fused_chain); training / autograd runs the children in order."""
+
+    def forward(self, x):
+        if use_fused(self, x):
+            return run_fused_chain(list(_leaves(self)), x)
+        return super().forward(x)
+
+
+ConvBNAct = FusedSequential

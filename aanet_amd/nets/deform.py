@@ -75,6 +75,8 @@ class DeformConv2d(nn.Module):
                                    oc.dilation) for i in range(g)], 1)
 
     def forward(self, x):
+        if self.modulation and use_fused(self, x):
+            return self.forward_fused(x)
         if self.modulation:
             offset_mask = self._offset_conv(x)
             offset_channel = self.deformable_groups * 2 * self.kernel_size * self.kernel_size
@@ -191,6 +193,8 @@ class DeformBottleneck(_BottleneckBase):
         self.stride = stride
 
     def forward(self, x):
+        if use_fused(self, x):
+            return self._forward_fused(x, deform=True)
         return self._forward_ref(x)
 
 

@@ -114,6 +114,43 @@ class DisparityRegressionFunction(Function):
         return gc, None
 
 
+# ------------------------------------------------------------------ disparity warp ------
+def disp_warp(img, disp, with_mask=True):
+    """nets/warp.py:41-64 (padding 'border') -> (warped [B,C,H,W], valid mask or None)."""
+    require_gpu(img, disp, names=("img", "disp"))
+    B, C, H, W = img.shape
+    if tuple(disp.shape) != (B, 1, H, W):
+        raise ValueError(f"disp must be [B, 1, H, W] = {(B, 1, H, W)}, got {tuple(disp.shape)}")
+    warped = torch.empty_like(img)
+    valid = torch.empty_like(img) if with_mask else None
+    call("aanet_disp_warp_f32", ptr(img), ptr(disp), ptr(warped), ptr(valid), B, C, H, W,
+         stream_of(img))
+    return warped, valid
+
+
+class DispWarpFunction(Function):
+    """Warped image with autograd to the disparity (and to the image when it requires grad)."""
+
+    @staticmethod
+    def forward(ctx, img, disp):
+        img, disp = img.contiguous(), disp.contiguous()
+        ctx.save_for_backward(img, disp)
+        return disp_warp(img, disp, with_mask=False)[0]
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_warped):
+        img, disp = ctx.saved_tensors
+        grad_warped = grad_warped.contiguous()
+        require_gpu(grad_warped, names=("grad_warped",))
+        gd = torch.empty_like(disp)
+        gi = torch.zeros_like(img) if ctx.needs_input_grad[0] else None
+        B, C, H, W = img.shape
+        call("aanet_disp_warp_bwd_f32", ptr(img), ptr(disp), ptr(grad_warped), ptr(gd), ptr(gi),
+             B, C, H, W, stream_of(img))
+        return gi, gd
+
+
 # ------------------------------------------------------- modulated deformable conv ------
 def mdcn_forward(x, offset, mask, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
                  deformable_groups=1, out=None):

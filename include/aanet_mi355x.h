@@ -85,6 +85,22 @@ int aanet_disp_regress_f32(const float *cost, float *disp, int n, int d, int h, 
 int aanet_disp_regress_bwd_f32(const float *cost, const float *grad_disp, float *grad_cost, int n,
                                int d, int h, int w, int negate, aanet_stream_t stream);
 
+/* ------------------------------------------------------------ disparity warp ----------- */
+
+/* nets/warp.py:41-64 (disp_warp, padding 'border'): img [n, c, h, w], disp [n, 1, h, w] ->
+ * warped [n, c, h, w] = img sampled at (x - disp, y) (grid_sample, bilinear, align_corners=True,
+ * border padding); valid_mask [n, c, h, w] (or NULL) = 1 where grid_sample of ones with zeros
+ * padding is >= 0.9999, else 0.  Both OVERWRITTEN.  h, w >= 2.  The reference's
+ * `assert disp.min() >= 0` (warp.py:52) is the caller's: the kernel warps any disparity. */
+int aanet_disp_warp_f32(const float *img, const float *disp, float *warped, float *valid_mask,
+                        int n, int c, int h, int w, aanet_stream_t stream);
+
+/* Autograd of the warped image: grad_disp [n, 1, h, w] OVERWRITTEN; grad_img [n, c, h, w]
+ * (or NULL) ACCUMULATED (caller zeroes; float atomics). */
+int aanet_disp_warp_bwd_f32(const float *img, const float *disp, const float *grad_warped,
+                            float *grad_disp, float *grad_img, int n, int c, int h, int w,
+                            aanet_stream_t stream);
+
 /* ------------------------------------------------------ modulated deformable conv ------ */
 
 /* deform_conv_cuda.cpp:490-569 (modulated_deform_conv_cuda_forward) + kernel.cu:570-633.

@@ -198,3 +198,68 @@ def mdcn_backward(x, offset, mask, weight, grad_out, with_bias=False, stride=1, 
                                     N, C, H, W, Co, kh, kw, stride, padding, dilation, groups,
                                     deformable_groups)
     return gx, goff, gm, gw, gb
+
+
+# ------------------------------------------------------------------ disparity warp --------
+def _warp_coords(disp, H, W):
+    """nets/warp.py:5-16 + grid_sample(align_corners=True) unnormalisation, in float32 steps."""
+    f = np.float32
+    x = np.arange(W, dtype=f)[None, None, :]
+    y = np.arange(H, dtype=f)[None, :, None]
+    nx = f(2) * ((x - disp[:, 0]) / f(W - 1)) - f(1)
+    ny = f(2) * (y / f(H - 1)) - f(1)
+    ix = ((nx + f(1)) / f(2)) * f(W - 1)
+    iy = np.broadcast_to(((ny + f(1)) / f(2)) * f(H - 1), ix.shape)
+    return ix.astype(f), iy.astype(f)
+
+
+def _corners(ix, iy):
+    x0, y0 = np.floor(ix), np.floor(iy)
+    w = ((x0 + 1 - ix) * (y0 + 1 - iy), (ix - x0) * (y0 + 1 - iy),
+         (x0 + 1 - ix) * (iy - y0), (ix - x0) * (iy - y0))
+    pos = ((y0, x0), (y0, x0 + 1), (y0 + 1, x0), (y0 + 1, x0 + 1))
+    return [(yy.astype(np.int64), xx.astype(np.int64), ww) for (yy, xx), ww in zip(pos, w)]
+
+
+def disp_warp(img, disp):
+    """nets/warp.py:41-64 (padding 'border'): (warped [B,C,H,W], valid mask [B,C,H,W]).
+    grid_sample's border clip is min(size-1, max(v, 0)); corners outside the image add 0."""
+    img = np.ascontiguousarray(img, np.float32)
+    disp = np.ascontiguousarray(disp, np.float32)
+    B, C, H, W = img.shape
+    ix, iy = _warp_coords(disp, H, W)
+    ixc = np.minimum(np.float32(W - 1), np.maximum(ix, np.float32(0)))
+    iyc = np.minimum(np.float32(H - 1), np.maximum(iy, np.float32(0)))
+    b = np.arange(B)[:, None, None]
+    out = np.zeros_like(img)
+    for yy, xx, ww in _corners(ixc, iyc):
+        ok = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
+        v = img[b, :, np.clip(yy, 0, H - 1), np.clip(xx, 0, W - 1)]  # [B,H,W,C]
+        out += np.moveaxis(v * (ww * ok)[..., None], -1, 1)
+    m = np.zeros(ix.shape, np.float32)
+    for yy, xx, ww in _corners(ix, iy):  # grid_sample(ones, zeros padding): unclipped
+        m += ww * ((yy >= 0) & (yy < H) & (xx >= 0) & (xx < W))
+    valid = np.where(m < np.float32(0.9999), np.float32(0), np.float32(1))
+    return out, np.repeat(valid[:, None], C, axis=1)
+
+
+def disp_warp_bwd(img, disp, grad_warped):
+    """d(sum grad_warped * warped)/d disp of disp_warp (float64): the x-derivative of the
+    bilinear sample times the border clip's pass-through (0 where clipped) times -1."""
+    img = np.asarray(img, np.float64)
+    g = np.asarray(grad_warped, np.float64)
+    B, C, H, W = img.shape
+    ix, iy = (a.astype(np.float64) for a in _warp_coords(np.asarray(disp, np.float32), H, W))
+    pas = ((ix > 0) & (ix < W - 1)).astype(np.float64)
+    ixc, iyc = np.clip(ix, 0, W - 1), np.clip(iy, 0, H - 1)
+    x0, y0 = np.floor(ixc), np.floor(iyc)
+    b = np.arange(B)[:, None, None]
+    gix = np.zeros(ix.shape)
+    for dy, dx, sgn_x, wy in ((0, 0, -1, y0 + 1 - iyc), (0, 1, 1, y0 + 1 - iyc),
+                              (1, 0, -1, iyc - y0), (1, 1, 1, iyc - y0)):
+        yy, xx = (y0 + dy).astype(np.int64), (x0 + dx).astype(np.int64)
+        ok = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
+        v = img[b, :, np.clip(yy, 0, H - 1), np.clip(xx, 0, W - 1)]  # [B,H,W,C]
+        gv = np.moveaxis(g, 1, -1)
+        gix += sgn_x * wy * ok * (v * gv).sum(-1)
+    return (-gix * pas)[:, None]

@@ -56,11 +56,12 @@ class _StandInModulatedDeformConv(nn.Module):
         self.weight.data.uniform_(-stdv, stdv)
 
     def forward(self, x, offset, mask):
+        dtype = np.float64 if x.dtype == torch.float64 else np.float32  # fp64: sensitivity runs
         out = oracle.mdcn_forward(x.detach().numpy(), offset.detach().numpy(), mask.detach().numpy(),
                                   self.weight.detach().numpy(),
                                   None if self.bias is None else self.bias.detach().numpy(),
                                   self.stride, self.padding, self.dilation, self.groups,
-                                  self.deformable_groups)
+                                  self.deformable_groups, dtype=dtype)
         return torch.from_numpy(out)
 
 

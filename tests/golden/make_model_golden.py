@@ -1,0 +1,109 @@
+"""Full-model golden vectors from the REFERENCE's own nets/aanet.py.
+Run in the build container only (needs /root/reference; never on the GPU box):
+    python tests/golden/make_model_golden.py
+Imports the reference package by path exactly as make_golden.py does (nets/__init__.py and the
+CUDA-only deform_conv_cuda are never executed; nets.deform_conv is the stand-in whose
+ModulatedDeformConv runs the oracle DCN).  Builds AANet and AANet+ as the reference's
+inference scripts configure them (scripts/aanet_inference.sh, scripts/aanet+_inference.sh),
+fills every parameter/buffer with tests.golden_io.synthetic_value (name-keyed, so the test
+can rebuild the same weights in our model without shipping them), runs eval forward on small
+seeded image pairs (tests.golden_io.synthetic_pair, rebuilt by the test from the seed), and
+saves DATA ONLY: the output disparity pyramid, the state-dict (name, shape) list and
+checksums of the filled weights and of the images, plus the same model's float64 outputs
+(the reference's own fp32 rounding sensitivity, which the tests use as the scale).  Also disp_warp vectors
+(nets/warp.py:41-64) for the oracle and the HIP warp kernel.
+"""
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
+
+from make_golden import REF, load_reference, save  # noqa: E402
+from tests.golden_io import fill_synthetic, synthetic_pair  # noqa: E402
+
+MODELS = {
+    # tag: (constructor kwargs, image (H, W), batch, seed)
+    "aanet": (dict(feature_type="aanet", feature_pyramid_network=True,
+                   refinement_type="stereodrnet", no_intermediate_supervision=True), (48, 96), 2, 11),
+    "aanet_inter": (dict(feature_type="aanet", feature_pyramid_network=True,
+                         refinement_type="stereodrnet", no_intermediate_supervision=False),
+                    (48, 96), 1, 12),
+    "aanetplus": (dict(feature_type="ganet", feature_pyramid=True, refinement_type="hourglass",
+                       no_intermediate_supervision=True), (96, 192), 1, 13),
+    # -AA variants (scripts/*-aa_inference.sh): other feature extractors + adaptive aggregation
+    "stereonet_aa": (dict(feature_type="stereonet", num_scales=1, num_fusions=4,
+                          num_deform_blocks=4, refinement_type="stereonet"), (64, 128), 1, 14),
+    "gcnet_aa": (dict(feature_type="gcnet", feature_pyramid=True, num_downsample=1,
+                      no_intermediate_supervision=True), (48, 96), 1, 15),
+    "psmnet_aa": (dict(feature_type="psmnet", feature_pyramid=True,
+                       no_intermediate_supervision=True), (256, 256), 1, 16),
+    # 3-D aggregators on concat / difference volumes (C5)
+    "psmnet_hg": (dict(feature_type="psmnet", feature_similarity="concat",
+                       aggregation_type="psmnet_hourglass", refinement_type=None), (256, 256), 1, 17),
+    "psmnet_basic": (dict(feature_type="psmnet", feature_similarity="concat",
+                          aggregation_type="psmnet_basic", refinement_type=None), (256, 256), 1, 18),
+    "gcnet_3d": (dict(feature_type="gcnet", feature_similarity="concat", aggregation_type="gcnet",
+                      refinement_type=None), (64, 128), 1, 19),
+    "stereonet_3d": (dict(feature_type="stereonet", feature_similarity="difference",
+                          aggregation_type="stereonet", refinement_type="stereonet"), (64, 128), 1, 20),
+}
+# max_disp per config (the image-resolution disparity range; GC-Net needs D/2 divisible by 16)
+MAX_DISP_OF = {"gcnet_3d": 64, "psmnet_aa": 64, "psmnet_hg": 64, "psmnet_basic": 64}
+MAX_DISP = 48
+
+
+def checksum(sd):
+    return np.float64(sum(float(v.double().abs().sum()) for v in sd.values()))
+
+
+def main():
+    load_reference()  # installs the stand-in `nets` package + nets.deform_conv
+    aanet = importlib.import_module("nets.aanet")
+    warp = importlib.import_module("nets.warp")
+    g = torch.Generator().manual_seed(20261016)
+
+    # ---- disp_warp (warp.py:41-64): fractional, integer and out-of-range disparities
+    for tag, (B, C, H, W) in {"a": (2, 3, 9, 17), "b": (1, 4, 5, 33)}.items():
+        img = torch.randn(B, C, H, W, generator=g)
+        disp = torch.rand(B, 1, H, W, generator=g) * (W * 0.6)
+        disp[:, :, 0, :4] = torch.tensor([0.0, 1.0, 2.5, float(W + 3)])  # exact / beyond the edge
+        warped, valid = warp.disp_warp(img, disp.clone())
+        save(f"warp_{tag}", img=img, disp=disp, warped=warped, valid=valid)
+
+    # ---- full models (aanet.py:14-229)
+    only = set(sys.argv[1:])
+    for tag, (kw, (H, W), B, seed) in MODELS.items():
+        if only and tag not in only:
+            continue
+        torch.manual_seed(seed)
+        max_disp = MAX_DISP_OF.get(tag, MAX_DISP)
+        model = aanet.AANet(max_disp, 1, **kw)
+        names = fill_synthetic(model, seed)
+        model.eval()
+        left, right = synthetic_pair(B, H, W, seed)
+        with torch.no_grad():
+            pyr = model(left, right)
+            # the same model in float64: how far the reference's own fp32 result is from the
+            # exact answer (the tests hold our fp32 result to the same distance)
+            pyr64 = model.double()(left.double(), right.double())
+        save(f"model_{tag}", shape=np.array([B, H, W]), config=np.array(json.dumps(kw)),
+             img_checksum=np.float64(float(left.double().sum() + right.double().abs().sum())),
+             names=np.array([n for n, _ in names]),
+             shapes=np.array([",".join(map(str, s)) for _, s in names]),
+             checksum=checksum(model.state_dict()), seed=seed, max_disp=max_disp,
+             **{f"disp{i}": d for i, d in enumerate(pyr)},
+             **{f"disp64_{i}": d for i, d in enumerate(pyr64)})
+        print(f"  {tag}: {len(names)} entries, pyramid " +
+              ", ".join(f"{tuple(d.shape)} mean {d.mean():.2f}" for d in pyr))
+
+
+if __name__ == "__main__":
+    main()

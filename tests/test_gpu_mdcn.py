@@ -120,6 +120,8 @@ BWD_CASES = [
     (2, 32, 9, 26, 32, 3, 1, 2, 2, 2),
     (1, 16, 5, 13, 16, 3, 1, 2, 2, 2),
     (1, 48, 10, 21, 36, 3, 2, 1, 1, 3),
+    (1, 128, 8, 20, 128, 3, 2, 2, 2, 2),   # feature-extractor DCN: Co=128 (> 64 KB LDS tile)
+    (1, 64, 7, 18, 96, 3, 2, 2, 2, 2),     # GANet conv3a: 64 -> 96, stride 2
 ]
 
 

@@ -1,0 +1,128 @@
+"""GPU parity of the full models and the refinement warp against the
+reference's own outputs (tests/golden/make_model_golden.py: nets/aanet.py run on CPU with the
+oracle DCN, name-keyed synthetic weights, seeded image pairs).  Eval mode runs with the HIP
+engine fusions on and off."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from aanet_amd import nets, ops, train
+from oracle import oracle
+from tests.golden_io import fill_synthetic, golden, golden_names, synthetic_pair
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+MODEL_FIXTURES = golden_names("model_")
+
+
+# ------------------------------------------------------------------ disparity warp --------
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_disp_warp_vs_reference_golden(tag):
+    g = golden(f"warp_{tag}")
+    img, disp = torch.from_numpy(g["img"]).to(DEV), torch.from_numpy(g["disp"]).to(DEV)
+    warped, valid = nets.disp_warp(img, disp)
+    assert np.abs(warped.cpu().numpy() - g["warped"]).max() <= 1e-5
+    assert np.array_equal(valid.cpu().numpy(), g["valid"])
+
+
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_disp_warp_backward_vs_oracle(tag):
+    g = golden(f"warp_{tag}")
+    img = torch.from_numpy(g["img"]).to(DEV).requires_grad_()
+    disp = torch.from_numpy(g["disp"]).to(DEV).requires_grad_()
+    warped, _ = nets.disp_warp(img, disp)
+    go = torch.randn(warped.shape, generator=torch.Generator().manual_seed(5)).to(DEV)
+    (warped * go).sum().backward()
+    ref_d = oracle.disp_warp_bwd(g["img"], g["disp"], go.cpu().numpy())
+    assert np.abs(disp.grad.cpu().numpy() - ref_d).max() <= 1e-4 * max(1.0, np.abs(ref_d).max())
+    # image gradient: the transpose of the bilinear sampling, checked through linearity --
+    # <grad_img, img> equals <grad_out, warped> because warped is linear in img
+    lhs = float((img.grad.double() * img.detach().double()).sum())
+    rhs = float((go.double() * warped.detach().double()).sum())
+    assert lhs == pytest.approx(rhs, rel=1e-5, abs=1e-4)
+
+
+def test_disp_warp_rejects_bad_shapes():
+    img = torch.zeros(1, 3, 4, 5, device=DEV)
+    with pytest.raises(ValueError):
+        ops.disp_warp(img, torch.zeros(1, 3, 4, 5, device=DEV))
+
+
+# ------------------------------------------------------------------ full models -----------
+def build(tag, fuse=True):
+    g = golden(tag)
+    m = nets.AANet(int(g["max_disp"]), 1, **json.loads(str(g["config"])))
+    fill_synthetic(m, int(g["seed"]))
+    m = m.to(DEV).eval()
+    for mod in m.modules():
+        mod.aanet_fuse = fuse
+    B, H, W = (int(v) for v in g["shape"])
+    left, right = synthetic_pair(B, H, W, int(g["seed"]))
+    return g, m, left.to(DEV), right.to(DEV)
+
+
+# the north-star models: held to the 1e-3 px bar against the reference's fp32 output itself
+STRICT = {"model_aanet", "model_aanet_inter", "model_aanetplus"}
+
+
+def _stats(e):
+    return float(e.mean()), float(np.percentile(e, 99)), float(e.max())
+
+
+@pytest.mark.parametrize("fuse", [True, False])
+@pytest.mark.parametrize("tag", MODEL_FIXTURES)
+def test_full_model_vs_reference_golden(tag, fuse):
+    """Every level of the disparity pyramid against the reference run on the same weights and
+    images.  Deep random-weight nets amplify fp32 rounding very differently per configuration
+    (PSMNet's 25 un-normalised residual blocks turn it into sparse 0.1-0.7 px flips of near-tie
+    soft-argmins -- in the reference's OWN fp32 run, measured against its fp64 run), so the
+    test holds our fp32 result to the exact (fp64) answer no worse than the reference's own fp32
+    distance times 2 (mean, p99) / 4 (max), and the AANet / AANet+ models additionally to max 1e-3 px
+    against the reference's fp32 output."""
+    g, m, left, right = build(tag, fuse)
+    with torch.no_grad():
+        pyr = m(left, right)
+    n = len([k for k in g if k.startswith("disp") and not k.startswith("disp64")])
+    assert len(pyr) == n
+    report = []
+    for i, d in enumerate(pyr):
+        ref32, ref64 = g[f"disp{i}"], g[f"disp64_{i}"]
+        assert tuple(d.shape) == ref32.shape
+        ours = d.cpu().numpy().astype(np.float64)
+        e32 = _stats(np.abs(ours - ref32))
+        e64 = _stats(np.abs(ours - ref64))
+        sens = _stats(np.abs(ref32.astype(np.float64) - ref64))
+        report.append((i, e32, e64, sens))
+        # mean and p99 within 2x the reference's own fp32 distance; the max (a single sparse
+        # near-tie flip, a noisy one-sample statistic) within 4x
+        for got, bound, k, slack in zip(e64, sens, (2, 2, 4), (1e-5, 1e-4, 1e-3)):
+            assert got <= k * bound + slack, (i, "vs fp64", e64, "ref fp32 vs fp64", sens)
+        if tag in STRICT:
+            assert e32[2] <= 1e-3, (i, e32)
+    print(tag, "fused" if fuse else "ref-order", ["L%d vs32 mean/p99/max %.1e/%.1e/%.1e | "
+          "vs64 %.1e/%.1e/%.1e | ref32-vs-64 %.1e/%.1e/%.1e" % ((i,) + a + b + c)
+          for i, a, b, c in report])
+
+
+def test_full_model_training_step():
+    """AANet with intermediate supervision in train mode: the 5-level pyramid, the reference
+    loss weights, backward through every HIP kernel (DCN in the feature extractor and the
+    aggregation, warp in the refinement), finite non-zero gradients everywhere."""
+    g, m, left, right = build("model_aanet_inter")
+    m.train()
+    pyr = m(left, right)
+    assert len(pyr) == 5
+    gt = torch.rand(left.shape[0], *left.shape[2:], device=DEV) * 40 + 1
+    total, per = train.disparity_loss(pyr, gt, gt > 0)
+    total.backward()
+    assert torch.isfinite(total)
+    groups = {"feature_extractor": 0.0, "fpn": 0.0, "aggregation": 0.0, "refinement": 0.0}
+    for name, p in m.named_parameters():
+        assert p.grad is not None, name
+        assert torch.isfinite(p.grad).all(), name
+        top = name.split(".")[0]
+        if top in groups:
+            groups[top] += float(p.grad.abs().sum())
+    assert all(v > 0 for v in groups.values()), groups

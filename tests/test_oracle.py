@@ -227,3 +227,32 @@ def test_cost_volume_backward_matches_torch_autograd_of_reference_formula():
         ol, or_ = oracle.shift_volume_bwd(g.numpy(), C, concat, dtype=np.float64)
         np.testing.assert_allclose(ol, gl.numpy(), rtol=1e-12, atol=1e-12)
         np.testing.assert_allclose(or_, gr.numpy(), rtol=1e-12, atol=1e-12)
+
+
+# ------------------------------------------------------------------ disparity warp --------
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_disp_warp_vs_reference_golden(tag):
+    """oracle.disp_warp against nets/warp.py:41-64 run by the reference (make_model_golden.py)."""
+    g = golden(f"warp_{tag}")
+    warped, valid = oracle.disp_warp(g["img"], g["disp"])
+    assert np.abs(warped - g["warped"]).max() <= 1e-6
+    assert np.array_equal(valid, g["valid"])
+
+
+def test_disp_warp_bwd_vs_torch_autograd_f64():
+    import torch
+    import torch.nn.functional as F
+    g = golden("warp_a")
+    img = torch.from_numpy(g["img"]).double()
+    disp = torch.from_numpy(g["disp"]).double().requires_grad_()
+    B, C, H, W = img.shape
+    xs = torch.arange(W, dtype=torch.float64).view(1, 1, W).expand(B, H, W)
+    ys = torch.arange(H, dtype=torch.float64).view(1, H, 1).expand(B, H, W)
+    gx = 2 * ((xs - disp[:, 0]) / (W - 1)) - 1
+    gy = 2 * (ys / (H - 1)) - 1
+    out = F.grid_sample(img, torch.stack((gx, gy), -1), mode="bilinear", padding_mode="border",
+                        align_corners=True)
+    go = torch.randn(out.shape, generator=torch.Generator().manual_seed(3), dtype=torch.float64)
+    (out * go).sum().backward()
+    ref = oracle.disp_warp_bwd(g["img"], g["disp"], go.numpy())
+    assert np.abs(ref - disp.grad.numpy()).max() <= 1e-9
