@@ -78,6 +78,31 @@ def main():
         warped, valid = warp.disp_warp(img, disp.clone())
         save(f"warp_{tag}", img=img, disp=disp, warped=warped, valid=valid)
 
+    # ---- file formats (utils/file_io.py:34-105): PFM bytes written by the reference's own
+    # write_pfm, and the reference's demo prediction PNG (a data file it ships) as-is
+    import shutil
+    import tempfile
+    fio = importlib.import_module("ref_file_io") if "ref_file_io" in sys.modules else None
+    if fio is None:
+        spec = importlib.util.spec_from_file_location("ref_file_io",
+                                                      os.path.join(REF, "utils", "file_io.py"))
+        fio = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(fio)
+    gray = (torch.rand(7, 11, generator=g) * 90).numpy()
+    color = (torch.rand(5, 6, 3, generator=g) * 2 - 1).numpy()
+    blobs = {}
+    with tempfile.TemporaryDirectory() as td:
+        for name, arr in (("gray", gray), ("color", color)):
+            path = os.path.join(td, name + ".pfm")
+            fio.write_pfm(path, arr)
+            blobs[name + "_bytes"] = np.frombuffer(open(path, "rb").read(), np.uint8)
+        demo = os.path.join(REF, "demo", "pred", "000151_10_pred.png")
+        shutil.copyfile(demo, os.path.join(HERE, "kitti_demo_pred.png"))
+        kd = fio._read_kitti_disp(demo)
+    save("pfm_ref", gray=gray, color=color, **blobs)
+    save("kitti_demo_stats", shape=np.array(kd.shape), total=np.float64(kd.astype(np.float64).sum()),
+         nonzero=np.int64((kd > 0).sum()), row100=kd[100].copy())
+
     # ---- full models (aanet.py:14-229)
     only = set(sys.argv[1:])
     for tag, (kw, (H, W), B, seed) in MODELS.items():
