@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--train-batch", type=int, default=4, help="training pairs per GPU")
     ap.add_argument("--deterministic", action="store_true",
                     help="--train with torch.use_deterministic_algorithms (det DCN backward)")
+    ap.add_argument("--model", default=None, choices=sorted(FULL_MODELS),
+                    help="time the full model (features + hot path + refinement) instead")
     ap.add_argument("--only", default=None,
                     help="profiling mode: run only one kernel family (corr|mdcn|regress|step)")
     return ap.parse_args()
@@ -185,36 +187,12 @@ def cpu_baseline(model, left, right, gpu_disp):
                 seconds=dt), float(diff.mean()), float(diff.max())
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    device = torch.device("cuda", local_rank)
-    torch.cuda.set_device(device)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=device)
-
-    if args.train:
-        train_main(args, device, rank, world)
-        return
-    model = build_model(device)
-    left, right = make_features(args.batch, rank, device, args.features)
-
-    def step():
-        with torch.no_grad():
-            return model(left, right)[0]
-
-    if args.only:
-        profile_only(args, model, left, right, step)
-        return
-
+def timed_run(step, args, world):
+    """W warmup steps, optional HIP-graph capture of one step, then exactly K timed steps between
+    barrier + synchronize pairs.  -> (last output, elapsed seconds, graph or None)."""
     for _ in range(args.warmup):
         out = step()
     torch.cuda.synchronize()
-
     graph = None
     if not args.no_graph:
         try:
@@ -232,7 +210,6 @@ def main():
             print(f"hip graph capture failed ({e}); timing eager launches", file=sys.stderr)
             graph = None
             torch.cuda.synchronize()
-
     run = graph.replay if graph is not None else step
     if world > 1:
         dist.barrier()
@@ -243,7 +220,39 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    return out, time.perf_counter() - t0, graph
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    if args.train:
+        train_main(args, device, rank, world)
+        return
+    if args.model:
+        model_main(args, device, rank, world)
+        return
+    model = build_model(device)
+    left, right = make_features(args.batch, rank, device, args.features)
+
+    def step():
+        with torch.no_grad():
+            return model(left, right)[0]
+
+    if args.only:
+        profile_only(args, model, left, right, step)
+        return
+
+    out, elapsed, graph = timed_run(step, args, world)
     disp = out  # graph output buffer (or last eager output)
 
     from aanet_amd import dist as adist
@@ -293,6 +302,63 @@ def main():
             line["epe_vs_ref"] = epe
             line["max_abs_disp_err_vs_ref"] = mx
         print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+FULL_MODELS = {
+    # scripts/aanet_inference.sh / aanet+_inference.sh (KITTI): constructor kwargs
+    "aanet": dict(feature_type="aanet", feature_pyramid_network=True, refinement_type="stereodrnet",
+                  no_intermediate_supervision=True),
+    "aanetplus": dict(feature_type="ganet", feature_pyramid=True, refinement_type="hourglass",
+                      no_intermediate_supervision=True),
+}
+
+
+def model_main(args, device, rank, world):
+    """--model: the whole network of the reference's KITTI inference scripts on synthetic
+    384x1248 image pairs (ImageNet-normalised noise), eval, random-init weights of that
+    architecture (offset convs non-zero).  Secondary line: not the headline metric."""
+    from aanet_amd.nets import AANet
+    torch.manual_seed(0)
+    model = AANet(MAXD_IMG, **FULL_MODELS[args.model])
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for name, mod in model.named_modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.running_mean.copy_(0.05 * torch.randn(mod.num_features, generator=g))
+                mod.running_var.copy_(0.8 + 0.4 * torch.rand(mod.num_features, generator=g))
+            if name.endswith("offset_conv"):
+                mod.weight.normal_(0.0, 0.01, generator=g)
+                mod.bias.normal_(0.0, 0.5, generator=g)
+    model = model.to(device).eval()
+    gen = torch.Generator(device=device).manual_seed(4321 + rank)
+    left = torch.randn((args.batch, 3, H_IMG, W_IMG), device=device, generator=gen)
+    right = torch.randn((args.batch, 3, H_IMG, W_IMG), device=device, generator=gen)
+
+    def step():
+        with torch.no_grad():
+            return model(left, right)[-1]
+
+    out, elapsed, graph = timed_run(step, args, world)
+    from aanet_amd import dist as adist
+    rec = adist.make_record(device, pairs=args.batch * args.steps, elapsed_s=elapsed,
+                            disp_min=float(out.min()), disp_max=float(out.max()))
+    summary = adist.summarize(adist.gather_records(rec))
+    if rank == 0:
+        print(json.dumps({
+            "metric": f"full-model stereo-pairs/s @384x1248 ({args.model}, KITTI config) fp32",
+            "value": summary["pairs"] / summary["elapsed_max_s"], "unit": "stereo-pairs/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": 1000.0 * summary["elapsed_max_s"] / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (N(0,1) image pairs, random-init weights)",
+            "config": {"workload": f"{args.model}: {FULL_MODELS[args.model]}, max_disp 192",
+                       "batch_per_gpu": args.batch, "global_batch": args.batch * world,
+                       "parallelism": f"dp{world} (pairs sharded, no data-path collective)",
+                       "hip_graph": graph is not None},
+            "disp_range": [summary["disp_min"], summary["disp_max"]]}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
