@@ -21,10 +21,19 @@ template <int NJ>
 struct CorrSmem {
   static constexpr int RW = TX + 16 * (NJ - 1);       // right-feature window width
   static constexpr int DC = 16 * (NJ - 1) + 1 > 64 ? 64 : 16 * (NJ - 1) + 1;
-  static constexpr int STAGE = CC * TX + CC * RW;      // floats per stage
-  static constexpr int OUTP = TX + 1;                  // padded [d][x] output pitch
+  // LDS row pitches = 16 (mod 32) dwords: an MFMA operand read (ds_read_b32, two 32-lane groups,
+  // bank = dword mod 32) has lanes kr = 0,1 one row apart -> 16 banks apart, conflict-free
+  static constexpr int LP = TX + 16;
+  static constexpr int RP = RW + 16;
+  static constexpr int STAGE = CC * LP + CC * RP;      // floats per stage
+  // [d][x] band tile pitch: odd (lanes jj distinct) with 4*(OUTP+1) = 16 (mod 32) (kr groups
+  // disjoint) -> conflict-free band writes
+  static constexpr int OUTP = TX + 3;
+  // band rows dl = 16j + i - jj span [-15, 16*NJ): rows outside [0, dchunk) are scratch, so the
+  // band is written without per-element predicates (immediate LDS offsets from one base)
+  static constexpr int OROWS = 16 * NJ + 15;
   static constexpr int BYTES_STAGE = 2 * STAGE * 4;
-  static constexpr int BYTES_OUT = 64 * OUTP * 4;
+  static constexpr int BYTES_OUT = OROWS * OUTP * 4;
   static constexpr int BYTES = BYTES_STAGE > BYTES_OUT ? BYTES_STAGE : BYTES_OUT;
 };
 
@@ -68,24 +77,32 @@ __global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
   constexpr int RPT = (CC * RW + NTHREADS - 1) / NTHREADS;
   f32x4 lq[VEC ? 1 : 1], rq[VEC ? RPT4 : 1];
   float lreg[VEC ? 1 : LPT], rreg[VEC ? 1 : RPT];
+  const int HW4 = (int)(HW * 4);  // VEC requires C*H*W*4 < 2^31 (launcher)
+  const int lrow = tid / (TX / 4), lcol = x0 + 4 * (tid % (TX / 4));
+  const bool lok = lcol < W;
+  const int lbase = (lrow * (int)HW + y * W + lcol) * 4;
+  int rrow[RPT4], rbase[RPT4];
+  bool rok[RPT4];
+#pragma unroll
+  for (int i = 0; i < RPT4; ++i) {
+    const int e = tid + i * NTHREADS;
+    const int x = xr0 + 4 * (e % (RW / 4));
+    rrow[i] = e / (RW / 4);
+    rok[i] = e < RQ && x >= 0 && x < W;
+    rbase[i] = (rrow[i] * (int)HW + y * W + x) * 4;
+  }
 
   auto load_stage = [&](int c0) {
     if (VEC) {
-      {
-        const int row = tid / (TX / 4), col4 = tid % (TX / 4);
-        const int c = c0 + row, x = x0 + 4 * col4;
-        const int off = (c < C && x < W) ? (int)((((long)c * H + y) * W + x) * 4) : img_bytes;
-        lq[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(Lr, off, 0, 0));
-      }
+      // per-thread int32 byte offsets (lbase / rbase, hoisted) + the stage's channel offset
+      // (scalar); out-of-range elements take the OOB offset, whose load returns 0
+      const int coff = c0 * HW4;
+      lq[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+          Lr, (c0 + lrow < C && lok && tid < LQ) ? lbase + coff : img_bytes, 0, 0));
 #pragma unroll
-      for (int i = 0; i < RPT4; ++i) {
-        const int e = tid + i * NTHREADS;
-        const int row = e / (RW / 4), col4 = e % (RW / 4);
-        const int c = c0 + row, x = xr0 + 4 * col4;
-        const bool ok = e < RQ && c < C && x >= 0 && x < W;
-        const int off = ok ? (int)((((long)c * H + y) * W + x) * 4) : img_bytes;
-        rq[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(Rr, off, 0, 0));
-      }
+      for (int i = 0; i < RPT4; ++i)
+        rq[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+            Rr, (c0 + rrow[i] < C && rok[i]) ? rbase[i] + coff : img_bytes, 0, 0));
     } else {
 #pragma unroll
       for (int i = 0; i < LPT; ++i) {
@@ -102,25 +119,28 @@ __global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
     }
   };
   auto store_stage = [&](int buf) {
-    float *sL = smem + buf * S::STAGE, *sR = sL + CC * TX;
+    float *sL = smem + buf * S::STAGE, *sR = sL + CC * S::LP;
     if (VEC) {
-      reinterpret_cast<f32x4 *>(sL)[tid] = lq[0];
+      if (tid < LQ)
+        *reinterpret_cast<f32x4 *>(sL + lrow * S::LP + 4 * (tid % (TX / 4))) = lq[0];
 #pragma unroll
       for (int i = 0; i < RPT4; ++i) {
         const int e = tid + i * NTHREADS;
-        if (e < RQ) reinterpret_cast<f32x4 *>(sR)[e] = rq[i];
+        if (e < RQ) *reinterpret_cast<f32x4 *>(sR + rrow[i] * S::RP + 4 * (e % (RW / 4))) = rq[i];
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < LPT; ++i) sL[tid + i * NTHREADS] = lreg[i];
+      for (int i = 0; i < LPT; ++i) {
+        const int e = tid + i * NTHREADS;
+        sL[(e / TX) * S::LP + e % TX] = lreg[i];
+      }
 #pragma unroll
       for (int i = 0; i < RPT; ++i) {
         const int e = tid + i * NTHREADS;
-        if (e < CC * RW) sR[e] = rreg[i];
+        if (e < CC * RW) sR[(e / RW) * S::RP + e % RW] = rreg[i];
       }
     }
   };
-  (void)LQ;
 
   f32x4 acc[NJ];
 #pragma unroll
@@ -134,14 +154,14 @@ __global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
   for (int s = 0; s < nstages; ++s) {
     const int buf = s & 1;
     if (s + 1 < nstages) load_stage((s + 1) * CC);
-    const float *sL = smem + buf * S::STAGE, *sR = sL + CC * TX;
+    const float *sL = smem + buf * S::STAGE, *sR = sL + CC * S::LP;
 #pragma unroll
     for (int ks = 0; ks < CC / 4; ++ks) {
       const int row = 4 * ks + kr;
-      const float a = sL[row * TX + 16 * wave + jj];
+      const float a = sL[row * S::LP + 16 * wave + jj];
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const float bv = sR[row * RW + 16 * wave + jj + 16 * (NJ - 1 - j)];
+        const float bv = sR[row * S::RP + 16 * wave + jj + 16 * (NJ - 1 - j)];
         acc[j] = mfma16x16x4(a, bv, acc[j]);
       }
     }
@@ -150,17 +170,16 @@ __global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
   }
 
   // Band -> [d][x] tile in LDS.  Lane holds x' column jj, rows i = 4*kr + r (x).
-  float *sO = smem;
-  const float Cf = (float)C;
+  // Row dl = 16j + 4kr + r - jj, column 16*wave + 4kr + r: one base per lane, the (j, r) part
+  // is an immediate offset.  Rows outside [0, dmax) land in the scratch rows and are not stored.
+  float *sO = smem + 15 * S::OUTP;
+  const float invC = 1.f / (float)C;  // exact for power-of-two C (AANet: 128, 32)
   const int dmax = min(dchunk, D - d0);
+  float *sOl = sO + (4 * kr - jj) * S::OUTP + 16 * wave + 4 * kr;
 #pragma unroll
   for (int j = 0; j < NJ; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = 4 * kr + r;
-      const int dl = 16 * j + i - jj;
-      if (dl >= 0 && dl < dmax) sO[dl * S::OUTP + 16 * wave + i] = acc[j][r] / Cf;
-    }
+    for (int r = 0; r < 4; ++r) sOl[(16 * j + r) * S::OUTP + r] = acc[j][r] * invC;
   __syncthreads();
   if (VEC) {
     for (int e = tid; e < dmax * (TX / 4); e += NTHREADS) {
