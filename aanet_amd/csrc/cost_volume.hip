@@ -3,13 +3,15 @@
 // Correlation (cost.py:40-48) is a banded contraction over channels:
 //   P[x][x'] = sum_c L[c][x] * R[c][x'],  out[d][x] = P[x][x-d] / C  for 0 <= d < D.
 // One workgroup owns a 64-wide x tile of one (b, y) row and a chunk of <=64 disparities.
-// Channels stream through LDS in 16-channel stages (double buffered: the next stage's
-// global loads are issued before the current stage's MFMAs).  Each of the 4 waves owns 16 x
+// Channels stream through LDS in 16-channel stages (double-buffered LDS, two stages of loads in
+// flight in a register ring).  Each of the 4 waves owns 16 x
 // and computes the 16 x (16*NJ) band of P with v_mfma_f32_16x16x4_f32 (exact fp32), so
 // every L / R element is read from HBM once and the FMAs run on the matrix pipe.  The band
 // is transposed through LDS to [d][x] and stored as full 256-B rows.  x' < 0 reads are
 // zero, which produces the x < d zero fill of cost.py:41 for free.
 #include "common.h"
+
+#include <type_traits>
 
 namespace {
 
@@ -42,6 +44,10 @@ struct CorrSmem {
 // neighbouring x tiles overlap by half, and the overlap is then served by the same L2.
 // Loads are 16-byte buffer loads whose range check supplies the zero padding (x < 0, x >= W,
 // c >= C); requires W % 4 == 0 (the launcher falls back to the scalar kernel otherwise).
+// Staging is a two-slot register ring: stage s+2's loads are issued before stage s's MFMAs, so
+// two stages (24 KB per workgroup) are in flight.  L is read once: non-temporal loads; the
+// volume is written once: non-temporal stores (tools/corr_lab.hip: -6 % vs default policy).
+// R keeps the default policy, because the neighbouring tile re-reads half of its window from L2.
 template <int NJ, int VEC>
 __global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
     const float *__restrict__ L, const float *__restrict__ R, float *__restrict__ out, int C,
@@ -75,8 +81,8 @@ __global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
   constexpr int RPT4 = (RQ + NTHREADS - 1) / NTHREADS;
   constexpr int LPT = CC * TX / NTHREADS;    // scalar fallback
   constexpr int RPT = (CC * RW + NTHREADS - 1) / NTHREADS;
-  f32x4 lq[VEC ? 1 : 1], rq[VEC ? RPT4 : 1];
-  float lreg[VEC ? 1 : LPT], rreg[VEC ? 1 : RPT];
+  f32x4 lq[2][1], rq[2][VEC ? RPT4 : 1];
+  float lreg[2][VEC ? 1 : LPT], rreg[2][VEC ? 1 : RPT];
   const int HW4 = (int)(HW * 4);  // VEC requires C*H*W*4 < 2^31 (launcher)
   const int lrow = tid / (TX / 4), lcol = x0 + 4 * (tid % (TX / 4));
   const bool lok = lcol < W;
@@ -92,52 +98,53 @@ __global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
     rbase[i] = (rrow[i] * (int)HW + y * W + x) * 4;
   }
 
-  auto load_stage = [&](int c0) {
+  auto load_stage = [&](int c0, int slot) {
     if (VEC) {
       // per-thread int32 byte offsets (lbase / rbase, hoisted) + the stage's channel offset
       // (scalar); out-of-range elements take the OOB offset, whose load returns 0
       const int coff = c0 * HW4;
-      lq[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-          Lr, (c0 + lrow < C && lok && tid < LQ) ? lbase + coff : img_bytes, 0, 0));
+      lq[slot][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+          Lr, (c0 + lrow < C && lok && tid < LQ) ? lbase + coff : img_bytes, 0, 2 /* nt */));
 #pragma unroll
       for (int i = 0; i < RPT4; ++i)
-        rq[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+        rq[slot][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
             Rr, (c0 + rrow[i] < C && rok[i]) ? rbase[i] + coff : img_bytes, 0, 0));
     } else {
 #pragma unroll
       for (int i = 0; i < LPT; ++i) {
         const int e = tid + i * NTHREADS, row = e / TX, col = e % TX;
         const int c = c0 + row, x = x0 + col;
-        lreg[i] = (c < C && x < W) ? Lrow[(long)c * HW + x] : 0.f;
+        lreg[slot][i] = (c < C && x < W) ? Lrow[(long)c * HW + x] : 0.f;
       }
 #pragma unroll
       for (int i = 0; i < RPT; ++i) {
         const int e = tid + i * NTHREADS, row = e / RW, col = e % RW;
         const int c = c0 + row, x = xr0 + col;
-        rreg[i] = (e < CC * RW && c < C && x >= 0 && x < W) ? Rrow[(long)c * HW + x] : 0.f;
+        rreg[slot][i] = (e < CC * RW && c < C && x >= 0 && x < W) ? Rrow[(long)c * HW + x] : 0.f;
       }
     }
   };
-  auto store_stage = [&](int buf) {
+  auto store_stage = [&](int slot, int buf) {
     float *sL = smem + buf * S::STAGE, *sR = sL + CC * S::LP;
     if (VEC) {
       if (tid < LQ)
-        *reinterpret_cast<f32x4 *>(sL + lrow * S::LP + 4 * (tid % (TX / 4))) = lq[0];
+        *reinterpret_cast<f32x4 *>(sL + lrow * S::LP + 4 * (tid % (TX / 4))) = lq[slot][0];
 #pragma unroll
       for (int i = 0; i < RPT4; ++i) {
         const int e = tid + i * NTHREADS;
-        if (e < RQ) *reinterpret_cast<f32x4 *>(sR + rrow[i] * S::RP + 4 * (e % (RW / 4))) = rq[i];
+        if (e < RQ)
+          *reinterpret_cast<f32x4 *>(sR + rrow[i] * S::RP + 4 * (e % (RW / 4))) = rq[slot][i];
       }
     } else {
 #pragma unroll
       for (int i = 0; i < LPT; ++i) {
         const int e = tid + i * NTHREADS;
-        sL[(e / TX) * S::LP + e % TX] = lreg[i];
+        sL[(e / TX) * S::LP + e % TX] = lreg[slot][i];
       }
 #pragma unroll
       for (int i = 0; i < RPT; ++i) {
         const int e = tid + i * NTHREADS;
-        if (e < CC * RW) sR[(e / RW) * S::RP + e % RW] = rreg[i];
+        if (e < CC * RW) sR[(e / RW) * S::RP + e % RW] = rreg[slot][i];
       }
     }
   };
@@ -146,27 +153,41 @@ __global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
 #pragma unroll
   for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nstages = (C + CC - 1) / CC;
-  load_stage(0);
-  store_stage(0);
-  __syncthreads();
+  // a wave whose 16 x all lie past W (the last tile of a row whose W is not a multiple of 64)
+  // skips its MFMAs; it still stages and meets every barrier
+  const bool active = x0 + 16 * wave < W;
   const int kr = lane >> 4, jj = lane & 15;
-  for (int s = 0; s < nstages; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < nstages) load_stage((s + 1) * CC);
-    const float *sL = smem + buf * S::STAGE, *sR = sL + CC * S::LP;
+  // one stage: issue stage s+2's loads into the ring slot stage s vacated, run stage s's MFMAs
+  // from LDS buffer P (all operands read before the MFMA run), then stage s+1 into buffer 1-P
+  const int nstages = (C + CC - 1) / CC;
+  auto step = [&](auto P_, int s) {
+    constexpr int P = decltype(P_)::value;
+    if (s + 2 < nstages) load_stage((s + 2) * CC, P);
+    if (active) {
+      const float *sL = smem + P * S::STAGE, *sR = sL + CC * S::LP;
+      float a[CC / 4], bv[CC / 4][NJ];
 #pragma unroll
-    for (int ks = 0; ks < CC / 4; ++ks) {
-      const int row = 4 * ks + kr;
-      const float a = sL[row * S::LP + 16 * wave + jj];
+      for (int ks = 0; ks < CC / 4; ++ks) {
+        const int row = 4 * ks + kr;
+        a[ks] = sL[row * S::LP + 16 * wave + jj];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const float bv = sR[row * S::RP + 16 * wave + jj + 16 * (NJ - 1 - j)];
-        acc[j] = mfma16x16x4(a, bv, acc[j]);
+        for (int j = 0; j < NJ; ++j) bv[ks][j] = sR[row * S::RP + 16 * wave + jj + 16 * (NJ - 1 - j)];
       }
+#pragma unroll
+      for (int ks = 0; ks < CC / 4; ++ks)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[j] = mfma16x16x4(a[ks], bv[ks][j], acc[j]);
     }
-    if (s + 1 < nstages) store_stage(buf ^ 1);
+    if (s + 1 < nstages) store_stage(1 - P, 1 - P);
     __syncthreads();
+  };
+  load_stage(0, 0);
+  if (nstages > 1) load_stage(CC, 1);
+  store_stage(0, 0);
+  __syncthreads();
+  for (int s = 0; s < nstages; s += 2) {
+    step(std::integral_constant<int, 0>(), s);
+    if (s + 1 < nstages) step(std::integral_constant<int, 1>(), s + 1);
   }
 
   // Band -> [d][x] tile in LDS.  Lane holds x' column jj, rows i = 4*kr + r (x).
@@ -186,14 +207,17 @@ __global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
       const int dl = e / (TX / 4), xq = e % (TX / 4);
       if (x0 + 4 * xq < W) {
         const float *src = sO + dl * S::OUTP + 4 * xq;
-        *reinterpret_cast<f32x4 *>(out + (((long)b * D + d0 + dl) * H + y) * W + x0 + 4 * xq) =
-            f32x4{src[0], src[1], src[2], src[3]};
+        __builtin_nontemporal_store(
+            f32x4{src[0], src[1], src[2], src[3]},
+            reinterpret_cast<f32x4 *>(out + (((long)b * D + d0 + dl) * H + y) * W + x0 + 4 * xq));
       }
     }
   } else {
     for (int e = tid; e < dmax * TX; e += NTHREADS) {
       const int dl = e / TX, xl = e % TX;
-      if (x0 + xl < W) out[(((long)b * D + d0 + dl) * H + y) * W + x0 + xl] = sO[dl * S::OUTP + xl];
+      if (x0 + xl < W)
+        __builtin_nontemporal_store(sO[dl * S::OUTP + xl],
+                                    out + (((long)b * D + d0 + dl) * H + y) * W + x0 + xl);
     }
   }
 }

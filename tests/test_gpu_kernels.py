@@ -55,7 +55,9 @@ def test_corr_volume_vs_reference_golden(name):
 
 @pytest.mark.parametrize("B,C,H,W,D", [(2, 128, 5, 200, 64), (1, 128, 3, 416, 64), (1, 128, 4, 208, 32),
                                        (2, 128, 3, 104, 16), (1, 32, 3, 130, 192), (1, 7, 2, 65, 24),
-                                       (1, 3, 2, 5, 1), (1, 64, 2, 70, 100)])
+                                       (1, 3, 2, 5, 1), (1, 64, 2, 70, 100),
+                                       # odd stage counts (3, 5 stages) on both load paths
+                                       (1, 48, 2, 96, 40), (1, 40, 2, 66, 30), (2, 80, 2, 136, 64)])
 def test_corr_volume_vs_oracle(B, C, H, W, D):
     rng = np.random.default_rng(B * 1000 + C + D)
     L = rng.standard_normal((B, C, H, W)).astype(np.float32)
