@@ -289,16 +289,19 @@ __global__ __launch_bounds__(256) void corr_volume_bwd_kernel(
 }
 
 // ----------------------------------------------------------------- concat / difference ---
-// Output-indexed, write-bound: out[b][oc][d][y][x]; 4 consecutive x per thread.
-template <bool CONCAT>
+// Output-indexed, write-bound: out[b][oc][d][y][x]; 4 consecutive x per thread.  Index math is
+// 32-bit when the volume has < 2^31 quads (IDX = int; C5 at B=8 is 1.5e8 quads), and the volume
+// is written with non-temporal stores (written once, read once by the 3-D aggregation).
+template <bool CONCAT, typename IDX>
 __global__ __launch_bounds__(256) void shift_volume_kernel(const float *__restrict__ L,
                                                            const float *__restrict__ R,
                                                            float *__restrict__ out, int C, int H,
-                                                           int W, int D, long total4, int W4) {
+                                                           int W, int D, long total4_, int W4) {
   const int OC = CONCAT ? 2 * C : C;
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total4; e += (long)gridDim.x * 256) {
+  const IDX total4 = (IDX)total4_;
+  for (IDX e = (IDX)blockIdx.x * 256 + threadIdx.x; e < total4; e += (IDX)gridDim.x * 256) {
     const int xq = (int)(e % W4);
-    long t = e / W4;
+    IDX t = e / W4;
     const int y = (int)(t % H);
     t /= H;
     const int d = (int)(t % D);
@@ -308,30 +311,87 @@ __global__ __launch_bounds__(256) void shift_volume_kernel(const float *__restri
     const int x = 4 * xq;
     const long HW = (long)H * W;
     float v[4];
+    if (CONCAT && oc < C) {
+      const float *src = L + ((long)b * C + oc) * HW + (long)y * W;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int xx = x + u;
-      float r = 0.f;
-      if (xx < W && xx >= d) {
-        if (CONCAT) {
-          r = oc < C ? L[((long)b * C + oc) * HW + (long)y * W + xx]
-                     : R[((long)b * C + oc - C) * HW + (long)y * W + xx - d];
-        } else {
-          r = L[((long)b * C + oc) * HW + (long)y * W + xx] -
-              R[((long)b * C + oc) * HW + (long)y * W + xx - d];
-        }
+      for (int u = 0; u < 4; ++u) v[u] = (x + u < W && x + u >= d) ? src[x + u] : 0.f;
+    } else {
+      const int c = CONCAT ? oc - C : oc;
+      const float *rs = R + ((long)b * C + c) * HW + (long)y * W - d;
+      const float *ls = L + ((long)b * C + c) * HW + (long)y * W;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int xx = x + u;
+        float r = 0.f;
+        if (xx < W && xx >= d) r = CONCAT ? rs[xx] : ls[xx] - rs[xx];
+        v[u] = r;
       }
-      v[u] = r;
     }
     float *o = out + ((((long)b * OC + oc) * D + d) * H + y) * W + x;
     if ((W & 3) == 0) {
-      *reinterpret_cast<float4 *>(o) = make_float4(v[0], v[1], v[2], v[3]);
+      __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, reinterpret_cast<f32x4 *>(o));
     } else {
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (x + u < W) o[u] = v[u];
     }
   }
+}
+
+// Band form (W % 4 == 0): one workgroup per band of YB consecutive source rows y of one (b, c).
+// The band's left and right rows are read once into LDS, then the workgroup writes all D shifted
+// copies: concat oc = c (left, x >= d) and oc = C + c (right at x - d); difference oc = c.  Each
+// (oc, d) plane receives YB*W contiguous floats (16-byte non-temporal stores): long contiguous
+// write streams run at 5.2 TB/s where one-row (1.2 KB) segments ran at 3.5 TB/s
+// (tools/shift_lab.hip, C5 [4,32,96,312], D=48).  HBM reads are exactly the two feature maps.
+template <bool CONCAT>
+__global__ __launch_bounds__(256) void shift_volume_band_kernel(const float *__restrict__ L,
+                                                                const float *__restrict__ R,
+                                                                float *__restrict__ out, int C,
+                                                                int H, int W, int D, int YB) {
+  extern __shared__ __attribute__((aligned(16))) float srow[];
+  const int tid = threadIdx.x;
+  const int nyb = (H + YB - 1) / YB;
+  const int yb = blockIdx.x % nyb, bc = blockIdx.x / nyb, c = bc % C, b = bc / C;
+  const int y0 = yb * YB, rows = min(YB, H - y0);
+  const int W4 = W >> 2, S4 = rows * W4;
+  float *sL = srow, *sR = srow + YB * W;
+  const f32x4 *gl = reinterpret_cast<const f32x4 *>(L + ((long)bc * H + y0) * W);
+  const f32x4 *gr = reinterpret_cast<const f32x4 *>(R + ((long)bc * H + y0) * W);
+  for (int q = tid; q < S4; q += 256) {
+    reinterpret_cast<f32x4 *>(sL)[q] = __builtin_nontemporal_load(gl + q);
+    reinterpret_cast<f32x4 *>(sR)[q] = __builtin_nontemporal_load(gr + q);
+  }
+  __syncthreads();
+  const int OC = CONCAT ? 2 * C : C;
+  const long HW = (long)H * W;
+  float *o0 = out + (((long)b * OC + c) * D * H + y0) * W;               // oc = c
+  float *o1 = CONCAT ? o0 + (long)C * D * HW : nullptr;                  // oc = C + c
+  for (int e = tid; e < D * S4; e += 256) {
+    const int d = e / S4, r = e - d * S4, yy = r / W4, x = 4 * (r - yy * W4);
+    const float *l = sL + yy * W, *rr = sR + yy * W;
+    f32x4 vl, vr;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = x + u >= d;
+      vl[u] = ok ? l[x + u] : 0.f;
+      vr[u] = ok ? rr[x + u - d] : 0.f;
+    }
+    const long off = (long)d * HW + 4 * r;
+    if (CONCAT) {
+      __builtin_nontemporal_store(vl, reinterpret_cast<f32x4 *>(o0 + off));
+      __builtin_nontemporal_store(vr, reinterpret_cast<f32x4 *>(o1 + off));
+    } else {
+      __builtin_nontemporal_store(vl - vr, reinterpret_cast<f32x4 *>(o0 + off));
+    }
+  }
+}
+
+// rows per band: 8, fewer when the band's two LDS rows would exceed 64 KB
+int band_rows(int w) {
+  int yb = 8;
+  while (yb > 1 && 2L * yb * w * 4 > 64 * 1024) yb >>= 1;
+  return yb;
 }
 
 template <bool CONCAT>
@@ -414,8 +474,17 @@ extern "C" int aanet_concat_volume_f32(const float *left, const float *right, fl
   AANET_HOST_CHECK(left && right && out && n > 0 && c > 0 && h > 0 && w > 0 && max_disp > 0);
   const int W4 = (w + 3) / 4;
   const long total4 = (long)n * 2 * c * max_disp * h * W4;
-  hipLaunchKernelGGL(shift_volume_kernel<true>, dim3(grid_for(total4)), dim3(256), 0,
-                     as_hip(stream), left, right, out, c, h, w, max_disp, total4, W4);
+  if (w % 4 == 0 && 2L * w * 4 <= 64 * 1024 && (long)n * c * h < 0x7fffffffL) {
+    const int yb = band_rows(w);
+    hipLaunchKernelGGL(shift_volume_band_kernel<true>, dim3((unsigned)(n * c * host_div_up(h, yb))),
+                       dim3(256), 2 * yb * w * sizeof(float), as_hip(stream), left, right, out, c,
+                       h, w, max_disp, yb);
+  } else if (total4 < 0x7fffffffL - 8192L * 256)
+    hipLaunchKernelGGL((shift_volume_kernel<true, int>), dim3(grid_for(total4)), dim3(256), 0,
+                       as_hip(stream), left, right, out, c, h, w, max_disp, total4, W4);
+  else
+    hipLaunchKernelGGL((shift_volume_kernel<true, long>), dim3(grid_for(total4)), dim3(256), 0,
+                       as_hip(stream), left, right, out, c, h, w, max_disp, total4, W4);
   return aanet_launch_status();
 }
 
@@ -424,8 +493,17 @@ extern "C" int aanet_diff_volume_f32(const float *left, const float *right, floa
   AANET_HOST_CHECK(left && right && out && n > 0 && c > 0 && h > 0 && w > 0 && max_disp > 0);
   const int W4 = (w + 3) / 4;
   const long total4 = (long)n * c * max_disp * h * W4;
-  hipLaunchKernelGGL(shift_volume_kernel<false>, dim3(grid_for(total4)), dim3(256), 0,
-                     as_hip(stream), left, right, out, c, h, w, max_disp, total4, W4);
+  if (w % 4 == 0 && 2L * w * 4 <= 64 * 1024 && (long)n * c * h < 0x7fffffffL) {
+    const int yb = band_rows(w);
+    hipLaunchKernelGGL(shift_volume_band_kernel<false>, dim3((unsigned)(n * c * host_div_up(h, yb))),
+                       dim3(256), 2 * yb * w * sizeof(float), as_hip(stream), left, right, out, c,
+                       h, w, max_disp, yb);
+  } else if (total4 < 0x7fffffffL - 8192L * 256)
+    hipLaunchKernelGGL((shift_volume_kernel<false, int>), dim3(grid_for(total4)), dim3(256), 0,
+                       as_hip(stream), left, right, out, c, h, w, max_disp, total4, W4);
+  else
+    hipLaunchKernelGGL((shift_volume_kernel<false, long>), dim3(grid_for(total4)), dim3(256), 0,
+                       as_hip(stream), left, right, out, c, h, w, max_disp, total4, W4);
   return aanet_launch_status();
 }
 

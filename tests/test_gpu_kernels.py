@@ -121,6 +121,21 @@ def test_shift_volume_bit_exact_vs_reference_golden(name):
 
 
 @pytest.mark.parametrize("concat", [True, False])
+@pytest.mark.parametrize("B,C,H,W,D", [(2, 3, 4, 40, 7),     # row kernel (W % 4 == 0)
+                                       (1, 5, 3, 41, 9),     # flat kernel (ragged W)
+                                       (1, 2, 2, 12, 20),    # D > W: rows d >= W all zero
+                                       (1, 4, 2, 600, 3),    # W > 256 threads per row
+                                       (2, 2, 19, 24, 5)])   # ragged last band of rows
+def test_shift_volume_paths_bit_exact(concat, B, C, H, W, D):
+    rng = np.random.default_rng(B * 100 + W + D)
+    L = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    R = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    out = t2n(ops.shift_volume(g2t(L), g2t(R), D, concat))
+    ref = (oracle.concat_volume if concat else oracle.diff_volume)(L, R, D)
+    assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("concat", [True, False])
 def test_shift_volume_c5_shape_and_backward(concat):
     """Config C5-like (PSMNet feature [B,32,H/4,W/4], D=48) at reduced H; bit-exact + grads."""
     rng = np.random.default_rng(5)

@@ -27,6 +27,8 @@ up1, up2 = res[:, :, :64, :208].contiguous(), res[:, :, :32, :104].contiguous()
 fl = torch.randn(B, 128, H, W, device=dev, generator=g)
 fr = torch.randn(B, 128, H, W, device=dev, generator=g)
 vol64 = torch.randn(B, 64, H, W, device=dev, generator=g)
+f5l = torch.randn(4, 32, 96, 312, device=dev, generator=g)
+f5r = torch.randn(4, 32, 96, 312, device=dev, generator=g)
 cases = {
     "conv1x1": (lambda: ops.conv2d_fused(x, w1, b, act="relu", packed_weight=p1), 2 * B * H * W * C * C),
     "conv1x1_res": (lambda: ops.conv2d_fused(x, w1, b, act="relu", residual=res, packed_weight=p1),
@@ -56,6 +58,9 @@ cases = {
     "csa_sum": (lambda: ops.csa_sum([x, up1, up2]), 0),
     "corr": (lambda: ops.corr_volume(fl, fr, 64), 0),
     "regress": (lambda: ops.disp_regress(vol64), 0),
+    # C5 (PSMNet 4-D volume, 384x1248 -> 1/4: [B,32,96,312], D=192/4=48), B=4
+    "concat": (lambda: ops.shift_volume(f5l, f5r, 48, True), 0),
+    "diff": (lambda: ops.shift_volume(f5l, f5r, 48, False), 0),
 }
 for name, (fn, flops) in cases.items():
     if names and name not in names:
@@ -70,6 +75,8 @@ for name, (fn, flops) in cases.items():
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / iters
     gbs = {"corr": 4 * (2 * B * 128 * H * W + B * 64 * H * W), "regress": 4 * (B * 64 * H * W + B * H * W),
-           "csa_sum": 4 * (2 * B * C * H * W + B * C * H * W * 5 // 16)}.get(name)
+           "csa_sum": 4 * (2 * B * C * H * W + B * C * H * W * 5 // 16),
+           "concat": 4 * (2 * 4 * 32 * 96 * 312 + 4 * 64 * 48 * 96 * 312),
+           "diff": 4 * (2 * 4 * 32 * 96 * 312 + 4 * 32 * 48 * 96 * 312)}.get(name)
     rate = f"{gbs / ms / 1e6:6.0f} GB/s" if gbs else f"{flops / ms / 1e9:6.1f} TF/s"
     print(f"{name:12s} {ms * 1e3:8.1f} us  {rate}")
