@@ -36,6 +36,7 @@ _SIGNATURES = {
     "aanet_mdcn_bwd_det_f32": [_P] * 10 + [_I] * 12 + [_P, ctypes.c_size_t, _P],
     "aanet_conv2d_fused_f32": [_P] * 6 + [_I, _I, _P] + [_I] * 12 + [_P],
     "aanet_conv_weight_pack_f32": [_P, _P, _I, _I, _I, _I, _P],
+    "aanet_conv_weight_pack_split_f32": [_P, _P, _I, _I, _I, _I, _I, _P],
     "aanet_conv2d_pw_f32": [_P] * 5 + [_I] + [_P] * 3 + [_I, _I, _P] + [_I] * 10 + [_P, _I, _P],
     "aanet_mdcn_pw_f32": [_P, _P, _L, _P, _L, _I, _F, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _P]
     + [_I] * 11 + [_P, _I, _P],
@@ -69,13 +70,15 @@ def lib():
         L.aanet_mdcn_bwd_det_workspace_size.argtypes = [_I] * 12
         L.aanet_mdcn_bwd_det_workspace_size.restype = ctypes.c_size_t
         L.aanet_version.restype = _I
+        L.aanet_conv_weight_pack_split_bytes.argtypes = [_I] * 5
+        L.aanet_conv_weight_pack_split_bytes.restype = _L
         _lib = L
     return _lib
 
 
 def exported_symbols():
-    return (["aanet_version", "aanet_status_string", "aanet_mdcn_bwd_det_workspace_size"]
-            + list(_SIGNATURES))
+    return (["aanet_version", "aanet_status_string", "aanet_mdcn_bwd_det_workspace_size",
+             "aanet_conv_weight_pack_split_bytes"] + list(_SIGNATURES))
 
 
 def call(name, *args):
@@ -97,6 +100,31 @@ def is_nhwc(t):
 
 
 LAYOUT_IN_NHWC, LAYOUT_OUT_NHWC = 1, 2  # AANET_LAYOUT_* (include/aanet_mi355x.h)
+CONV_EXACT_F32 = 8  # AANET_CONV_EXACT_F32: exact f32 MFMA instead of the split-bf16 contraction
+CONV_WEIGHTS_SPLIT = 16  # AANET_CONV_WEIGHTS_SPLIT: weight buffers carry bf16 piece fragments
+
+_exact_f32 = os.environ.get("AANET_EXACT_F32", "0") == "1"
+
+
+def set_exact_f32(on):
+    """Select the conv engine's contraction arithmetic for the fused eval paths: False (default)
+    = split-bf16 pieces with fp32 accumulation where the engine has the configuration (fp32-
+    accurate, include/aanet_mi355x.h AANET_CONV_EXACT_F32); True = exact f32 MFMA everywhere.
+    Returns the previous setting.  Env: AANET_EXACT_F32=1."""
+    global _exact_f32
+    prev, _exact_f32 = _exact_f32, bool(on)
+    return prev
+
+
+def conv_flags(*packed):
+    """Contraction flags for a fused conv call whose packed weight buffers are `packed`: the split
+    contraction when every buffer carries its pieces (ops.pack_weight_split) and exact mode is
+    off, else the exact f32 engine."""
+    if _exact_f32:
+        return CONV_EXACT_F32
+    if packed and all(getattr(w, "_aanet_split", False) for w in packed):
+        return CONV_WEIGHTS_SPLIT
+    return 0
 
 
 class CsaEpilogue(ctypes.Structure):

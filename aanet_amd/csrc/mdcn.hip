@@ -24,6 +24,8 @@ constexpr int PT = 64;     // pixels per workgroup tile
 constexpr int KC = 32;     // max channels per K chunk
 constexpr int CP = PT + 16;  // sCol pitch (floats): rows r, r+1 land 16 banks apart
 
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
 struct MdcnArgs {
   const float *x;
   const float *offset;
@@ -46,6 +48,8 @@ struct MdcnArgs {
   float *out;
   int N, C, H, W, Co, kh, kw, stride, pad, dil, groups, dg, Ho, Wo;
   int layout;  // AANET_LAYOUT_* bits (conv engine only)
+  int split;   // conv engine: split-bf16 contraction (AANET_CONV_EXACT_F32 clear, weights carry pieces)
+  const bf16x8_t *wsplit, *tail_wsplit;  // bf16 piece fragments of weight / tail_w (split_frag_offset)
   // CSA epilogue (tail kernels): csa_out = csa_act(out + sum_j up_r[j](up[j])), r = 2 or 4
   float *csa_out;
   const float *up[3];
@@ -299,6 +303,83 @@ __device__ __forceinline__ void make_samp4(int o[4], f32x4 &wv, float h, float w
   o[3] = ok4 ? ((hl + 1) * W + wl + 1) * rowb : oob;
 }
 
+// ---- split-bf16 contraction (conv engine PREC 1) --------------------------------------------
+// x = h + m + l exactly, three bf16 pieces carrying x's 24 significand bits (weights: round to
+// nearest even, h = bf16(x), m = bf16(x - h), l = x - h - m; activations: truncation, split3).  A product
+// a*b = sum_{i,j} a_i b_j; the six terms down to 2^-16 relative (mm, hl, lh, hm, mh, hh -- small
+// first) run as v_mfma_f32_16x16x32_bf16 with fp32 accumulation.  Every bf16 x bf16 product is
+// exact in fp32 and the three dropped terms (ml, lm, ll) are below 2^-23 |a b|, i.e. under one
+// fp32 rounding of the product: the contraction is fp32-accurate, not a reduced-precision one.
+// Measured on the C2 scale-0 3x3 conv against an fp64 reference (tools/split_lab.hip): max error
+// 8.7e-6 (split) vs 1.0e-5 (exact f32 MFMA fma chain), mean 3.9e-7 vs 4.8e-7; keeping all nine
+// terms changed no output.  bf16 MFMA runs at 16x the f32-MFMA rate, so the six products take
+// 6/16 of the matrix-pipe time of the f32 contraction.
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef bf16x8_t bf16x8;
+
+// Weights for PREC 1 are split once (aanet_conv_weight_pack_split_f32) into MFMA A-operand
+// fragments, streamed from L2 straight into registers: frag(g, t, k, cc, blk, pc, lane) = the 8
+// bf16 of piece pc of rows co = g*Cog + 64t + 16blk + (lane & 15), channels 32cc + 8(lane >> 4)
+// + 0..7 of tap k (zero past the group's Cog).  They follow the f32 packed weights in the same
+// buffer, at a 256-byte aligned offset, so the f32 engine reads the buffer unchanged.
+__host__ __device__ inline long split_frag_offset(int co, int cg, int kk) {
+  return ((long)co * cg * kk * 4 + 255) / 256 * 256;
+}
+__host__ __device__ inline long split_frag_count(int co, int cg, int kk, int groups) {
+  const int cog = co / groups;
+  return (long)groups * ((cog + 63) / 64) * kk * (cg / 32) * 4 * 3 * 64;
+}
+
+// Activations are split by truncation, two values at a time: h = the upper 16 bits of x, r = x - h
+// (exact, <= 16 significant bits), m = the upper 16 bits of r, l = r - m (exact, <= 8 significant
+// bits, so its upper half IS its bf16 value): x = h + m + l exactly.  v_perm_b32 packs two upper
+// halves into one bf16x2 register: 11 VALU ops per two values.
+__device__ __forceinline__ unsigned hi_pair(float a, float b) {  // (bf16 hi(a), bf16 hi(b))
+  return __builtin_amdgcn_perm(__builtin_bit_cast(unsigned, b), __builtin_bit_cast(unsigned, a), 0x07060302u);
+}
+__device__ __forceinline__ float trunc16(float a) {
+  return __builtin_bit_cast(float, __builtin_bit_cast(unsigned, a) & 0xffff0000u);
+}
+__device__ __forceinline__ void split3(f32x4 v, bf16x4 &h, bf16x4 &m, bf16x4 &l) {
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 hh, mm, ll;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float x0 = v[2 * i], x1 = v[2 * i + 1];
+    hh[i] = hi_pair(x0, x1);
+    const float r0 = x0 - trunc16(x0), r1 = x1 - trunc16(x1);
+    mm[i] = hi_pair(r0, r1);
+    ll[i] = hi_pair(r0 - trunc16(r0), r1 - trunc16(r1));
+  }
+  h = __builtin_bit_cast(bf16x4, hh);
+  m = __builtin_bit_cast(bf16x4, mm);
+  l = __builtin_bit_cast(bf16x4, ll);
+}
+
+// Element offset of (row, 16-byte quad q8) in a [rows][32] bf16 piece plane.  Quads are XOR-
+// swizzled by row>>2, so the 16 rows of an MFMA operand read (ds_read_b128, lanes jj = 0..15 at
+// one quad) land on 16 distinct quads of the 256-byte bank row: conflict-free without padding.
+__device__ __forceinline__ int swz(int row, int q8) { return row * 32 + ((q8 ^ ((row >> 2) & 3)) << 3); }
+
+// channels 4*q4 .. 4*q4+3 of one row, as its three pieces (planes `pe` elements apart)
+__device__ __forceinline__ void put_split(__bf16 *plane, int pe, int row, int q4, f32x4 v) {
+  bf16x4 h, m, l;
+  split3(v, h, m, l);
+  const int o = swz(row, q4 >> 1) + ((q4 & 1) << 2);
+  *reinterpret_cast<bf16x4 *>(plane + o) = h;
+  *reinterpret_cast<bf16x4 *>(plane + pe + o) = m;
+  *reinterpret_cast<bf16x4 *>(plane + 2 * pe + o) = l;
+}
+
+__device__ __forceinline__ f32x4 mfma_split6(const bf16x8 (&A)[3], const bf16x8 (&B)[3], f32x4 t) {
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1], B[1], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[2], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[2], B[0], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[1], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1], B[0], t, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[0], t, 0, 0, 0);
+}
+
 // FULL: every chunk holds KC channels (Cg % KC == 0, and cpg % KC == 0 for the DCN), so the
 // staging code has no per-row guards.  Those guards are wave-uniform, and the compiler turns
 // them into scalar branches, which split the loop body and defeat the MFMA/staging interleave.
@@ -309,7 +390,7 @@ __device__ __forceinline__ void make_samp4(int o[4], f32x4 &wv, float h, float w
 // groups: the second MFMA half of a chunk is skipped); 2: 32 channels spanning two 16-channel
 // deformable groups (one sampling state per (pixel, group)).
 template <int MODE, int CO_T, int PTT, int PACKED, int TAIL, int SCHED, int FULL, int LAYOUT,
-          int CFG = 0>
+          int CFG = 0, int PREC = 0>
 __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   constexpr int CK = CFG == 1 ? 16 : 32;   // channels per K chunk
   constexpr int GPC = CFG == 2 ? 2 : 1;    // deformable groups per chunk
@@ -325,7 +406,11 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   constexpr int NIT = INH ? PTT * (CK / 4) / FNT : 1;  // NHWC staging items per thread
   static_assert(!INH || (FULL && NIT >= 1 && FNT % (CK / 4) == 0), "NHWC staging needs full chunks");
   static_assert(!(ONH && TAIL), "NHWC output with a pointwise tail is not instantiated");
-  constexpr int BUF = (PTT + CO_T) * SP; // floats per LDS buffer
+  // PREC 1 (split-bf16 contraction, see split4 / SplitLds): both operand tiles as three bf16
+  // piece planes of 32-channel rows, 64 B per row (XOR-swizzled 16-byte quads, no padding)
+  constexpr bool SPL = PREC == 1;
+  static_assert(!SPL || (CK == 32 && FULL && PACKED && CO_T >= 32), "split-bf16 configuration");
+  constexpr int BUF = SPL ? PTT * 48 : (PTT + CO_T) * SP; // floats per LDS buffer
   constexpr int OP = PTT + 4;            // epilogue tile pitch
   static_assert(CO_T * OP <= 2 * BUF, "epilogue tile must fit the staging buffers");
   // DCN: the sampling state of a (pixel, tap, deformable group) is computed once, by the threads
@@ -405,6 +490,20 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     wlane[i] = PACKED ? (co * Cg + cl) * 4 : (co * Cg * K + cl * K) * 4;
   }
   const int pl4 = (int)psafe * 4;
+  // PREC 1: the wave's A fragments (its NCB 16-row blocks x 3 pieces) come from the pre-split
+  // weight fragments in global memory (L2-resident), loaded one chunk ahead of their MFMAs
+  bf16x8 fa[SPL ? NCB : 1][3];
+  const int sT = (Cog + 63) / 64, sNCC = Cg / 32;
+  const int st64 = (cot * CO_T) / 64, sbb = ((cot * CO_T) % 64) / 16 + wc0;
+  auto load_a = [&](const bf16x8 *frag, long tile_base) {
+#pragma unroll
+    for (int m = 0; m < NCB; ++m)
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc) fa[m][pc] = frag[((tile_base + sbb + m) * 3 + pc) * 64 + lane];
+  };
+  auto load_a_chunk = [&](const ChunkIt<CK> &c) {
+    load_a(a.wsplit, ((((long)gc * sT + st64) * K + c.k) * sNCC + ((c.c0 - cbeg) >> 5)) * 4);
+  };
 
   auto load_params_raw = [&](const ChunkIt<CK> &c) {
     const int g = c.c0 / cpg + pgi;
@@ -468,9 +567,11 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     const int rows = c.c1 - c.c0;
     const int wbase = PACKED ? (((c.k * a.Co + co0) * Cg + (c.c0 - cbeg)) * 4)
                              : (((co0 * Cg + (c.c0 - cbeg)) * K + c.k) * 4);
+    if constexpr (!SPL) {
 #pragma unroll
-    for (int i = 0; i < WPT; ++i)
-      wreg[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, wlane[i], wbase, 0));
+      for (int i = 0; i < WPT; ++i)
+        wreg[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, wlane[i], wbase, 0));
+    }
     if constexpr (INH) {
       const int soff = __builtin_amdgcn_readfirstlane(c.c0 * 4);
       if (MODE == 0) {
@@ -516,11 +617,14 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   };
   auto store_stage = [&](const ChunkIt<CK> &c, int buf) {
     float *sC = smem + buf * BUF, *sW = sC + PTT * SP;
+    __bf16 *sB = reinterpret_cast<__bf16 *>(smem + buf * BUF);
     const int rows = c.c1 - c.c0;
+    if constexpr (!SPL) {
 #pragma unroll
-    for (int i = 0; i < WPT; ++i) {
-      const int e = tid + FNT * i;
-      sW[(e / CK) * SP + e % CK] = wreg[i];
+      for (int i = 0; i < WPT; ++i) {
+        const int e = tid + FNT * i;
+        sW[(e / CK) * SP + e % CK] = wreg[i];
+      }
     }
     if constexpr (INH) {
 #pragma unroll
@@ -534,7 +638,10 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
           v = __builtin_elementwise_fma(nc[i][2], f32x4(nw[i][2]), v);
           v = __builtin_elementwise_fma(nc[i][3], f32x4(nw[i][3]), v);
         }
-        *reinterpret_cast<f32x4 *>(sC + npx[i] * SP + 4 * nq) = v;
+        if constexpr (SPL)
+          put_split(sB, PTT * 32, npx[i], nq, v);
+        else
+          *reinterpret_cast<f32x4 *>(sC + npx[i] * SP + 4 * nq) = v;
       }
       return;
     }
@@ -552,9 +659,13 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       }
     }
 #pragma unroll
-    for (int q = 0; q < CPT / 4; ++q)
-      *reinterpret_cast<f32x4 *>(sC + spx * SP + scb + 4 * q) =
-          f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+    for (int q = 0; q < CPT / 4; ++q) {
+      const f32x4 vq = f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+      if constexpr (SPL)
+        put_split(sB, PTT * 32, spx, scb / 4 + q, vq);
+      else
+        *reinterpret_cast<f32x4 *>(sC + spx * SP + scb + 4 * q) = vq;
+    }
   };
 
   f32x4 acc[NCB][NPB];
@@ -576,6 +687,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     get_params(0);
   }
   issue_loads(cur);
+  if constexpr (SPL) load_a_chunk(cur);
   store_stage(cur, 0);
   nxt = cur;
   nxt.advance(K, cend, cpg, CUT);
@@ -614,9 +726,27 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     read_frag(buf, h, f);
     mma(f);
   };
+  // PREC 1: the whole 32-channel chunk is one K step of v_mfma_f32_16x16x32_bf16 per piece pair.
+  // A: the fragments in fa; B: read one 16-pixel block at a time (12 VGPRs live, not 24).
+  auto mma_s = [&](int buf) {
+    const __bf16 *sB = reinterpret_cast<const __bf16 *>(smem + buf * BUF);
+#pragma unroll
+    for (int b = 0; b < NPB; ++b) {
+      bf16x8 fb[3];
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc)
+        fb[pc] = *reinterpret_cast<const bf16x8 *>(sB + pc * PTT * 32 + swz(16 * (wp0 + b) + jj, kr));
+#pragma unroll
+      for (int m = 0; m < NCB; ++m) acc[m][b] = mfma_split6(fa[m], fb, acc[m][b]);
+    }
+  };
   auto mfma_chunk = [&](int buf) {
-    mfma_half(buf, 0);
-    mfma_half(buf, 1);
+    if constexpr (SPL) {
+      mma_s(buf);
+    } else {
+      mfma_half(buf, 0);
+      mfma_half(buf, 1);
+    }
   };
 
   for (int buf = 0;; buf ^= 1) {
@@ -628,7 +758,38 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       issue_loads(nxt);
     }
     if (MODE && has_nn && pwave) load_params_raw(nn);
-    if (SCHED) {
+    if (SPL && SCHED && MODE == 0) {
+      // all B fragments of chunk c first; then chunk c+1's staging (split, LDS writes) is
+      // interleaved with chunk c's bf16 MFMAs.  (The DCN variants keep the sequential order: the
+      // extra 12 live VGPRs of this form spill them past the 128-VGPR cap.)
+      const __bf16 *sB = reinterpret_cast<const __bf16 *>(smem + buf * BUF);
+      bf16x8 fb[NPB][3];
+#pragma unroll
+      for (int b = 0; b < NPB; ++b)
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc)
+          fb[b][pc] = *reinterpret_cast<const bf16x8 *>(sB + pc * PTT * 32 + swz(16 * (wp0 + b) + jj, kr));
+      if (has_next) store_stage(nxt, buf ^ 1);
+#pragma unroll
+      for (int b = 0; b < NPB; ++b)
+#pragma unroll
+        for (int m = 0; m < NCB; ++m) acc[m][b] = mfma_split6(fa[m], fb[b], acc[m][b]);
+      if (has_next) {
+#pragma unroll
+        for (int i = 0; i < 6 * NCB * NPB; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
+          if (i % 3 == 0) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS_WRITE
+        }
+      }
+      if (!has_next) break;
+      load_a_chunk(nxt);
+    } else if (SPL) {
+      mma_s(buf);
+      if (!has_next) break;
+      load_a_chunk(nxt);
+      store_stage(nxt, buf ^ 1);
+    } else if (SCHED) {
       // chunk c+1's staging math + LDS writes are interleaved with the second half of chunk c's
       // MFMAs (different LDS buffers), so each wave keeps its matrix pipe busy by itself.
       // The half-1 operands are read before the staging writes: LDS reads and writes of the two
@@ -688,13 +849,17 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
           }
           v[r] = t;
         }
-        *reinterpret_cast<f32x4 *>(sC + (16 * (wp0 + b) + jj) * SP + 16 * (mg & 1) + 4 * kr) = v;
+        if constexpr (SPL)
+          put_split(reinterpret_cast<__bf16 *>(sC), PTT * 32, 16 * (wp0 + b) + jj, 4 * (mg & 1) + kr, v);
+        else
+          *reinterpret_cast<f32x4 *>(sC + (16 * (wp0 + b) + jj) * SP + 16 * (mg & 1) + 4 * kr) = v;
         acc[m][b] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
     constexpr int NH = (CO_T + 31) / 32;  // channel chunks of the pointwise GEMM
 #pragma unroll
     for (int h2 = 0; h2 < NH; ++h2) {
+      if constexpr (SPL) continue;  // tail weights: pre-split fragments (tail_wsplit)
       float *sW = smem + h2 * BUF + PTT * SP;
       for (int e = tid; e < KC * CO_T; e += FNT) {
         const int co2 = e / KC, cl = e % KC, c = 32 * h2 + cl;
@@ -707,7 +872,10 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     }
     __syncthreads();
 #pragma unroll
-    for (int h2 = 0; h2 < NH; ++h2) mfma_chunk(h2);
+    for (int h2 = 0; h2 < NH; ++h2) {
+      if constexpr (SPL) load_a(a.tail_wsplit, (long)h2 * 4);
+      mfma_chunk(h2);
+    }
   }
 
   // Epilogue: accumulators -> LDS [co][px] -> 16-byte row segments (+ residual) -> HBM.
@@ -1156,6 +1324,7 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
   a.groups = groups;
   a.dg = dg;
   a.layout = 0;
+  a.split = 0;
   a.csa_out = nullptr;
   a.num_up = 0;
   a.csa_act = 0;
@@ -1174,6 +1343,40 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
 template <int MODE, int CO_T, int PTT, int FULL, int CFG>
 void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
   const dim3 blk(FNT);
+  if constexpr (FULL && CFG == 0 && CO_T >= 32) {  // split-bf16 contraction (PREC 1)
+    static const int nosched = [] { const char *e = getenv("AANET_SPLIT_NOSCHED"); return e ? atoi(e) : 0; }();
+    if (a.split && packed && nosched) {  // A/B switch: staging after the MFMAs, not interleaved
+      if (a.tail_w) {
+        if (a.layout == 1)
+          hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 0, 1, 1, CFG, 1>), grid, blk, 0, st, a);
+        else
+          hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 0, 1, 0, CFG, 1>), grid, blk, 0, st, a);
+      } else if (a.layout == 1) {
+        hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 0, 1, 1, CFG, 1>), grid, blk, 0, st, a);
+      } else if (a.layout == 2) {
+        hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 0, 1, 2, CFG, 1>), grid, blk, 0, st, a);
+      } else {
+        hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 0, 1, 0, CFG, 1>), grid, blk, 0, st, a);
+      }
+      return;
+    }
+    if (a.split && packed) {
+      if (a.tail_w) {
+        if (a.layout == 1)
+          hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1, 1, 1, CFG, 1>), grid, blk, 0, st, a);
+        else
+          hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1, 1, 0, CFG, 1>), grid, blk, 0, st, a);
+        return;
+      }
+      switch (a.layout) {
+        case 1: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, 1, 1, CFG, 1>), grid, blk, 0, st, a); break;
+        case 2: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, 1, 2, CFG, 1>), grid, blk, 0, st, a); break;
+        case 3: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, 1, 3, CFG, 1>), grid, blk, 0, st, a); break;
+        default: hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 1, 1, 0, CFG, 1>), grid, blk, 0, st, a); break;
+      }
+      return;
+    }
+  }
   if (a.tail_w) {
     if (FULL && a.layout == 1)
       hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1, FULL, FULL ? 1 : 0, CFG>), grid, blk, 0, st, a);
@@ -1326,6 +1529,56 @@ __global__ void pack_weight_kernel(const float *__restrict__ w, float *__restric
   }
 }
 
+// PREC 1 needs weight buffers from aanet_conv_weight_pack_split_f32 (AANET_CONV_WEIGHTS_SPLIT)
+// and the split arithmetic selected (AANET_CONV_EXACT_F32 clear); a tail kernel's pointwise
+// weights then carry their fragments too.
+void set_split(MdcnArgs &a, int flags, int packed) {
+  a.split = packed && (flags & AANET_CONV_WEIGHTS_SPLIT) && !(flags & AANET_CONV_EXACT_F32);
+  if (!a.split) return;
+  const int cg = a.C / a.groups, kk = a.kh * a.kw;
+  a.wsplit = reinterpret_cast<const bf16x8_t *>(reinterpret_cast<const char *>(a.weight) +
+                                                split_frag_offset(a.Co, cg, kk));
+  if (a.tail_w)
+    a.tail_wsplit = reinterpret_cast<const bf16x8_t *>(reinterpret_cast<const char *>(a.tail_w) +
+                                                       split_frag_offset(a.Co2, a.Co, 1));
+}
+
+// one thread per (g, t, k, cc, blk, lane): 8 weights -> their three bf16 pieces
+__global__ void pack_split_kernel(const float *__restrict__ w, bf16x8_t *__restrict__ frag, int Co,
+                                  int Cg, int K, int groups) {
+  const int Cog = Co / groups, T = (Cog + 63) / 64, NCC = Cg / 32;
+  const long total = (long)groups * T * K * NCC * 4 * 64;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int lane = (int)(e & 63);
+    long r = e >> 6;
+    const int blk = (int)(r & 3);
+    r >>= 2;
+    const int cc = (int)(r % NCC);
+    r /= NCC;
+    const int k = (int)(r % K);
+    r /= K;
+    const int t = (int)(r % T), g = (int)(r / T);
+    const int row = 64 * t + 16 * blk + (lane & 15);
+    const int co = g * Cog + row;
+    bf16x8_t ph, pm, pl;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = 32 * cc + 8 * (lane >> 4) + j;
+      const float v = row < Cog ? w[((long)co * Cg + c) * K + k] : 0.f;
+      const __bf16 h = (__bf16)v;
+      const float r1 = v - (float)h;
+      const __bf16 m = (__bf16)r1;
+      ph[j] = h;
+      pm[j] = m;
+      pl[j] = (__bf16)(r1 - (float)m);
+    }
+    const long o = (((((long)g * T + t) * K + k) * NCC + cc) * 4 + blk) * 3 * 64 + lane;
+    frag[o] = ph;
+    frag[o + 64] = pm;
+    frag[o + 128] = pl;
+  }
+}
+
 int set_csa(MdcnArgs &a, const aanet_csa_epilogue_t *csa) {
   if (!csa) return AANET_OK;
   if (!csa->out || csa->num_up < 0 || csa->num_up > 3 || csa->act < 0 || csa->act > 2)
@@ -1370,7 +1623,8 @@ extern "C" int aanet_conv2d_fused_f32(const float *x, const float *weight, const
   MdcnArgs a = make_args(x, nullptr, 0, nullptr, 0, 0, 1.f, weight, bias, post_scale, post_shift,
                          act, out, n, c, h, w, co, kh, kw, stride, pad, dil, groups, 1);
   a.residual = residual;
-  a.layout = layout;
+  set_split(a, layout, weight_packed);
+  a.layout = layout & ~(AANET_CONV_EXACT_F32 | AANET_CONV_WEIGHTS_SPLIT);
   return launch_fwd<0>(a, weight_packed, as_hip(stream));
 }
 
@@ -1382,6 +1636,8 @@ extern "C" int aanet_conv2d_pw_f32(const float *x, const float *weight_packed, c
                                    int pad, int dil, const aanet_csa_epilogue_t *csa, int layout,
                                    aanet_stream_t stream) {
   if (act < 0 || act > 2 || pw_act < 0 || pw_act > 2 || !pw_weight_packed) return AANET_EINVAL;
+  const int flags = layout;
+  layout &= ~(AANET_CONV_EXACT_F32 | AANET_CONV_WEIGHTS_SPLIT);
   if (layout != 0 && layout != 1) return AANET_EINVAL;
   MdcnArgs a = make_args(x, nullptr, 0, nullptr, 0, 0, 1.f, weight_packed, bias, post_scale,
                          post_shift, act, out, n, c, h, w, co, kh, kw, stride, pad, dil, 1, 1);
@@ -1393,6 +1649,7 @@ extern "C" int aanet_conv2d_pw_f32(const float *x, const float *weight_packed, c
   a.tail_act = pw_act;
   a.Co2 = co2;
   a.residual = residual;
+  set_split(a, flags, 1);
   return launch_fwd<0>(a, 1, as_hip(stream));
 }
 
@@ -1406,6 +1663,8 @@ extern "C" int aanet_mdcn_pw_f32(const float *x, const float *offset, long offse
                                  int dil, int dg, const aanet_csa_epilogue_t *csa, int layout,
                                  aanet_stream_t stream) {
   if (act < 0 || act > 2 || pw_act < 0 || pw_act > 2 || !pw_weight_packed) return AANET_EINVAL;
+  const int flags = layout;
+  layout &= ~(AANET_CONV_EXACT_F32 | AANET_CONV_WEIGHTS_SPLIT);
   if (layout != 0 && layout != 1) return AANET_EINVAL;
   MdcnArgs a = make_args(x, offset, offset_batch_stride, mask, mask_batch_stride, mask_logits,
                          mask_scale, weight_packed, bias, post_scale, post_shift, act, out, n, c,
@@ -1418,6 +1677,7 @@ extern "C" int aanet_mdcn_pw_f32(const float *x, const float *offset, long offse
   a.tail_act = pw_act;
   a.Co2 = co2;
   a.residual = residual;
+  set_split(a, flags, 1);
   return launch_fwd<1>(a, 1, as_hip(stream));
 }
 
@@ -1433,7 +1693,8 @@ extern "C" int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset,
   MdcnArgs a = make_args(x, offset, offset_batch_stride, mask, mask_batch_stride, mask_logits,
                          mask_scale, weight, bias, post_scale, post_shift, act, out, n, c, h, w,
                          co, kh, kw, stride, pad, dil, groups, dg);
-  a.layout = layout;
+  set_split(a, layout, weight_packed);
+  a.layout = layout & ~(AANET_CONV_EXACT_F32 | AANET_CONV_WEIGHTS_SPLIT);
   return launch_fwd<1>(a, weight_packed, as_hip(stream));
 }
 
@@ -1443,6 +1704,27 @@ extern "C" int aanet_conv_weight_pack_f32(const float *weight, float *weight_pac
   const long total = (long)co * cg * kh * kw;
   hipLaunchKernelGGL(pack_weight_kernel, dim3(host_div_up(total, 256) > 4096 ? 4096 : host_div_up(total, 256)),
                      dim3(256), 0, as_hip(stream), weight, weight_packed, co, cg, kh * kw);
+  return aanet_launch_status();
+}
+
+extern "C" long aanet_conv_weight_pack_split_bytes(int co, int cg, int kh, int kw, int groups) {
+  if (co <= 0 || cg <= 0 || kh <= 0 || kw <= 0 || groups <= 0 || co % groups || cg % 32) return 0;
+  return split_frag_offset(co, cg, kh * kw) + split_frag_count(co, cg, kh * kw, groups) * 16;
+}
+
+extern "C" int aanet_conv_weight_pack_split_f32(const float *weight, void *out, int co, int cg,
+                                                int kh, int kw, int groups,
+                                                aanet_stream_t stream) {
+  AANET_HOST_CHECK(weight && out);
+  if (aanet_conv_weight_pack_split_bytes(co, cg, kh, kw, groups) == 0) return AANET_EUNSUPPORTED;
+  const int rc = aanet_conv_weight_pack_f32(weight, static_cast<float *>(out), co, cg, kh, kw, stream);
+  if (rc) return rc;
+  const int kk = kh * kw;
+  const long n = split_frag_count(co, cg, kk, groups) / 3;
+  hipLaunchKernelGGL(pack_split_kernel, dim3(host_div_up(n, 256) > 4096 ? 4096 : host_div_up(n, 256)),
+                     dim3(256), 0, as_hip(stream), weight,
+                     reinterpret_cast<bf16x8_t *>(static_cast<char *>(out) + split_frag_offset(co, cg, kk)),
+                     co, cg, kk, groups);
   return aanet_launch_status();
 }
 

@@ -24,7 +24,8 @@ def _key(*tensors):
 
 def folded(conv, bn):
     """(weight, bias, packed weight) of conv followed by eval BN (bn may be None), cached on the
-    conv module; the packed copy is the [kh][kw][co][cg] layout the HIP engine streams."""
+    conv module; the packed copy is the [kh][kw][co][cg] layout the HIP engine streams, carrying
+    the split-bf16 fragments too when cg % 32 == 0 (ops.pack_weight_split)."""
     tensors = (conv.weight, conv.bias) + ((bn.weight, bn.bias, bn.running_mean, bn.running_var)
                                           if bn is not None else ())
     key = _key(*tensors)
@@ -40,7 +41,11 @@ def folded(conv, bn):
             w = (conv.weight * scale.view(-1, 1, 1, 1)).contiguous()
             b = shift if conv.bias is None else conv.bias * scale + shift
             b = b.contiguous()
-    wp = ops.pack_weight(w) if w.is_cuda else None
+    wp = None
+    if w.is_cuda:  # split-bf16 engine buffer where the shape has one, else plain packed f32
+        wp = ops.pack_weight_split(w, getattr(conv, "groups", 1))
+        if wp is None:
+            wp = ops.pack_weight(w)
     conv._aanet_fold = (key, w, b, wp)
     return w, b, wp
 

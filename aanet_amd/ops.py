@@ -180,7 +180,7 @@ def mdcn_forward_fused(x, offset_mask, weight, bias=None, post_scale=None, post_
     N, C, H, W = x.shape
     Co, _, kh, kw = weight.shape
     K = kh * kw
-    layout = _lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0
+    layout = (_lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0) | _lib.conv_flags(packed_weight)
     Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
     if offset_mask.shape != (N, deformable_groups * 3 * K, Ho, Wo):
         raise ValueError(f"offset_mask shape {tuple(offset_mask.shape)} unexpected")
@@ -208,6 +208,25 @@ def pack_weight(weight):
     return out
 
 
+def pack_weight_split(weight, groups=1):
+    """Weight buffer of the split-bf16 contraction (aanet_conv_weight_pack_split_f32): the
+    pack_weight layout, followed in the same allocation by the bf16 piece fragments.  Returned as
+    the [kh][kw][co][cg] float view of its head (so it is also a valid pack_weight result) and
+    tagged ``_aanet_split``; None when the shape has no split form (cg % 32 != 0)."""
+    require_gpu(weight, names=("weight",))
+    Co, Cg, kh, kw = weight.shape
+    nbytes = _lib.lib().aanet_conv_weight_pack_split_bytes(Co, Cg, kh, kw, groups)
+    if nbytes <= 0:
+        return None
+    buf = torch.empty(nbytes // 4, device=weight.device, dtype=torch.float32)
+    call("aanet_conv_weight_pack_split_f32", ptr(weight.contiguous()), ptr(buf), Co, Cg, kh, kw,
+         groups, stream_of(weight))
+    wp = buf[: Co * Cg * kh * kw].view(kh, kw, Co, Cg)
+    wp._aanet_split = True
+    wp._aanet_buf = buf
+    return wp
+
+
 def conv2d_fused(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None,
                  residual=None, post_scale=None, post_shift=None, packed_weight=None,
                  out_nhwc=False):
@@ -224,7 +243,8 @@ def conv2d_fused(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1
     Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
     if residual is not None and tuple(residual.shape) != (N, Co, Ho, Wo):
         raise ValueError("residual shape must match the output")
-    layout = (_lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0) | (_lib.LAYOUT_OUT_NHWC if out_nhwc else 0)
+    layout = ((_lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0) | (_lib.LAYOUT_OUT_NHWC if out_nhwc else 0)
+              | _lib.conv_flags(packed_weight))
     if residual is not None and out_nhwc and not (_lib.is_nhwc(residual) or Co == 1):
         raise ValueError("residual must be channels_last when out_nhwc=True")
     out = torch.empty((N, Co, Ho, Wo), device=x.device, dtype=x.dtype,
@@ -275,7 +295,8 @@ def conv2d_pw(x, weight, packed_weight, bias, post_scale, post_shift, act, pw_pa
          ptr(post_shift), ACT[act], ptr(pw_packed), ptr(pw_bias), ptr(residual), ACT[pw_act], Co2,
          ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation,
          None if desc is None else _lib.ctypes.byref(desc),
-         _lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0, stream_of(x))
+         (_lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0) | _lib.conv_flags(packed_weight, pw_packed),
+         stream_of(x))
     return out if desc is None else (out, csa_out)
 
 
@@ -302,7 +323,8 @@ def mdcn_pw(x, offset_mask, weight, packed_weight, bias, post_scale, post_shift,
          ACT[act], ptr(pw_packed), ptr(pw_bias), ptr(residual), ACT[pw_act], Co2, ptr(out), N, C,
          H, W, Co, kh, kw, stride, padding, dilation, deformable_groups,
          None if desc is None else _lib.ctypes.byref(desc),
-         _lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0, stream_of(x))
+         (_lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0) | _lib.conv_flags(packed_weight, pw_packed),
+         stream_of(x))
     return out if desc is None else (out, csa_out)
 
 

@@ -34,7 +34,19 @@ enum {
 enum {
   AANET_LAYOUT_NCHW = 0,
   AANET_LAYOUT_IN_NHWC = 1,  /* x is [n][h][w][c] */
-  AANET_LAYOUT_OUT_NHWC = 2  /* out (and residual) are [n][ho][wo][co] */
+  AANET_LAYOUT_OUT_NHWC = 2, /* out (and residual) are [n][ho][wo][co] */
+  /* Contraction arithmetic flag, OR-ed into `layout`.  Clear (default): where the engine has the
+   * configuration (packed weights, 32-channel chunks, >= 32 output channels per group) the
+   * 3x3/1x1/deformable contraction runs on the bf16 matrix cores with every fp32 operand split
+   * into three bf16 pieces and fp32 accumulation (six piece products; the dropped ones are below
+   * 2^-23 of each product), fp32-accurate: against an fp64 reference its error is no larger than
+   * the exact f32 MFMA chain's (mdcn.hip, split3).  Set: exact f32 MFMA (v_mfma_f32_16x16x4_f32,
+   * bitwise an fp32 fma chain) everywhere. */
+  AANET_CONV_EXACT_F32 = 8,
+  /* The weight buffers (weight_packed, and pw_weight_packed of the tail kernels) come from
+   * aanet_conv_weight_pack_split_f32: the f32 packed weights followed by their bf16 piece
+   * fragments.  Without it the engine runs the exact f32 contraction. */
+  AANET_CONV_WEIGHTS_SPLIT = 16
 };
 
 int aanet_version(void);
@@ -183,6 +195,15 @@ int aanet_mdcn_pw_f32(const float *x, const float *offset, long offset_batch_str
  * weight version by the caller (the eval path caches it with the folded BN). */
 int aanet_conv_weight_pack_f32(const float *weight, float *weight_packed, int co, int cg, int kh,
                                int kw, aanet_stream_t stream);
+
+/* Weight buffer for the split-bf16 contraction (AANET_CONV_WEIGHTS_SPLIT): the
+ * aanet_conv_weight_pack_f32 layout, then (at a 256-byte aligned offset) every weight split into
+ * three bf16 pieces and laid out as MFMA operand fragments (mdcn.hip, split_frag_offset).
+ * weight is the reference layout [co][cg][kh][kw] of a conv with `groups` groups; needs
+ * cg % 32 == 0.  _bytes returns the buffer size, 0 when unsupported. */
+long aanet_conv_weight_pack_split_bytes(int co, int cg, int kh, int kw, int groups);
+int aanet_conv_weight_pack_split_f32(const float *weight, void *out, int co, int cg, int kh, int kw,
+                                     int groups, aanet_stream_t stream);
 
 /* Cross-scale fusion sum (nets/aggregation.py:387-400): out[n,c,h,w] =
  * act(sum_j resize(inputs[j])), j in input order; inputs whose (in_h, in_w) differ from

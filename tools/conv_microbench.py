@@ -20,7 +20,9 @@ w3 = torch.randn(C, C, 3, 3, device=dev, generator=g) * 0.04
 wo = torch.randn(54, 32, 3, 3, device=dev, generator=g) * 0.01
 bo = torch.randn(54, device=dev, generator=g)
 b = torch.randn(C, device=dev, generator=g)
-p1, p3, po = ops.pack_weight(w1), ops.pack_weight(w3), ops.pack_weight(wo)
+p1, p3, po = ops.pack_weight_split(w1), ops.pack_weight_split(w3), ops.pack_weight_split(wo, 2)
+if os.environ.get("AANET_PACK_F32") == "1":  # plain f32 packed weights (exact engine only)
+    p1, p3, po = ops.pack_weight(w1), ops.pack_weight(w3), ops.pack_weight(wo)
 om = ops.conv2d_fused(x, wo, bo, 1, 2, 2, 2, packed_weight=po)
 xn = x.contiguous(memory_format=torch.channels_last)
 up1, up2 = res[:, :, :64, :208].contiguous(), res[:, :, :32, :104].contiguous()
