@@ -27,7 +27,7 @@ CONV_CASES = [
 
 @pytest.mark.parametrize("case", CONV_CASES)
 @pytest.mark.parametrize("epi", ["plain", "bias_relu", "bn_leaky_res"])
-@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("packed", [False, True, "split"])
 def test_conv2d_fused_vs_torch_cpu(case, epi, packed):
     N, C, H, W, Co, k, s, p, d, g = case
     gen = torch.Generator().manual_seed(hash(case) % 1000)
@@ -49,9 +49,20 @@ def test_conv2d_fused_vs_torch_cpu(case, epi, packed):
                            act, None if res is None else res.to(DEV),
                            sc.to(DEV) if epi == "bn_leaky_res" else None,
                            sh.to(DEV) if epi == "bn_leaky_res" else None,
-                           packed_weight=ops.pack_weight(wd) if packed else None).cpu()
+                           packed_weight=_packed(wd, g, packed)).cpu()
     err = (got - ref).abs().max().item()
     assert err <= 2e-5 * (1 + ref.abs().max().item()), err
+
+
+def _packed(wd, groups, packed):
+    """None (reference layout), pack_weight (exact f32 engine) or the split-bf16 buffer (falls
+    back to pack_weight where the shape has no split form)."""
+    if not packed:
+        return None
+    if packed == "split":
+        ws = ops.pack_weight_split(wd, groups)
+        return ws if ws is not None else ops.pack_weight(wd)
+    return ops.pack_weight(wd)
 
 
 @pytest.mark.parametrize("sizes", [[(24, 48), (12, 24), (6, 12)], [(8, 20), (4, 10), (2, 5)], [(4, 8), (1, 2)], [(12, 24), (24, 48), (6, 12)],

@@ -1,0 +1,152 @@
+"""The conv engine's split-bf16 contraction (include/aanet_mi355x.h AANET_CONV_EXACT_F32 /
+AANET_CONV_WEIGHTS_SPLIT; aanet_amd/csrc/mdcn.hip split3).  Every fp32 operand is carried as
+three bf16 pieces and six piece products are accumulated in fp32; the claim is fp32 accuracy.
+These tests hold it to that: against an fp64 reference (torch double conv2d / the oracle's fp64
+DCN) the split path's error may not exceed the exact f32 MFMA engine's by more than a small
+factor, and its pieces must reconstruct the weights exactly."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from aanet_amd import _lib, ops
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+class exact_f32:
+    def __enter__(self):
+        self.prev = _lib.set_exact_f32(True)
+
+    def __exit__(self, *a):
+        _lib.set_exact_f32(self.prev)
+
+
+def _errs(got, ref64, scale64):
+    e = (got.double() - ref64).abs()
+    return e.max().item(), e.mean().item(), (e / (scale64 + 1e-30)).max().item()
+
+
+@pytest.mark.parametrize("case", [
+    # N, C, H, W, Co, k, stride, pad, dil, groups, nhwc
+    (2, 64, 24, 52, 64, 3, 1, 1, 1, 1, True),     # SimpleBottleneck conv2 (NHWC staging)
+    (2, 64, 24, 52, 64, 3, 1, 1, 1, 1, False),    # same, NCHW staging
+    (2, 64, 24, 52, 54, 3, 1, 2, 2, 2, True),     # offset_conv: grouped, dilated, Cog = 27
+    (2, 64, 24, 52, 64, 1, 1, 0, 1, 1, False),    # conv1 / conv3
+    (2, 64, 24, 52, 32, 3, 2, 1, 1, 1, False),    # CSA strided 3x3
+    (1, 128, 12, 40, 96, 3, 1, 1, 1, 1, False),   # Co > 64: two output tiles
+])
+def test_split_conv_accuracy_vs_fp64(case):
+    N, C, H, W, Co, k, s, p, d, g, nhwc = case
+    gen = torch.Generator().manual_seed(7)
+    x = torch.randn(N, C, H, W, generator=gen) * 3
+    w = torch.randn(Co, C // g, k, k, generator=gen) / (C // g * k * k) ** 0.5
+    ref = F.conv2d(x.double(), w.double(), None, s, p, d, g)
+    scale = F.conv2d(x.double().abs(), w.double().abs(), None, s, p, d, g)
+    xd, wd = x.to(DEV), w.to(DEV)
+    if nhwc:
+        xd = xd.contiguous(memory_format=torch.channels_last)
+    wsplit = ops.pack_weight_split(wd, g)
+    assert wsplit is not None and wsplit._aanet_split
+    got_s = ops.conv2d_fused(xd, wd, None, s, p, d, g, packed_weight=wsplit).cpu()
+    with exact_f32():
+        got_e = ops.conv2d_fused(xd, wd, None, s, p, d, g, packed_weight=wsplit).cpu()
+    es, ee = _errs(got_s, ref, scale), _errs(got_e, ref, scale)
+    assert not torch.equal(got_s, got_e), "split and exact paths are not distinct launches"
+    # fp32-accurate: max and mean error within 1.5x / 1.25x of the exact f32 fma chain's, and
+    # below 2^-21 of sum |x||w| (the chain's own error is ~2^-22 at K <= 1152)
+    assert es[0] <= 1.5 * ee[0] + 1e-7, (es, ee)
+    assert es[1] <= 1.25 * ee[1] + 1e-9, (es, ee)
+    assert es[2] <= 2.0 ** -21, (es, ee)
+
+
+def test_split_dcn_accuracy_vs_fp64_oracle():
+    rng = np.random.default_rng(3)
+    N, C, H, W, Co, dg = 1, 64, 20, 44, 64, 2
+    x = (rng.standard_normal((N, C, H, W)) * 2).astype(np.float32)
+    off = (rng.standard_normal((N, 2 * dg * 9, H, W)) * 1.5).astype(np.float32)
+    mlog = rng.standard_normal((N, dg * 9, H, W)).astype(np.float32)
+    w = (rng.standard_normal((Co, C, 3, 3)) / 24).astype(np.float32)
+    mask = (2.0 / (1.0 + np.exp(-mlog.astype(np.float64)))).astype(np.float32)
+    ref = torch.from_numpy(oracle.mdcn_forward(x, off, mask, w, None, 1, 2, 2, 1, dg, dtype=np.float64))
+    scale = torch.from_numpy(oracle.mdcn_forward(np.abs(x), off, mask, np.abs(w), None, 1, 2, 2, 1, dg,
+                                                 dtype=np.float64))
+    om = torch.from_numpy(np.concatenate([off, mlog], 1)).to(DEV)
+    xd = torch.from_numpy(x).to(DEV).contiguous(memory_format=torch.channels_last)
+    wd = torch.from_numpy(w).to(DEV)
+    wsplit = ops.pack_weight_split(wd)
+    got_s = ops.mdcn_forward_fused(xd, om, wd, None, None, None, None, 1, 2, 2, dg, 2.0,
+                                   packed_weight=wsplit).cpu()
+    with exact_f32():
+        got_e = ops.mdcn_forward_fused(xd, om, wd, None, None, None, None, 1, 2, 2, dg, 2.0,
+                                       packed_weight=wsplit).cpu()
+    es, ee = _errs(got_s, ref, scale), _errs(got_e, ref, scale)
+    # the sampled values themselves carry fp32 rounding (bilinear blend), shared by both paths
+    assert es[0] <= 1.5 * ee[0] + 1e-7, (es, ee)
+    assert es[1] <= 1.25 * ee[1] + 1e-9, (es, ee)
+
+
+@pytest.mark.parametrize("dcn", [False, True])
+def test_split_tail_kernels_match_exact(dcn):
+    """Bottleneck tail kernels (conv2/DCN + conv3 pointwise GEMM + CSA epilogue) on the split
+    path against the exact engine: fp32-level agreement."""
+    gen = torch.Generator(device=DEV).manual_seed(11)
+    N, C, H, W = 2, 64, 16, 52
+    x = torch.randn(N, C, H, W, device=DEV, generator=gen).contiguous(memory_format=torch.channels_last)
+    w3 = torch.randn(C, C, 3, 3, device=DEV, generator=gen) * 0.04
+    w1 = torch.randn(C, C, 1, 1, device=DEV, generator=gen) * 0.1
+    b = torch.randn(C, device=DEV, generator=gen)
+    res = torch.randn(N, C, H, W, device=DEV, generator=gen)
+    ups = [torch.randn(N, C, H // r, W // r, device=DEV, generator=gen) for r in (2, 4)]
+    p3, p1 = ops.pack_weight_split(w3), ops.pack_weight_split(w1)
+    om = torch.randn(N, 54, H, W, device=DEV, generator=gen)
+
+    def run():
+        if dcn:
+            return ops.mdcn_pw(x, om, w3, p3, None, b, b, "relu", p1, b, res, "relu", 1, 2, 2, 2,
+                               csa_up=ups)
+        return ops.conv2d_pw(x, w3, p3, b, None, None, "relu", p1, b, res, "relu", 1, 1, 1, csa_up=ups)
+
+    s_out, s_csa = run()
+    with exact_f32():
+        e_out, e_csa = run()
+    for a, e in ((s_out, e_out), (s_csa, e_csa)):
+        assert (a - e).abs().max().item() <= 2e-5 * (1 + e.abs().max().item())
+
+
+def test_split_pack_reconstructs_weights_exactly():
+    """Head of the buffer = pack_weight (bit-exact); pieces h + m + l == w exactly."""
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    Co, Cg, k, g = 54, 32, 3, 2
+    w = torch.randn(Co, Cg, k, k, device=DEV, generator=gen) * 0.3
+    ws = ops.pack_weight_split(w, g)
+    assert torch.equal(ws, ops.pack_weight(w))
+    buf = ws._aanet_buf.cpu().numpy().view(np.uint8)
+    off = ((Co * Cg * k * k * 4 + 255) // 256) * 256
+    frag = buf[off:].view(np.uint16).reshape(-1, 3, 64, 8)  # (g, t, k, cc, blk) x piece x lane x 8
+    f32 = lambda u: (u.astype(np.uint32) << 16).view(np.float32).astype(np.float64)  # noqa: E731
+    total = f32(frag[:, 0]) + f32(frag[:, 1]) + f32(frag[:, 2])
+    Cog, T, NCC, K = Co // g, 1, Cg // 32, k * k
+    wn = w.cpu().numpy().astype(np.float64)
+    total = total.reshape(g, T, K, NCC, 4, 64, 8)
+    for gi in range(g):
+        for kk in range(K):
+            for blk in range(4):
+                for lane in range(64):
+                    row = 16 * blk + (lane & 15)
+                    for j in range(8):
+                        c = 8 * (lane >> 4) + j
+                        want = wn[gi * Cog + row, c, kk // k, kk % k] if row < Cog else 0.0
+                        assert total[gi, 0, kk, 0, blk, lane, j] == want
+
+
+def test_split_unsupported_shapes_fall_back():
+    """cg % 32 != 0: no split buffer (None); the fused path then runs the exact engine."""
+    w = torch.randn(16, 16, 3, 3, device=DEV)
+    assert ops.pack_weight_split(w) is None
+    x = torch.randn(1, 16, 8, 8, device=DEV)
+    got = ops.conv2d_fused(x, w, None, 1, 1, 1, 1, packed_weight=ops.pack_weight(w)).cpu()
+    ref = F.conv2d(x.cpu(), w.cpu(), None, 1, 1)
+    assert (got - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item())
