@@ -49,6 +49,7 @@ struct MdcnArgs {
   int N, C, H, W, Co, kh, kw, stride, pad, dil, groups, dg, Ho, Wo;
   int layout;  // AANET_LAYOUT_* bits (conv engine only)
   int split;   // conv engine: split-bf16 contraction (AANET_CONV_EXACT_F32 clear, weights carry pieces)
+  int halo;    // conv engine: 3x3 stride-1 halo-tile form (conv_fwd_kernel HALO)
   const bf16x8_t *wsplit, *tail_wsplit;  // bf16 piece fragments of weight / tail_w (split_frag_offset)
   // CSA epilogue (tail kernels): csa_out = csa_act(out + sum_j up_r[j](up[j])), r = 2 or 4
   float *csa_out;
@@ -389,8 +390,13 @@ __device__ __forceinline__ f32x4 mfma_split6(const bf16x8 (&A)[3], const bf16x8 
 // CFG: chunk shape.  0: 32 channels of one deformable group; 1: 16 channels (16-channel conv
 // groups: the second MFMA half of a chunk is skipped); 2: 32 channels spanning two 16-channel
 // deformable groups (one sampling state per (pixel, group)).
+// HALO (plain 3x3, stride 1, pad = dil <= 2, NHWC input, PREC 1): the tile is 8 rows x 16
+// columns of outputs; per 32-channel chunk its (8+2d) x (16+2d) input halo is loaded, split and
+// stored to LDS ONCE, and all nine taps read their B operand from it at shifted positions (the
+// im2col form stages, splits and synchronises once per tap).  The next chunk's halo is in flight
+// in registers during the nine taps; A fragments are double-buffered across taps.
 template <int MODE, int CO_T, int PTT, int PACKED, int TAIL, int SCHED, int FULL, int LAYOUT,
-          int CFG = 0, int PREC = 0>
+          int CFG = 0, int PREC = 0, int HALO = 0>
 __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   constexpr int CK = CFG == 1 ? 16 : 32;   // channels per K chunk
   constexpr int GPC = CFG == 2 ? 2 : 1;    // deformable groups per chunk
@@ -426,12 +432,15 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   const int wc0 = __builtin_amdgcn_readfirstlane((wave / WP) * NCB);  // first co block of the wave
   const int wp0 = __builtin_amdgcn_readfirstlane((wave % WP) * NPB);  // first px block of the wave
   const long P = (long)a.Ho * a.Wo;
-  const int ntiles = (int)((P + PTT - 1) / PTT);
+  static_assert(!HALO || (MODE == 0 && PREC == 1 && PTT == 128 && (LAYOUT & 1)), "halo configuration");
+  const int htx = HALO ? (a.Wo + 15) / 16 : 1;
+  const int ntiles = HALO ? htx * ((a.Ho + 7) / 8) : (int)((P + PTT - 1) / PTT);
   // XCD-aware remap of the pixel-tile index (bijective for any grid size)
   const int nwg = gridDim.x, b0 = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b0 & 7;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b0 >> 3);
   const int n = bid / ntiles, tile = bid % ntiles;
+  const int hy0 = HALO ? (tile / htx) * 8 : 0, hx0 = HALO ? (tile % htx) * 16 : 0;  // HALO tile origin
   const int Cg = a.C / a.groups, Cog = a.Co / a.groups, K = a.kh * a.kw, cpg = a.C / a.dg;
   const int ncot = (Cog + CO_T - 1) / CO_T;
   const int gc = blockIdx.y / ncot, cot = blockIdx.y % ncot;
@@ -677,6 +686,9 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   const int kr = lane >> 4, jj = lane & 15;
   constexpr int CUT = MODE && GPC == 1;  // chunks stop at deformable-group boundaries
   ChunkIt<CK> cur, nxt, nn;
+  bool has_next = false;
+  int slot = 1;  // parameter slot of `nxt`
+  if constexpr (!HALO) {
   cur.first(cbeg, cend, cpg, CUT);
   if (MODE) {
     if (pwave) {
@@ -691,13 +703,13 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   store_stage(cur, 0);
   nxt = cur;
   nxt.advance(K, cend, cpg, CUT);
-  bool has_next = nxt.c0 < cend;
+  has_next = nxt.c0 < cend;
   if (MODE && has_next && pwave) {
     load_params_raw(nxt);
     finish_params(nxt, 1);
   }
-  int slot = 1;  // parameter slot of `nxt`
   __syncthreads();
+  }
 
   struct Frag {
     f32x4 A[NCB], B[NPB];
@@ -749,7 +761,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     }
   };
 
-  for (int buf = 0;; buf ^= 1) {
+  if constexpr (!HALO) for (int buf = 0;; buf ^= 1) {
     nn = nxt;
     nn.advance(K, cend, cpg, CUT);
     const bool has_nn = has_next && nn.c0 < cend;
@@ -827,6 +839,93 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     has_next = has_nn;
   }
 
+  if constexpr (HALO) {
+    const int d = a.dil;
+    const int hw = 16 + 2 * d, npos = (8 + 2 * d) * hw;
+    const int hy = hy0 - d, hx = hx0 - d;
+    constexpr int HIT = 4;  // halo quads per thread: npos * 8 <= 4 * FNT for d <= 2
+    int hoff[HIT];
+#pragma unroll
+    for (int i = 0; i < HIT; ++i) {
+      const int e = tid + FNT * i, pos = e >> 3;
+      const int yy = hy + pos / hw, xx = hx + pos % hw;
+      const bool ok = pos < npos && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+      hoff[i] = ok ? ((yy * a.W + xx) * a.C + 4 * (e & 7)) * 4 : img_bytes;  // zero padding: OOB
+    }
+    f32x4 hv[HIT];
+    auto load_halo = [&](int c0) {
+      const int soff = __builtin_amdgcn_readfirstlane(c0 * 4);
+#pragma unroll
+      for (int i = 0; i < HIT; ++i)
+        hv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, hoff[i], soff, 0));
+    };
+    bf16x8 ha0[NCB][3], ha1[NCB][3];  // A fragments of two taps (double buffer)
+    // A fragments by buffer loads: per-lane offset lane*16 (one VGPR), everything else in the
+    // wave-uniform SGPR offset, so no per-tap address lives in VGPRs
+    const auto war = __builtin_amdgcn_make_buffer_rsrc((void *)a.wsplit, (short)0, 0x7ffffff0, 0x00020000);
+    auto load_ha = [&](bf16x8 (&ha)[NCB][3], int c0, int k) {
+      const int base = ((((gc * sT + st64) * K + k) * sNCC + ((c0 - cbeg) >> 5)) * 4 + sbb) * 3;
+#pragma unroll
+      for (int m = 0; m < NCB; ++m)
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc)
+          ha[m][pc] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+              war, lane * 16, __builtin_amdgcn_readfirstlane((base + 3 * m + pc) * 1024), 0));
+    };
+    // B fragment LDS address of (tile row r, column jj) at halo row/column shift (si, sj)
+    const int jjd = jj;
+    // tap k of the chunk at c0: prefetch the next tap's A (the next chunk's tap 0 after tap 8),
+    // then the B fragments at the tap's shifted halo positions and the MFMAs
+    auto tap = [&](bf16x8 (&cur)[NCB][3], bf16x8 (&nxt)[NCB][3], int k, int c0, bool more) {
+      // keep the scheduler from hoisting later taps' work (SSA values, no WAR on the buffers)
+      // above this tap: 9 taps of fragments and addresses would not fit the 128-VGPR budget
+      __builtin_amdgcn_sched_barrier(0);
+      if (k < 8)
+        load_ha(nxt, c0, k + 1);
+      else if (more)
+        load_ha(nxt, c0 + 32, 0);
+      const int ti = k / 3, tj = k % 3;
+      int col = jjd;
+      asm volatile("" : "+v"(col));  // recomputed per tap (not hoisted as 18 live addresses)
+#pragma unroll
+      for (int b = 0; b < NPB; ++b) {
+        const int pos = (wp0 + b + ti * d) * hw + col + tj * d;
+        const __bf16 *sH = reinterpret_cast<const __bf16 *>(smem) + swz(pos, kr);
+        bf16x8 fb[3];
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) fb[pc] = *reinterpret_cast<const bf16x8 *>(sH + pc * npos * 32);
+#pragma unroll
+        for (int m = 0; m < NCB; ++m) acc[m][b] = mfma_split6(cur[m], fb, acc[m][b]);
+      }
+    };
+    auto stage = [&](int c0) {
+      __syncthreads();  // every wave is done with the previous chunk's halo
+#pragma unroll
+      for (int i = 0; i < HIT; ++i) {
+        const int pos = (tid + FNT * i) >> 3;
+        if (pos < npos) put_split(reinterpret_cast<__bf16 *>(smem), npos * 32, pos, tid & 7, hv[i]);
+      }
+      __syncthreads();
+      const bool more = c0 + 32 < cend;
+      if (more) load_halo(c0 + 32);
+      return more;
+    };
+    load_halo(cbeg);
+    load_ha(ha0, cbeg, 0);
+    // nine taps per chunk: the A buffers alternate, so consecutive chunks start on opposite ones
+    for (int c0 = cbeg; c0 < cend; c0 += 64) {
+      bool more = stage(c0);
+      tap(ha0, ha1, 0, c0, more); tap(ha1, ha0, 1, c0, more); tap(ha0, ha1, 2, c0, more);
+      tap(ha1, ha0, 3, c0, more); tap(ha0, ha1, 4, c0, more); tap(ha1, ha0, 5, c0, more);
+      tap(ha0, ha1, 6, c0, more); tap(ha1, ha0, 7, c0, more); tap(ha0, ha1, 8, c0, more);
+      if (!more) break;
+      more = stage(c0 + 32);
+      tap(ha1, ha0, 0, c0 + 32, more); tap(ha0, ha1, 1, c0 + 32, more); tap(ha1, ha0, 2, c0 + 32, more);
+      tap(ha0, ha1, 3, c0 + 32, more); tap(ha1, ha0, 4, c0 + 32, more); tap(ha0, ha1, 5, c0 + 32, more);
+      tap(ha1, ha0, 6, c0 + 32, more); tap(ha0, ha1, 7, c0 + 32, more); tap(ha1, ha0, 8, c0 + 32, more);
+    }
+  }
+
   if (TAIL) {
     // act(post_scale*(acc+bias)+post_shift) -> LDS as the B operand [px][c] of a second GEMM with
     // the pointwise weights [co2][c] (channels 32h..32h+31 in buffer h), then re-contract.
@@ -890,12 +989,28 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
         sO[(16 * (wc0 + m) + 4 * kr + r) * OP + 16 * (wp0 + b) + jj] = acc[m][b][r];
   __syncthreads();
   const long p0 = (long)tile * PTT;
+  // output pixel of tile-local index px (flattened, -1 outside the image); quad q = px 4q..4q+3
+  auto pix = [&](int px) -> long {
+    if constexpr (HALO) {
+      const int y = hy0 + (px >> 4), x = hx0 + (px & 15);
+      return (y < a.Ho && x < a.Wo) ? (long)y * a.Wo + x : -1;
+    } else {
+      return p0 + px < P ? p0 + px : -1;
+    }
+  };
+  const bool vec = HALO ? (a.Wo & 3) == 0 : (P & 3) == 0;
+  auto quad_ok = [&](int q) -> bool {  // the quad is inside the image and 16-byte aligned
+    if constexpr (HALO)
+      return vec && hy0 + (q >> 2) < a.Ho && hx0 + 4 * (q & 3) + 3 < a.Wo;
+    else
+      return vec && p0 + 4 * q + 3 < P;
+  };
   if constexpr (ONH) {  // [px][co] rows of 16-byte channel quads
     constexpr int CQ = CO_T / 4;
     for (int e = tid; e < PTT * CQ; e += FNT) {
       const int px = e / CQ, cq = e % CQ, co = co0 + 4 * cq;
-      const long pe = p0 + px;
-      if (co >= co_end || pe >= P) continue;
+      const long pe = pix(px);
+      if (co >= co_end || pe < 0) continue;
       f32x4 v;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -911,7 +1026,6 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     }
     return;
   }
-  const bool vec = (P & 3) == 0;
   constexpr int QPR = PTT / 4;  // float4 per tile row
   const int cout = TAIL ? a.Co2 : a.Co;
   const int cend_o = TAIL ? a.Co2 : co_end;
@@ -934,9 +1048,9 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     for (int b = 0; b < EB; ++b) {
       const int e = tid + (i0 + b) * FNT;
       const int col = e / QPR, q = e % QPR, co = co0 + col;
-      const long pe = p0 + 4 * q;
-      eok[b] = (NE % FNT == 0 || e < NE) && co < cend_o && vec && pe + 3 < P;
+      eok[b] = (NE % FNT == 0 || e < NE) && co < cend_o && quad_ok(q);
       if (!eok[b]) continue;
+      const long pe = pix(4 * q);
       const long o = ((long)n * cout + co) * P + pe;
       ev[b] = *reinterpret_cast<const f32x4 *>(sO + col * OP + 4 * q);
       if (a.residual) er[b] = *reinterpret_cast<const f32x4 *>(a.residual + o);
@@ -962,7 +1076,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       if (!eok[b]) continue;
       const int e = tid + (i0 + b) * FNT;
       const int col = e / QPR, q = e % QPR, co = co0 + col;
-      const long pe = p0 + 4 * q;
+      const long pe = pix(4 * q);
       const long o = ((long)n * cout + co) * P + pe;
       const float bias = ebias ? ebias[co] : 0.f;
       const float sc = esc ? esc[co] : 1.f;
@@ -996,23 +1110,23 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     }
   }
   // pixels the quad path does not cover (P % 4 != 0, ragged last tile): one element at a time
-  if (!vec || p0 + PTT > P) {
+  if (!quad_ok(QPR - 1) || !quad_ok(0)) {
     for (int e = tid; e < NE; e += FNT) {
       const int col = e / QPR, q = e % QPR, co = co0 + col;
-      const long pe = p0 + 4 * q;
-      if (co >= cend_o || pe >= P || (vec && pe + 3 < P)) continue;
+      if (co >= cend_o || quad_ok(q)) continue;
       const float bias = ebias ? ebias[co] : 0.f;
       const float sc = esc ? esc[co] : 1.f;
       const float sh = esc ? esh[co] : 0.f;
-      const long o = ((long)n * cout + co) * P + pe;
       const f32x4 v = *reinterpret_cast<const f32x4 *>(sO + col * OP + 4 * q);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if (pe + u >= P) break;
+        const long pe = pix(4 * q + u);
+        if (pe < 0) continue;
+        const long o = ((long)n * cout + co) * P + pe;
         float t = v[u] + bias;
         if (esc) t = t * sc + sh;
-        if (a.residual) t += a.residual[o + u];
-        a.out[o + u] = apply_act(t, eact);
+        if (a.residual) t += a.residual[o];
+        a.out[o] = apply_act(t, eact);
       }
     }
   }
@@ -1325,6 +1439,7 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
   a.dg = dg;
   a.layout = 0;
   a.split = 0;
+  a.halo = 0;
   a.csa_out = nullptr;
   a.num_up = 0;
   a.csa_act = 0;
@@ -1359,6 +1474,17 @@ void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
         hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 0, 1, 0, CFG, 1>), grid, blk, 0, st, a);
       }
       return;
+    }
+    if constexpr (MODE == 0 && PTT == 128) {
+      if (a.split && packed && a.halo) {  // 3x3 stride-1 halo-tile form (NHWC input)
+        if (a.tail_w)
+          hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 1, 1, 1, 1, CFG, 1, 1>), grid, blk, 0, st, a);
+        else if (a.layout == 3)
+          hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 0, 1, 1, 3, CFG, 1, 1>), grid, blk, 0, st, a);
+        else
+          hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 0, 1, 1, 1, CFG, 1, 1>), grid, blk, 0, st, a);
+        return;
+      }
     }
     if (a.split && packed) {
       if (a.tail_w) {
@@ -1418,7 +1544,8 @@ void launch_fwd_t(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
 }
 
 template <int MODE>
-int launch_fwd(const MdcnArgs &a, int packed, hipStream_t st) {
+int launch_fwd(const MdcnArgs &a_in, int packed, hipStream_t st) {
+  MdcnArgs a = a_in;
   const int rc = check_shapes(a);
   if (rc) return rc;
   if (!a.x || !a.weight || !a.out) return AANET_EINVAL;
@@ -1451,7 +1578,13 @@ int launch_fwd(const MdcnArgs &a, int packed, hipStream_t st) {
   static const int ptt_env = [] { const char *e = getenv("AANET_PTT"); return e ? atoi(e) : 0; }();
   if (ptt_env == 64 && co_t != 16) ptt = 64;  // A/B switch (tools/conv_microbench.py)
   if (full_cfg(a, MODE, co_t) == 1) ptt = 128;  // 16-channel chunks are staged 4 per thread
-  dim3 grid((unsigned)(a.N * host_div_up(P, ptt)), (unsigned)(a.groups * ncot));
+  static const int nohalo = [] { const char *e = getenv("AANET_NO_HALO"); return e ? atoi(e) : 0; }();
+  a.halo = !nohalo && MODE == 0 && a.split && packed && (a.layout & 1) && a.kh == 3 && a.kw == 3 &&
+           a.stride == 1 && a.pad == a.dil && a.dil <= 2 && co_t >= 32 && full_cfg(a, 0, co_t) == 0;
+  if (a.halo) ptt = 128;
+  dim3 grid((unsigned)(a.halo ? (long)a.N * host_div_up(a.Wo, 16) * host_div_up(a.Ho, 8)
+                              : a.N * host_div_up(P, ptt)),
+            (unsigned)(a.groups * ncot));
   if (ptt == 128) {
     switch (co_t) {
       case 16: launch_fwd_t<MODE, 16, 128>(a, packed, grid, st); break;

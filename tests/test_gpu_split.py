@@ -37,6 +37,10 @@ def _errs(got, ref64, scale64):
     (2, 64, 24, 52, 64, 1, 1, 0, 1, 1, False),    # conv1 / conv3
     (2, 64, 24, 52, 32, 3, 2, 1, 1, 1, False),    # CSA strided 3x3
     (1, 128, 12, 40, 96, 3, 1, 1, 1, 1, False),   # Co > 64: two output tiles
+    # halo-tile form (NHWC 3x3 stride 1): odd chunk counts, ragged tiles, Wo % 4 != 0, dil 2
+    (1, 96, 13, 30, 64, 3, 1, 1, 1, 1, True),     # 3 channel chunks, element epilogue
+    (1, 64, 9, 20, 40, 3, 1, 2, 2, 1, True),      # dilation 2, Co = 40 of a 64 tile
+    (2, 32, 8, 16, 32, 3, 1, 1, 1, 1, True),      # one chunk, 32-channel tile, exact tile fit
 ])
 def test_split_conv_accuracy_vs_fp64(case):
     N, C, H, W, Co, k, s, p, d, g, nhwc = case
@@ -150,3 +154,20 @@ def test_split_unsupported_shapes_fall_back():
     got = ops.conv2d_fused(x, w, None, 1, 1, 1, 1, packed_weight=ops.pack_weight(w)).cpu()
     ref = F.conv2d(x.cpu(), w.cpu(), None, 1, 1)
     assert (got - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item())
+
+
+def test_halo_conv_nhwc_output_vs_torch():
+    """Halo-tile 3x3 with a channels-last output (AANET_LAYOUT_OUT_NHWC) and a residual."""
+    gen = torch.Generator().manual_seed(9)
+    x = torch.randn(2, 64, 11, 36, generator=gen)
+    w = torch.randn(64, 64, 3, 3, generator=gen) / 24
+    b = torch.randn(64, generator=gen)
+    res = torch.randn(2, 64, 11, 36, generator=gen)
+    ref = F.relu(F.conv2d(x, w, b, 1, 1) + res)
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+    rd = res.to(DEV).contiguous(memory_format=torch.channels_last)
+    wd = w.to(DEV)
+    got = ops.conv2d_fused(xd, wd, b.to(DEV), 1, 1, 1, 1, "relu", rd,
+                           packed_weight=ops.pack_weight_split(wd), out_nhwc=True)
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    assert (got.cpu() - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item())
