@@ -1460,7 +1460,7 @@ void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
   const dim3 blk(FNT);
   if constexpr (FULL && CFG == 0 && CO_T >= 32) {  // split-bf16 contraction (PREC 1)
     static const int nosched = [] { const char *e = getenv("AANET_SPLIT_NOSCHED"); return e ? atoi(e) : 0; }();
-    if (a.split && packed && nosched) {  // A/B switch: staging after the MFMAs, not interleaved
+    if (a.split && packed && nosched && !(MODE == 1 && a.tail_w && a.layout == 1)) {  // A/B switch
       if (a.tail_w) {
         if (a.layout == 1)
           hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 0, 1, 1, CFG, 1>), grid, blk, 0, st, a);
@@ -1486,7 +1486,12 @@ void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
         return;
       }
     }
-    if (a.split && packed) {
+    // The deformable tail kernel with NHWC staging is excluded: on the split path it was not
+    // bit-reproducible run to run at C2 scale (B=8: ~1e3 of 2.7e7 outputs moved, only with
+    // fractional offsets; tests/test_gpu_split.py::test_fused_paths_bit_reproducible) -- the
+    // cause is not yet found, so that configuration runs the exact f32 contraction.
+    const bool racy = MODE == 1 && a.tail_w && a.layout == 1;
+    if (a.split && packed && !racy) {
       if (a.tail_w) {
         if (a.layout == 1)
           hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1, 1, 1, CFG, 1>), grid, blk, 0, st, a);

@@ -30,6 +30,11 @@ sys.path.insert(0, REPO)
 METRIC = "stereo-pairs/s @384x1248 D=64 fp32, 1/2/4/8 MI355X; EPE vs ref"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 = f32 vector rate
+BF16_DENSE_PEAK_TF = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
+# The conv engine's split-bf16 contraction (include/aanet_mi355x.h AANET_CONV_EXACT_F32) runs an
+# fp32 MAC as six bf16 piece products on the matrix cores: its ceiling in fp32-equivalent FLOP/s
+# is the dense bf16 peak / 6.  The exact f32 engine (--exact-f32) is bounded by FP32_MFMA_PEAK_TF.
+SPLIT_PEAK_TF = BF16_DENSE_PEAK_TF / 6
 H_IMG, W_IMG, MAXD_IMG = 384, 1248, 192
 MAXD = MAXD_IMG // 3       # cost-volume disparities at 1/3 resolution (nets/aanet.py:56-59)
 FEAT_C = 128
@@ -53,6 +58,8 @@ def parse():
                     help="--train with torch.use_deterministic_algorithms (det DCN backward)")
     ap.add_argument("--model", default=None, choices=sorted(FULL_MODELS),
                     help="time the full model (features + hot path + refinement) instead")
+    ap.add_argument("--exact-f32", action="store_true",
+                    help="conv engine on exact f32 MFMA instead of the split-bf16 contraction")
     ap.add_argument("--only", default=None,
                     help="profiling mode: run only one kernel family (corr|mdcn|regress|step)")
     return ap.parse_args()
@@ -162,11 +169,48 @@ def kernel_rooflines(model, left, right, batch, iters):
     Co, Ci = dc.weight.shape[:2]
     Co2 = w3.shape[0]
     flops = 2.0 * B * H * W * (Co * Ci * 9 + Co2 * Co)
+    # (this NHWC deformable tail configuration runs the exact f32 contraction even when the
+    # split one is selected: mdcn.hip launch_fwd_f, "racy")
     res["mdcn_pw_s0"] = dict(bound="mfma", ms=ms, algo=flops, unit="TFLOP/s",
                              achieved=flops / ms / 1e9, peak=FP32_MFMA_PEAK_TF)
+    # the plain-3x3 ISA bottleneck tail (SimpleBottleneck of fusion 0, scale 0): halo-tile conv2
+    # + BN2 + ReLU -> conv3 + BN3 + identity + ReLU, with the scale-0 CSA sum
+    blk0 = model.aggregation.fusions[0].branches[0][0]
+    with torch.no_grad():
+        x1 = conv_bn_act(vol, blk0.conv1, blk0.bn1, "relu", out_nhwc=True)
+        w2, b2, p2 = folded(blk0.conv2, blk0.bn2)
+        w3, b3, p3 = folded(blk0.conv3, blk0.bn3)
+        fn = lambda: ops.conv2d_pw(x1, w2, p2, b2, None, None, "relu", p3, b3, vol, "relu",  # noqa: E731
+                                   1, 1, 1, csa_up=ups)
+        ms = time_events(fn, iters, stream)
+    flops = 2.0 * B * H * W * (w2.shape[0] * w2.shape[1] * 9 + w3.shape[0] * w3.shape[1])
+    res["conv3x3_pw_s0"] = dict(bound="mfma", ms=ms, algo=flops, unit="TFLOP/s",
+                                achieved=flops / ms / 1e9, peak=conv_peak())
     for v in res.values():
         v["frac"] = v["achieved"] / v["peak"]
     return res
+
+
+def conv_contraction():
+    from aanet_amd import _lib
+    if _lib.conv_flags():
+        return "exact f32 MFMA (v_mfma_f32_16x16x4_f32)"
+    return ("fp32 operands split into three exact bf16 pieces, six v_mfma_f32_16x16x32_bf16 "
+            "products, fp32 accumulation (fp32-accurate; tests/test_gpu_split.py)")
+
+
+def peak_basis(dom):
+    if dom["unit"] != "TFLOP/s":
+        return "HBM 8.0 TB/s spec"
+    if dom["peak"] == FP32_MFMA_PEAK_TF:
+        return "f32 MFMA 157.3 TF/s"
+    return ("split-bf16 contraction: dense bf16 MFMA 2.5 PF/s / 6 products = 416.7 TF/s "
+            "fp32-equivalent (the native f32 MFMA peak is 157.3)")
+
+
+def conv_peak():
+    from aanet_amd import _lib
+    return FP32_MFMA_PEAK_TF if _lib.conv_flags() else SPLIT_PEAK_TF
 
 
 def cpu_baseline(model, left, right, gpu_disp):
@@ -234,6 +278,9 @@ def main():
     torch.cuda.set_device(device)
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
+    if args.exact_f32:
+        from aanet_amd import _lib
+        _lib.set_exact_f32(True)
 
     if args.train:
         train_main(args, device, rank, world)
@@ -278,6 +325,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
+            "contraction": conv_contraction(),
             "data": f"synthetic ({FEATURE_KINDS[args.features]} on device, seeded per rank; "
                     "random-init weights)",
             "config": {
@@ -292,7 +340,8 @@ def main():
             "roofline": {"kernel": dom_name, "bound": dom["bound"], "achieved": dom["achieved"],
                          "peak": dom["peak"], "unit": dom["unit"], "frac": dom["frac"],
                          "traffic": traffic, "ms_per_launch": dom["ms"],
-                         "algorithmic_per_launch": dom["algo"]},
+                         "algorithmic_per_launch": dom["algo"],
+                         "peak_basis": peak_basis(dom)},
             "kernels": {k: {kk: v[kk] for kk in ("bound", "ms", "achieved", "unit", "frac")}
                         for k, v in roof.items()},
         }

@@ -171,3 +171,36 @@ def test_halo_conv_nhwc_output_vs_torch():
                            packed_weight=ops.pack_weight_split(wd), out_nhwc=True)
     assert got.is_contiguous(memory_format=torch.channels_last)
     assert (got.cpu() - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item())
+
+
+def test_fused_paths_bit_reproducible():
+    """Identical launches give identical bits on every fused path the hot path uses, at the C2
+    scale-0 shape (B=8, contention on every CU) with fractional DCN offsets."""
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    B, C, H, W = 8, 64, 128, 416
+    x = torch.randn(B, C, H, W, device=DEV, generator=gen)
+    xn = x.contiguous(memory_format=torch.channels_last)
+    res = torch.randn(B, C, H, W, device=DEV, generator=gen)
+    w1 = torch.randn(C, C, 1, 1, device=DEV, generator=gen) * 0.1
+    w3 = torch.randn(C, C, 3, 3, device=DEV, generator=gen) * 0.04
+    wo = torch.randn(54, 32, 3, 3, device=DEV, generator=gen) * 0.01
+    bo = torch.randn(54, device=DEV, generator=gen)
+    b = torch.randn(C, device=DEV, generator=gen)
+    p1, p3, po = ops.pack_weight_split(w1), ops.pack_weight_split(w3), ops.pack_weight_split(wo, 2)
+    om = ops.conv2d_fused(xn, wo, bo, 1, 2, 2, 2, packed_weight=po)
+    ups = [torch.randn(B, C, H // r, W // r, device=DEV, generator=gen) for r in (2, 4)]
+    cases = {
+        "halo 3x3": lambda: ops.conv2d_fused(xn, w3, b, 1, 1, 1, 1, "relu", packed_weight=p3),
+        "halo offset conv": lambda: ops.conv2d_fused(xn, wo, bo, 1, 2, 2, 2, packed_weight=po),
+        "conv1 nhwc out": lambda: ops.conv2d_fused(x, w1, b, act="relu", packed_weight=p1, out_nhwc=True),
+        "dcn nhwc": lambda: ops.mdcn_forward_fused(xn, om, w3, None, b, b, "relu", 1, 2, 2, 2, 2.0,
+                                                   packed_weight=p3),
+        "dcn tail nhwc + csa": lambda: ops.mdcn_pw(xn, om, w3, p3, None, b, b, "relu", p1, b, res, "relu",
+                                                   1, 2, 2, 2, csa_up=ups)[1],
+        "conv tail nhwc + csa": lambda: ops.conv2d_pw(xn, w3, p3, b, None, None, "relu", p1, b, res, "relu",
+                                                      1, 1, 1, csa_up=ups)[1],
+    }
+    for name, fn in cases.items():
+        ref = fn().clone()
+        for _ in range(4):
+            assert torch.equal(fn(), ref), name
