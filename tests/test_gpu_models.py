@@ -82,7 +82,9 @@ def test_full_model_vs_reference_golden(tag, fuse):
     distance times 2 (mean, p99) / 4 (max), and the AANet / AANet+ models additionally to max 1e-3 px
     against the reference's fp32 output."""
     g, m, left, right = build(tag, fuse)
-    with torch.no_grad():
+    # the reference-order run puts every conv on MIOpen: deterministic algorithms, so the result
+    # does not move with MIOpen's per-run algorithm choice (p99 moved 0.026-0.035 px on PSMNet-AA)
+    with torch.no_grad(), torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=True):
         pyr = m(left, right)
     n = len([k for k in g if k.startswith("disp") and not k.startswith("disp64")])
     assert len(pyr) == n

@@ -28,19 +28,23 @@ pe = ops.pack_weight_split(eye)
 zero = torch.zeros(C, device=dev)
 cases = {
     "dcn_pw nhwc": lambda: ops.mdcn_pw(xn, om, w3, p3, None, b, b, "relu", p1, b, None, None, 1, 2, 2, 2),
-    "dcn_pw nhwc zero-offset": lambda: ops.mdcn_pw(xn, om0, w3, p3, None, b, b, "relu", p1, b, None, None, 1, 2, 2, 2),
-    "dcn_pw nhwc identity tail": lambda: ops.mdcn_pw(xn, om, w3, p3, None, b, b, "relu", pe, zero, None, None, 1, 2, 2, 2),
-    "dcn_pw nhwc B=1": lambda: ops.mdcn_pw(xn[:1], om[:1], w3, p3, None, b, b, "relu", p1, b, None, None, 1, 2, 2, 2),
-    "dcn nhwc": lambda: ops.mdcn_forward_fused(xn, om, w3, None, b, b, "relu", 1, 2, 2, 2, 2.0, packed_weight=p3),
+    "dcn_pw nhwc + csa": lambda: ops.mdcn_pw(xn, om, w3, p3, None, b, b, "relu", p1, b, res, "relu",
+                                             1, 2, 2, 2, csa_up=ups)[1],
+    "dcn_pw nchw": lambda: ops.mdcn_pw(x, om, w3, p3, None, b, b, "relu", p1, b, None, None, 1, 2, 2, 2),
 }
-for exact in (False,):
+refs = {}
+for exact in (True, False):
     _lib.set_exact_f32(exact)
     for name, fn in cases.items():
         ref = fn().clone()
         bad = 0
         mx = 0.0
-        for _ in range(6):
+        for _ in range(12):
             o = fn()
             bad = max(bad, int((o != ref).sum()))
             mx = max(mx, float((o - ref).abs().max()))
-        print(f"{'exact' if exact else 'split'} {name:28s} differing {bad:9d}  max {mx:.3e}", flush=True)
+        if exact:
+            refs[name] = ref
+        dx = float((ref - refs[name]).abs().max()) if name in refs else float("nan")
+        print(f"{'exact' if exact else 'split'} {name:28s} differing {bad:9d}  max {mx:.3e}  vs exact {dx:.3e}",
+              flush=True)
