@@ -1008,6 +1008,16 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   }
 
   // Epilogue: accumulators -> LDS [co][px] -> 16-byte row segments (+ residual) -> HBM.
+  constexpr int QPR = PTT / 4;  // float4 per tile row
+  constexpr int CQ = CO_T / 4;  // channel quads (NHWC output rows)
+  constexpr int NE = ONH ? PTT * CQ : CO_T * QPR;
+  constexpr int EPT = (NE + FNT - 1) / FNT;
+  const int cout = TAIL ? a.Co2 : a.Co;
+  const int cend_o = TAIL ? a.Co2 : co_end;
+  const float *ebias = TAIL ? a.tail_b : a.bias;
+  const float *esc = TAIL ? nullptr : a.post_scale;
+  const float *esh = TAIL ? nullptr : a.post_shift;
+  const int eact = TAIL ? a.tail_act : a.act;
   __syncthreads();
   float *sO = smem;
 #pragma unroll
@@ -1017,6 +1027,19 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         sO[(16 * (wc0 + m) + 4 * kr + r) * OP + 16 * (wp0 + b) + jj] = acc[m][b][r];
+  static_assert(!ONH || FNT % CQ == 0, "NHWC epilogue: one channel quad per thread");
+  // NHWC output: the 4 channels of the thread's quad (the NCHW form loads per item: holding its
+  // parameters here costs the DCN tail kernel spills)
+  float eb[4] = {0.f, 0.f, 0.f, 0.f}, es[4] = {1.f, 1.f, 1.f, 1.f}, eh[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (ONH) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cc = min(co0 + 4 * (tid % CQ) + i, cend_o - 1);
+      eb[i] = ebias ? ebias[cc] : 0.f;
+      es[i] = esc ? esc[cc] : 1.f;
+      eh[i] = esc ? esh[cc] : 0.f;
+    }
+  }
   __syncthreads();
   const long p0 = (long)tile * PTT;
   // output pixel of tile-local index px (flattened, -1 outside the image); quad q = px 4q..4q+3
@@ -1036,7 +1059,6 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       return vec && p0 + 4 * q + 3 < P;
   };
   if constexpr (ONH) {  // [px][co] rows of 16-byte channel quads
-    constexpr int CQ = CO_T / 4;
     for (int e = tid; e < PTT * CQ; e += FNT) {
       const int px = e / CQ, cq = e % CQ, co = co0 + 4 * cq;
       const long pe = pix(px);
@@ -1044,8 +1066,8 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       f32x4 v;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        float t = sO[(4 * cq + u) * OP + px] + (a.bias ? a.bias[co + u] : 0.f);
-        if (a.post_scale) t = t * a.post_scale[co + u] + a.post_shift[co + u];
+        float t = sO[(4 * cq + u) * OP + px] + eb[u];
+        if (a.post_scale) t = t * es[u] + eh[u];
         v[u] = t;
       }
       const long o = ((long)n * P + pe) * a.Co + co;
@@ -1056,18 +1078,9 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     }
     return;
   }
-  constexpr int QPR = PTT / 4;  // float4 per tile row
-  const int cout = TAIL ? a.Co2 : a.Co;
-  const int cend_o = TAIL ? a.Co2 : co_end;
-  const float *ebias = TAIL ? a.tail_b : a.bias;
-  const float *esc = TAIL ? nullptr : a.post_scale;
-  const float *esh = TAIL ? nullptr : a.post_shift;
-  const int eact = TAIL ? a.tail_act : a.act;
   // Items (4 pixels x 1 channel) are processed two at a time with every global load of the pair
   // (residual, CSA source segments) issued before any use: a per-item load->use chain would
   // expose the HBM / L2 latency once per item.
-  constexpr int NE = CO_T * QPR;
-  constexpr int EPT = (NE + FNT - 1) / FNT;
   constexpr int EB = EPT >= 2 ? 2 : 1;
   const bool csa = TAIL && a.csa_out;
 #pragma unroll
