@@ -34,6 +34,7 @@ _SIGNATURES = {
     "aanet_mdcn_fwd_fused_f32": [_P, _P, _L, _P, _L, _I, _F, _P, _I, _P, _P, _P, _I, _P] + [_I] * 13 + [_P],
     "aanet_mdcn_bwd_f32": [_P] * 10 + [_I] * 12 + [_P],
     "aanet_mdcn_bwd_det_f32": [_P] * 10 + [_I] * 12 + [_P, ctypes.c_size_t, _P],
+    "aanet_mdcn_bwd_ws_f32": [_P] * 10 + [_I] * 12 + [_P, ctypes.c_size_t, _P],
     "aanet_conv2d_fused_f32": [_P] * 6 + [_I, _I, _P] + [_I] * 12 + [_P],
     "aanet_conv_weight_pack_f32": [_P, _P, _I, _I, _I, _I, _P],
     "aanet_conv_weight_pack_split_f32": [_P, _P, _I, _I, _I, _I, _I, _P],
@@ -69,6 +70,8 @@ def lib():
         L.aanet_status_string.restype = ctypes.c_char_p
         L.aanet_mdcn_bwd_det_workspace_size.argtypes = [_I] * 12
         L.aanet_mdcn_bwd_det_workspace_size.restype = ctypes.c_size_t
+        L.aanet_mdcn_bwd_ws_workspace_size.argtypes = [_I] * 12
+        L.aanet_mdcn_bwd_ws_workspace_size.restype = ctypes.c_size_t
         L.aanet_version.restype = _I
         L.aanet_conv_weight_pack_split_bytes.argtypes = [_I] * 5
         L.aanet_conv_weight_pack_split_bytes.restype = _L
@@ -78,6 +81,7 @@ def lib():
 
 def exported_symbols():
     return (["aanet_version", "aanet_status_string", "aanet_mdcn_bwd_det_workspace_size",
+             "aanet_mdcn_bwd_ws_workspace_size",
              "aanet_conv_weight_pack_split_bytes"] + list(_SIGNATURES))
 
 

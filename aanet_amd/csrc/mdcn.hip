@@ -1226,7 +1226,11 @@ __global__ void mdcn_sample_index_kernel(MdcnArgs a, int *__restrict__ hl, int *
 // associative, so the sum -- and the fp32 grad_x converted from it -- does not depend on the
 // order in which the atomics land: the deterministic backward of torch's
 // use_deterministic_algorithms (the reference's col2im atomics, kernel.cu:688, are not).
-template <int DET>
+// NHS (float atomics only): grad_x is scattered into an NHWC workspace [N][H*W][C] with the lanes
+// of a wave on 32 consecutive channels of a corner -- each atomic instruction covers two fully used
+// 128-byte lines, where the NCHW form (lanes = pixels with data-dependent corners) spreads one
+// instruction over a dozen partly used lines; nhwc_to_nchw_kernel then writes grad_x.
+template <int DET, int NHS = 0>
 __global__ __launch_bounds__(NT) void mdcn_bwd_data_kernel(MdcnArgs a, const float *__restrict__ gout,
                                                            float *__restrict__ gx,
                                                            float *__restrict__ goff,
@@ -1239,6 +1243,7 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_kernel(MdcnArgs a, const flo
   float *sWt = sG + Co * GP;            // [KC][WTP]     W^T chunk
   float *sCg = sWt + KC * WTP;          // [KC][CP]      colg chunk
   float *sRed = sCg + KC * CP;          // [3][4][64]    cross-wave reduction
+  float *sS = sRed + 3 * 4 * 64;        // [PT][12]      NHS: per-pixel corners, weights, mask
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long P = (long)a.Ho * a.Wo;
@@ -1272,6 +1277,18 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_kernel(MdcnArgs a, const flo
     Samp s;
     pixel_samp(s, a, n, g, k, pvalid ? p : 0, ho, wo);
     float gm = 0.f, goh = 0.f, gow = 0.f;
+    if (NHS && wave == 0) {  // published for the chunk loop (its first barrier orders it)
+#pragma clang fp contract(off)
+      const bool on = pvalid && s.valid;
+      const float hh = 1.f - s.lh, hw = 1.f - s.lw;
+      float *q = sS + lane * 12;
+      q[0] = __builtin_bit_cast(float, on && (s.ok & 1) ? s.i1 : -1);
+      q[1] = __builtin_bit_cast(float, on && (s.ok & 2) ? s.i2 : -1);
+      q[2] = __builtin_bit_cast(float, on && (s.ok & 4) ? s.i3 : -1);
+      q[3] = __builtin_bit_cast(float, on && (s.ok & 8) ? s.i4 : -1);
+      q[4] = hh * hw, q[5] = hh * s.lw, q[6] = s.lh * hw, q[7] = s.lh * s.lw;
+      q[8] = s.m;
+    }
     for (int c0 = g * cpg; c0 < (g + 1) * cpg; c0 += KC) {
       const int rows = min(KC, (g + 1) * cpg - c0);
       __syncthreads();  // previous chunk's sCg / sWt readers are done
@@ -1313,11 +1330,42 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_kernel(MdcnArgs a, const flo
           const float top = cg * s.m;
           goh += wh * top;
           gow += ww * top;
+          if (NHS) continue;
           const long cb = (long)c * HW;
           if (s.ok & 1) scatter(cb + s.i1, hh * hw * top);
           if (s.ok & 2) scatter(cb + s.i2, hh * s.lw * top);
           if (s.ok & 4) scatter(cb + s.i3, s.lh * hw * top);
           if (s.ok & 8) scatter(cb + s.i4, s.lh * s.lw * top);
+        }
+      }
+      if (NHS) {
+        // lanes 0-31: channel cl of pixel 16w + 2t, lanes 32-63: of pixel 16w + 2t + 1
+        const int cl = lane & 31;
+        if (cl < rows) {
+          const long cbase = (long)n * HW * C + c0 + cl;
+          auto nadd = [&](int i, float v) {
+            if (DET)
+              atomicAdd(reinterpret_cast<unsigned long long *>(gxi + cbase + (long)i * C),
+                        (unsigned long long)__double2ll_rn((double)v * scale));
+            else
+              atomicAdd(gx + cbase + (long)i * C, v);
+          };
+#pragma unroll 2
+          for (int t = 0; t < 8; ++t) {
+#pragma clang fp contract(off)
+            const int px = 16 * wave + 2 * t + (lane >> 5);
+            const float *q = sS + px * 12;
+            const f32x4 qi = *reinterpret_cast<const f32x4 *>(q);
+            const f32x4 qw = *reinterpret_cast<const f32x4 *>(q + 4);
+            const float top = sCg[cl * CP + px] * q[8];
+            const float qi0 = qi[0], qi1 = qi[1], qi2 = qi[2], qi3 = qi[3];  // (bit_cast of an
+            const int i1 = __builtin_bit_cast(int, qi0), i2 = __builtin_bit_cast(int, qi1);  // element
+            const int i3 = __builtin_bit_cast(int, qi2), i4 = __builtin_bit_cast(int, qi3);  // lvalue)
+            if (i1 >= 0) nadd(i1, qw[0] * top);
+            if (i2 >= 0) nadd(i2, qw[1] * top);
+            if (i3 >= 0) nadd(i3, qw[2] * top);
+            if (i4 >= 0) nadd(i4, qw[3] * top);
+          }
         }
       }
     }
@@ -1435,6 +1483,37 @@ __global__ __launch_bounds__(256) void bias_grad_kernel(const float *__restrict_
     __syncthreads();
   }
   if (threadIdx.x == 0) gb[co] += red[0];
+}
+
+// grad_x NHWC workspace [N][HW][C] -> NCHW: 32 x 32 tiles through LDS (both sides coalesced).
+// T = long long: the deterministic fixed-point accumulator (value * scale), converted to fp32 here.
+template <typename T>
+__global__ __launch_bounds__(256) void nhwc_to_nchw_kernel(const T *__restrict__ src,
+                                                           float *__restrict__ dst, int C, long HW,
+                                                           const double *__restrict__ det_scale) {
+  __shared__ float t[32][33];
+  const double inv = det_scale ? 1.0 / *det_scale : 1.0;
+  const int n = blockIdx.z;
+  const long s0 = (long)blockIdx.x * 32;
+  const int c0 = blockIdx.y * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const T *sn = src + (long)n * HW * C;
+  float *dn = dst + (long)n * C * HW;
+  for (int r = ty; r < 32; r += 8) {
+    const long sp = s0 + r;
+    float v = 0.f;
+    if (sp < HW && c0 + tx < C) {
+      if constexpr (sizeof(T) == 8)
+        v = (float)((double)sn[sp * C + c0 + tx] * inv);
+      else
+        v = sn[sp * C + c0 + tx];
+    }
+    t[r][tx] = v;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int c = c0 + r;
+    if (c < C && s0 + tx < HW) dn[(long)c * HW + s0 + tx] = t[tx][r];
+  }
 }
 
 int check_shapes(const MdcnArgs &a) {
@@ -1679,14 +1758,6 @@ __global__ void det_scale_kernel(const unsigned *__restrict__ bounds, double *__
   const double b = (double)__uint_as_float(bounds[0]) * (double)__uint_as_float(bounds[1]) *
                    (double)__uint_as_float(bounds[2]);
   *scale = (b > 0.0 && isfinite(b)) ? ldexp(1.0, 38 - (int)ceil(log2(b))) : 1.0;
-}
-
-__global__ __launch_bounds__(256) void det_convert_kernel(const long long *__restrict__ gxi,
-                                                          float *__restrict__ gx, long n,
-                                                          const double *__restrict__ scale) {
-  const double inv = 1.0 / *scale;
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256)
-    gx[e] = (float)((double)gxi[e] * inv);
 }
 
 __global__ __launch_bounds__(256) void det_weight_reduce_kernel(const float *__restrict__ part,
@@ -2000,6 +2071,12 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
   const BwdPlan pl = bwd_plan(a);
   DetLayout L{};
   char *wb = static_cast<char *>(ws);
+  // det: 0 float atomics into grad_x (NCHW); 1 deterministic (fixed point, workspace);
+  // 2 float atomics into an NHWC workspace of n*h*w*c floats, then transposed into grad_x
+  // (the deterministic form always scatters into its fixed-point accumulator in NHWC order)
+  const int nhs = det != 0;
+  det = det == 1;
+  if (nhs && !det && (!ws || ws_bytes < (size_t)n * c * h * w * sizeof(float))) return AANET_EINVAL;
   if (det) {
     L = det_layout(a, pl);
     if (!ws || ws_bytes < L.total) return AANET_EINVAL;
@@ -2023,34 +2100,47 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
                        dim3(256), 0, st, mask, nm, bounds + 2);
     hipLaunchKernelGGL(det_scale_kernel, dim3(1), dim3(1), 0, st, bounds, scale);
   } else {
-    e = hipMemsetAsync(grad_x, 0, sizeof(float) * nx, st);
+    e = hipMemsetAsync(nhs ? ws : grad_x, 0, sizeof(float) * nx, st);  // float atomics
     if (e != hipSuccess) return (int)e;
   }
   const int GP = round_pitch(PT, 16), WTP = round_pitch(co, 2);
-  const size_t smem = sizeof(float) * ((size_t)co * GP + (size_t)KC * WTP + (size_t)KC * CP + 3 * 4 * 64);
+  const size_t smem = sizeof(float) * ((size_t)co * GP + (size_t)KC * WTP + (size_t)KC * CP + 3 * 4 * 64 +
+                                      (size_t)PT * 12);
   // sG grows with Co (Co = 128 in the feature extractor's DCNs: ~69 KB); a gfx950 workgroup may
   // use the CU's whole 160 KiB of LDS
   if (smem > 160 * 1024) return AANET_EUNSUPPORTED;
   static const bool lds_attr = [] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_kernel<0>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_kernel<1>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_kernel<1, 1>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_kernel<0, 1>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
   (void)lds_attr;
   const dim3 gdata((unsigned)(n * host_div_up(P, PT)), (unsigned)dg);
   if (det)
-    hipLaunchKernelGGL(mdcn_bwd_data_kernel<1>, gdata, dim3(NT), smem, st, a, grad_out, grad_x,
+    hipLaunchKernelGGL((mdcn_bwd_data_kernel<1, 1>), gdata, dim3(NT), smem, st, a, grad_out, grad_x,
                        grad_offset, grad_mask, GP, WTP, gxi, scale);
+  else if (nhs)
+    hipLaunchKernelGGL((mdcn_bwd_data_kernel<0, 1>), gdata, dim3(NT), smem, st, a, grad_out,
+                       static_cast<float *>(ws), grad_offset, grad_mask, GP, WTP, nullptr, nullptr);
   else
     hipLaunchKernelGGL(mdcn_bwd_data_kernel<0>, gdata, dim3(NT), smem, st, a, grad_out, grad_x,
                        grad_offset, grad_mask, GP, WTP, nullptr, nullptr);
   rc = aanet_launch_status();
   if (rc) return rc;
-  if (det) {
-    hipLaunchKernelGGL(det_convert_kernel, dim3(host_div_up((long)nx, 256) > 8192 ? 8192 : host_div_up((long)nx, 256)),
-                       dim3(256), 0, st, gxi, grad_x, (long)nx, scale);
+  {
+    const long HW = (long)h * w;
+    const dim3 gt((unsigned)host_div_up(HW, 32), (unsigned)host_div_up(c, 32), (unsigned)n);
+    if (det)
+      hipLaunchKernelGGL(nhwc_to_nchw_kernel<long long>, gt, dim3(256), 0, st, gxi, grad_x, c, HW, scale);
+    else if (nhs)
+      hipLaunchKernelGGL(nhwc_to_nchw_kernel<float>, gt, dim3(256), 0, st,
+                         static_cast<const float *>(ws), grad_x, c, HW, nullptr);
+    rc = aanet_launch_status();
+    if (rc) return rc;
   }
   const dim3 gw3(pl.nchunks, (unsigned)pl.nsplit, host_div_up(co, 64));
   if (det)
@@ -2086,6 +2176,27 @@ extern "C" int aanet_mdcn_bwd_f32(const float *x, const float *offset, const flo
   return mdcn_bwd_impl(x, offset, mask, weight, grad_out, grad_x, grad_offset, grad_mask,
                        grad_weight, grad_bias, n, c, h, w, co, kh, kw, stride, pad, dil, groups,
                        dg, 0, nullptr, 0, as_hip(stream));
+}
+
+extern "C" size_t aanet_mdcn_bwd_ws_workspace_size(int n, int c, int h, int w, int co, int kh,
+                                                   int kw, int stride, int pad, int dil,
+                                                   int groups, int dg) {
+  MdcnArgs a = make_args(nullptr, nullptr, -1, nullptr, -1, 0, 1.f, nullptr, nullptr, nullptr,
+                         nullptr, 0, nullptr, n, c, h, w, co, kh, kw, stride, pad, dil, groups, dg);
+  if (check_shapes(a)) return 0;
+  return (size_t)n * c * h * w * sizeof(float);
+}
+
+extern "C" int aanet_mdcn_bwd_ws_f32(const float *x, const float *offset, const float *mask,
+                                     const float *weight, const float *grad_out, float *grad_x,
+                                     float *grad_offset, float *grad_mask, float *grad_weight,
+                                     float *grad_bias, int n, int c, int h, int w, int co, int kh,
+                                     int kw, int stride, int pad, int dil, int groups, int dg,
+                                     void *workspace, size_t workspace_bytes,
+                                     aanet_stream_t stream) {
+  return mdcn_bwd_impl(x, offset, mask, weight, grad_out, grad_x, grad_offset, grad_mask,
+                       grad_weight, grad_bias, n, c, h, w, co, kh, kw, stride, pad, dil, groups,
+                       dg, 2, workspace, workspace_bytes, as_hip(stream));
 }
 
 extern "C" size_t aanet_mdcn_bwd_det_workspace_size(int n, int c, int h, int w, int co, int kh,

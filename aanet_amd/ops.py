@@ -345,8 +345,11 @@ def csa_sum(inputs, act="leaky"):
 
 
 def mdcn_backward(x, offset, mask, weight, grad_out, with_bias, stride, padding, dilation, groups,
-                  deformable_groups, deterministic=None):
+                  deformable_groups, deterministic=None, nchw_scatter=False):
     """deform_conv_cuda.cpp:571-685 -> (gX, gOffset, gMask, gW, gB or None).
+
+    Default: aanet_mdcn_bwd_ws_f32 (grad_x float atomics into an NHWC workspace, then
+    transposed); nchw_scatter=True: the workspace-free aanet_mdcn_bwd_f32.
 
     deterministic (default: torch.are_deterministic_algorithms_enabled()): the bit-reproducible
     form (aanet_mdcn_bwd_det_f32: fixed-point grad_x accumulation, ordered grad_W reduction)
@@ -371,9 +374,19 @@ def mdcn_backward(x, offset, mask, weight, grad_out, with_bias, stride, padding,
              ptr(gx), ptr(goff), ptr(gm), ptr(gw), ptr(gb), N, C, H, W, Co, kh, kw, stride,
              padding, dilation, groups, deformable_groups, ptr(ws), nbytes, stream_of(x))
         return gx, goff, gm, gw, gb
-    call("aanet_mdcn_bwd_f32", ptr(x), ptr(offset), ptr(mask), ptr(weight), ptr(grad_out), ptr(gx),
-         ptr(goff), ptr(gm), ptr(gw), ptr(gb), N, C, H, W, Co, kh, kw, stride, padding, dilation,
-         groups, deformable_groups, stream_of(x))
+    if nchw_scatter:  # the workspace-free entry point (grad_x atomics in NCHW)
+        call("aanet_mdcn_bwd_f32", ptr(x), ptr(offset), ptr(mask), ptr(weight), ptr(grad_out),
+             ptr(gx), ptr(goff), ptr(gm), ptr(gw), ptr(gb), N, C, H, W, Co, kh, kw, stride, padding,
+             dilation, groups, deformable_groups, stream_of(x))
+        return gx, goff, gm, gw, gb
+    nbytes = _lib.lib().aanet_mdcn_bwd_ws_workspace_size(N, C, H, W, Co, kh, kw, stride, padding,
+                                                         dilation, groups, deformable_groups)
+    if nbytes == 0:
+        raise ValueError("aanet_mdcn_bwd_ws_workspace_size: invalid shape")
+    ws = torch.empty((nbytes,), device=x.device, dtype=torch.uint8)
+    call("aanet_mdcn_bwd_ws_f32", ptr(x), ptr(offset), ptr(mask), ptr(weight), ptr(grad_out),
+         ptr(gx), ptr(goff), ptr(gm), ptr(gw), ptr(gb), N, C, H, W, Co, kh, kw, stride, padding,
+         dilation, groups, deformable_groups, ptr(ws), nbytes, stream_of(x))
     return gx, goff, gm, gw, gb
 
 

@@ -60,6 +60,9 @@ def parse():
                     help="time the full model (features + hot path + refinement) instead")
     ap.add_argument("--exact-f32", action="store_true",
                     help="conv engine on exact f32 MFMA instead of the split-bf16 contraction")
+    ap.add_argument("--dcn-sweep", action="store_true",
+                    help="C4: deform_conv2d forward + backward microbench over the aggregation / "
+                         "feature-extractor DCN shapes (secondary lines, not the headline)")
     ap.add_argument("--only", default=None,
                     help="profiling mode: run only one kernel family (corr|mdcn|regress|step)")
     return ap.parse_args()
@@ -213,22 +216,34 @@ def conv_peak():
     return FP32_MFMA_PEAK_TF if _lib.conv_flags() else SPLIT_PEAK_TF
 
 
+CPU_SAMPLE_S = 12.0  # seconds of CPU work in the cpu_baseline sample
+
+
 def cpu_baseline(model, left, right, gpu_disp):
-    """Time the CPU oracle (restated reference path) on ONE pair; also EPE vs the GPU output."""
+    """Time the CPU oracle (restated reference path) on a bounded sample of the batch's pairs
+    (pairs 0, 1, ... cyclically until >= CPU_SAMPLE_S seconds of CPU work, at least 2 pairs);
+    also EPE of the GPU output vs the oracle on pair 0."""
     from oracle import aggregation as oagg
     threads = torch.get_num_threads()
     sd = {k: v.detach().cpu().numpy() for k, v in model.aggregation.state_dict().items()}
-    lp = [t[:1].cpu().numpy() for t in left]
-    rp = [t[:1].cpu().numpy() for t in right]
+    B = left[0].shape[0]
+    pairs = [([t[i:i + 1].cpu().numpy() for t in left], [t[i:i + 1].cpu().numpy() for t in right])
+             for i in range(B)]
+    n, ref = 0, None
     t0 = time.perf_counter()
-    ref = oagg.hot_path(lp, rp, sd, MAXD, intermediate_supervision=False)[0]
+    while n < 2 or time.perf_counter() - t0 < CPU_SAMPLE_S:
+        lp, rp = pairs[n % B]
+        r = oagg.hot_path(lp, rp, sd, MAXD, intermediate_supervision=False)[0]
+        if n == 0:
+            ref = r
+        n += 1
     dt = time.perf_counter() - t0
     ours = gpu_disp[:1].cpu().numpy()
     diff = np.abs(ours.astype(np.float64) - ref.astype(np.float64))
-    return dict(value=1.0 / dt, unit="stereo-pairs/s", cores=threads, kind="port",
-                sample="1 pair of the C2 workload (features 128x128x416 pyramid, D=64): "
-                       "oracle/ C restatement (cost volume, DCN, regression) + torch-CPU convs",
-                seconds=dt), float(diff.mean()), float(diff.max())
+    return dict(value=n / dt, unit="stereo-pairs/s", cores=threads, kind="port",
+                sample=f"{n} pairs of the C2 workload (features 128x128x416 pyramid, D=64), "
+                       f"{dt:.1f} s: oracle/ C restatement (cost volume, DCN, regression) + "
+                       "torch-CPU convs", seconds=dt), float(diff.mean()), float(diff.max())
 
 
 def timed_run(step, args, world):
@@ -287,6 +302,9 @@ def main():
         return
     if args.model:
         model_main(args, device, rank, world)
+        return
+    if args.dcn_sweep:
+        dcn_sweep_main(args, device, rank)
         return
     model = build_model(device)
     left, right = make_features(args.batch, rank, device, args.features)
@@ -354,6 +372,60 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+# (name, C, H, W, stride) -- the AdaptiveAggregation DCN at its three scales
+# (C2 sizes) and AANetFeature layer3's DeformBottleneck DCNs (128 ch at 1/12, stride 1 and 2).
+# All deformable_groups=2, 3x3, dilation 2, padding 2, no bias (nets/deform.py:17-45).
+DCN_SHAPES = [("agg_s0", 64, 128, 416, 1), ("agg_s1", 32, 64, 208, 1), ("agg_s2", 16, 32, 104, 1),
+              ("feat_s1", 128, 32, 104, 1), ("feat_s2", 128, 64, 208, 2)]
+
+
+def dcn_sweep_main(args, device, rank):
+    """C4 microbench: the drop-in modulated DCN entry points (aanet_mdcn_fwd_f32 = the reference's
+    modulated_deform_conv_cuda_forward; aanet_mdcn_bwd_f32 / _det_f32 = ..._backward) per shape,
+    B=--batch, offsets N(0, 0.5^2) (fractional, some out of the image), mask U(0, 1).
+    Flops: forward 2*B*Ho*Wo*Co*C*9 (the MFMA contraction; bilinear lerps excluded); backward
+    counts dgrad + wgrad contractions (2x the forward).  One JSON line per shape on rank 0, then
+    the num_scales 1 / 3 aggregation totals."""
+    from aanet_amd import ops
+    B, dg, k, dil, pad = args.batch, 2, 3, 2, 2
+    gen = torch.Generator(device=device).manual_seed(1234 + rank)
+    stream = torch.cuda.current_stream()
+    iters = max(args.kernel_iters, 5)
+    tot = {}
+    for name, C, H, W, stride in DCN_SHAPES:
+        Ho, Wo = (H + 2 * pad - dil * (k - 1) - 1) // stride + 1, (W + 2 * pad - dil * (k - 1) - 1) // stride + 1
+        x = torch.randn((B, C, H, W), device=device, generator=gen)
+        off = 0.5 * torch.randn((B, 2 * dg * k * k, Ho, Wo), device=device, generator=gen)
+        mask = torch.rand((B, dg * k * k, Ho, Wo), device=device, generator=gen)
+        w = 0.05 * torch.randn((C, C, k, k), device=device, generator=gen)
+        out = torch.empty((B, C, Ho, Wo), device=device)
+        go = torch.randn((B, C, Ho, Wo), device=device, generator=gen)
+        fwd = lambda: ops.mdcn_forward(x, off, mask, w, None, stride, pad, dil, 1, dg, out=out)  # noqa: E731
+        bwd = lambda: ops.mdcn_backward(x, off, mask, w, go, False, stride, pad, dil, 1, dg,  # noqa: E731
+                                        deterministic=False)
+        bwd_det = lambda: ops.mdcn_backward(x, off, mask, w, go, False, stride, pad, dil, 1, dg,  # noqa: E731
+                                            deterministic=True)
+        flops = 2.0 * B * Ho * Wo * C * C * k * k
+        ms_f, ms_b, ms_d = (time_events(f, iters, stream) for f in (fwd, bwd, bwd_det))
+        line = {"bench": "dcn_sweep (C4)", "shape": name, "input": [B, C, H, W], "stride": stride,
+                "deformable_groups": dg, "dilation": dil, "fwd_us": ms_f * 1e3, "bwd_us": ms_b * 1e3,
+                "bwd_det_us": ms_d * 1e3,
+                "fwd_tflops": flops / ms_f / 1e9, "bwd_tflops": 2 * flops / ms_b / 1e9,
+                "fwd_frac_f32_mfma": flops / ms_f / 1e9 / FP32_MFMA_PEAK_TF,
+                "bwd_frac_f32_mfma": 2 * flops / ms_b / 1e9 / FP32_MFMA_PEAK_TF,
+                "data": "synthetic", "dtype": "f32"}
+        tot[name] = (ms_f, ms_b)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+    if rank == 0:
+        for ns, names in ((1, ["agg_s0"]), (3, ["agg_s0", "agg_s1", "agg_s2"])):
+            f = sum(tot[n][0] for n in names)
+            b = sum(tot[n][1] for n in names)
+            print(json.dumps({"bench": "dcn_sweep (C4)", "num_scales": ns, "fwd_us": f * 1e3,
+                              "fwd_bwd_us": (f + b) * 1e3, "per_module": "one DCN per scale"}),
+                  flush=True)
 
 
 FULL_MODELS = {

@@ -222,6 +222,18 @@ int aanet_mdcn_bwd_f32(const float *x, const float *offset, const float *mask, c
                        int kh, int kw, int stride, int pad, int dil, int groups, int dg,
                        aanet_stream_t stream);
 
+/* Faster form of aanet_mdcn_bwd_f32 (same contract, float atomics): grad_x is scattered into a
+ * caller-owned NHWC workspace (coalesced 128-byte atomic lines) and then transposed into grad_x.
+ * `workspace` (device) must hold aanet_mdcn_bwd_ws_workspace_size(...) = n*c*h*w*4 bytes. */
+size_t aanet_mdcn_bwd_ws_workspace_size(int n, int c, int h, int w, int co, int kh, int kw,
+                                        int stride, int pad, int dil, int groups, int dg);
+int aanet_mdcn_bwd_ws_f32(const float *x, const float *offset, const float *mask,
+                          const float *weight, const float *grad_out, float *grad_x,
+                          float *grad_offset, float *grad_mask, float *grad_weight,
+                          float *grad_bias, int n, int c, int h, int w, int co, int kh, int kw,
+                          int stride, int pad, int dil, int groups, int dg, void *workspace,
+                          size_t workspace_bytes, aanet_stream_t stream);
+
 /* Deterministic form of aanet_mdcn_bwd_f32 (same contract, bit-reproducible run to run):
  *   - grad_x: 64-bit fixed-point atomics. Integer adds are associative, so the sum does not
  *     depend on atomic ordering. The fixed-point scale is a power of two chosen on the device from

@@ -152,6 +152,24 @@ def test_mdcn_backward_vs_oracle(case, off_scale, deterministic):
         assert err.max() <= 1e-4 * scale + 1e-6, f"{name}: max err {err.max():.3g} (scale {scale:.3g})"
 
 
+@pytest.mark.parametrize("case", BWD_CASES)
+@pytest.mark.parametrize("nchw_scatter", [False, True])
+def test_mdcn_backward_entry_points_vs_oracle(case, nchw_scatter):
+    """Both float-atomic entry points: aanet_mdcn_bwd_ws_f32 (NHWC workspace scatter + transpose,
+    the default) and the workspace-free aanet_mdcn_bwd_f32 (NCHW scatter)."""
+    N, C, H, W, Co, k, s, p, d, dg = case
+    x, off, msk, w, b = make_case(7, N, C, H, W, Co, k, s, p, d, dg, off_scale=1.3)
+    Ho, Wo = off.shape[2:]
+    go = np.random.default_rng(8).standard_normal((N, Co, Ho, Wo)).astype(np.float32)
+    got = ops.mdcn_backward(g2t(x), g2t(off), g2t(msk), g2t(w), g2t(go), True, s, p, d, 1, dg,
+                            deterministic=False, nchw_scatter=nchw_scatter)
+    ref = oracle.mdcn_backward(x, off, msk, w, go, True, s, p, d, 1, dg)
+    for name, gt, r in zip(("grad_input", "grad_offset", "grad_mask", "grad_weight", "grad_bias"), got, ref):
+        err = np.abs(t2n(gt) - r)
+        scale = np.abs(r).max() + 1e-12
+        assert err.max() <= 1e-4 * scale + 1e-6, f"{name}: max err {err.max():.3g} (scale {scale:.3g})"
+
+
 def test_deform_conv_cuda_shim_matches_reference_call_sequence():
     """The pybind-compatible module, called exactly as nets/deform_conv/deform_conv.py:140-166
     calls deform_conv_cuda (in-place output, zeroed grads, vestigial bufs)."""
