@@ -1390,6 +1390,195 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_kernel(MdcnArgs a, const flo
   }
 }
 
+// (1b) the same data/coordinate gradients from channels-last copies: x as [N][H*W][C] and the
+// weight as wT[k][c][co] (both made by the launcher into the workspace), for C % 4 == 0 and
+// C/dg % 4 == 0.  Workgroup = (image n, 64-pixel tile, deformable group g).  Per (tap, chunk):
+//  - the W^T chunk is staged with coalesced rows of wT, colg = W^T gOut by MFMA into LDS;
+//  - offset/mask partials: thread = (pixel, channel quad), each corner one 16-byte load of 4
+//    channels (8 lanes = one 128-B line of a corner), reduced over the 8 quads by shuffles;
+//  - grad_x: lanes on 32 consecutive channels of a corner, atomics into the NHWC accumulator.
+template <int DET>
+__global__ __launch_bounds__(NT) void mdcn_bwd_data_nhwc_kernel(MdcnArgs a, const float *__restrict__ xh,
+                                                                const float *__restrict__ wT,
+                                                                const float *__restrict__ gout,
+                                                                float *__restrict__ gx,
+                                                                float *__restrict__ goff,
+                                                                float *__restrict__ gmask, int GP,
+                                                                int WTP, long long *__restrict__ gxi,
+                                                                const double *__restrict__ det_scale) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int Co = a.Co;
+  float *sG = sm;                       // [Co][GP]      gOut tile
+  float *sWt = sG + Co * GP;            // [KC][WTP]     W^T chunk
+  float *sCg = sWt + KC * WTP;          // [KC][CP]      colg chunk
+  float *sS = sCg + KC * CP;            // [PT][12]      per-pixel corners, weights, mask, fractions
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long P = (long)a.Ho * a.Wo;
+  const int ntiles = (int)((P + PT - 1) / PT);
+  const int n = blockIdx.x / ntiles, tile = blockIdx.x % ntiles, g = blockIdx.y;
+  const int K = a.kh * a.kw, cpg = a.C / a.dg, C = a.C;
+  const long HW = (long)a.H * a.W;
+  const double scale = DET ? *det_scale : 1.0;
+  const float *xn = xh + (long)n * HW * C;
+
+  for (int e = tid; e < Co * PT; e += NT) {
+    const int co = e / PT, pl = e % PT;
+    const long pp = (long)tile * PT + pl;
+    sG[co * GP + pl] = pp < P ? gout[((long)n * Co + co) * P + pp] : 0.f;
+  }
+  const int kr = lane >> 4, jj = lane & 15;
+  const int q = tid & 7;  // channel quad of the gradient role; pixels (tid >> 3) + 32 it
+  for (int k = 0; k < K; ++k) {
+    if (k) __syncthreads();  // every wave is done scattering tap k-1 (it reads sS)
+    if (wave == 0) {  // published for the chunk loop (its first barrier orders it)
+#pragma clang fp contract(off)
+      const long p = (long)tile * PT + lane;
+      const bool pvalid = p < P;
+      Samp s;
+      pixel_samp(s, a, n, g, k, pvalid ? p : 0, pvalid ? (int)(p / a.Wo) : 0, pvalid ? (int)(p % a.Wo) : 0);
+      const bool on = pvalid && s.valid;
+      const float hh = 1.f - s.lh, hw = 1.f - s.lw;
+      float *qq = sS + lane * 12;
+      qq[0] = __builtin_bit_cast(float, on && (s.ok & 1) ? s.i1 : -1);
+      qq[1] = __builtin_bit_cast(float, on && (s.ok & 2) ? s.i2 : -1);
+      qq[2] = __builtin_bit_cast(float, on && (s.ok & 4) ? s.i3 : -1);
+      qq[3] = __builtin_bit_cast(float, on && (s.ok & 8) ? s.i4 : -1);
+      qq[4] = hh * hw, qq[5] = hh * s.lw, qq[6] = s.lh * hw, qq[7] = s.lh * s.lw;
+      qq[8] = s.m, qq[9] = s.lh, qq[10] = s.lw, qq[11] = on ? 1.f : 0.f;
+    }
+    float gm[2] = {0.f, 0.f}, goh[2] = {0.f, 0.f}, gow[2] = {0.f, 0.f};
+    for (int c0 = g * cpg; c0 < (g + 1) * cpg; c0 += KC) {
+      const int rows = min(KC, (g + 1) * cpg - c0);
+      __syncthreads();  // previous chunk's sCg / sWt readers are done
+      for (int e = tid; e < KC * Co; e += NT) {
+        const int co = e % Co, cl = e / Co;
+        sWt[cl * WTP + co] = cl < rows ? wT[((long)k * C + c0 + cl) * Co + co] : 0.f;
+      }
+      __syncthreads();
+      f32x4 cacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      for (int ks = 0; ks < Co / 4; ++ks) {
+        const float bv = sG[(4 * ks + kr) * GP + 16 * wave + jj];
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const float av = sWt[(16 * cb + jj) * WTP + 4 * ks + kr];
+          cacc[cb] = mfma16x16x4(av, bv, cacc[cb]);
+        }
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sCg[(16 * cb + 4 * kr + r) * CP + 16 * wave + jj] = cacc[cb][r];
+      __syncthreads();
+      // offset / mask partials: (pixel, channel quad)
+      if (4 * q < rows) {
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+#pragma clang fp contract(off)
+          const int px = (tid >> 3) + 32 * it;
+          const float *qq = sS + px * 12;
+          const f32x4 qi = *reinterpret_cast<const f32x4 *>(qq);
+          const float qi0 = qi[0], qi1 = qi[1], qi2 = qi[2], qi3 = qi[3];
+          const int i1 = __builtin_bit_cast(int, qi0), i2 = __builtin_bit_cast(int, qi1);
+          const int i3 = __builtin_bit_cast(int, qi2), i4 = __builtin_bit_cast(int, qi3);
+          const float m = qq[8], lh = qq[9], lw = qq[10];
+          const float hh = 1.f - lh, hw = 1.f - lw;
+          const int cq = c0 + 4 * q;
+          const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+          const f32x4 v1 = i1 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i1 * C + cq) : z;
+          const f32x4 v2 = i2 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i2 * C + cq) : z;
+          const f32x4 v3 = i3 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i3 * C + cq) : z;
+          const f32x4 v4 = i4 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i4 * C + cq) : z;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float cg = sCg[(4 * q + u) * CP + px];
+            const float val = hh * hw * v1[u] + hh * lw * v2[u] + lh * hw * v3[u] + lh * lw * v4[u];
+            gm[it] += cg * val;
+            const float wh = -hw * v1[u] - lw * v2[u] + hw * v3[u] + lw * v4[u];
+            const float ww = -hh * v1[u] + hh * v2[u] - lh * v3[u] + lh * v4[u];
+            const float top = cg * m;
+            goh[it] += wh * top;
+            gow[it] += ww * top;
+          }
+        }
+      }
+      // grad_x: lanes 0-31 channel cl of pixel 16w + 2t, lanes 32-63 of pixel 16w + 2t + 1
+      const int cl = lane & 31;
+      if (cl < rows) {
+        const long cbase = (long)n * HW * C + c0 + cl;
+        auto nadd = [&](int i, float v) {
+          if (DET)
+            atomicAdd(reinterpret_cast<unsigned long long *>(gxi + cbase + (long)i * C),
+                      (unsigned long long)__double2ll_rn((double)v * scale));
+          else
+            atomicAdd(gx + cbase + (long)i * C, v);
+        };
+#pragma unroll 2
+        for (int t = 0; t < 8; ++t) {
+#pragma clang fp contract(off)
+          const int px = 16 * wave + 2 * t + (lane >> 5);
+          const float *qq = sS + px * 12;
+          const f32x4 qi = *reinterpret_cast<const f32x4 *>(qq);
+          const f32x4 qw = *reinterpret_cast<const f32x4 *>(qq + 4);
+          const float top = sCg[cl * CP + px] * qq[8];
+          const float qi0 = qi[0], qi1 = qi[1], qi2 = qi[2], qi3 = qi[3];
+          const int i1 = __builtin_bit_cast(int, qi0), i2 = __builtin_bit_cast(int, qi1);
+          const int i3 = __builtin_bit_cast(int, qi2), i4 = __builtin_bit_cast(int, qi3);
+          if (i1 >= 0) nadd(i1, qw[0] * top);
+          if (i2 >= 0) nadd(i2, qw[1] * top);
+          if (i3 >= 0) nadd(i3, qw[2] * top);
+          if (i4 >= 0) nadd(i4, qw[3] * top);
+        }
+      }
+    }
+    // reduce the 8 channel quads of each pixel (lanes 8j .. 8j+7), fixed order
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+#pragma unroll
+      for (int msk = 1; msk < 8; msk <<= 1) {
+        gm[it] += __shfl_xor(gm[it], msk);
+        goh[it] += __shfl_xor(goh[it], msk);
+        gow[it] += __shfl_xor(gow[it], msk);
+      }
+      const long p = (long)tile * PT + (tid >> 3) + 32 * it;
+      if (q == 0 && p < P) {
+        const long ob = (long)n * a.dg * 2 * K * P + (long)g * 2 * K * P;
+        goff[ob + (long)(2 * k) * P + p] = goh[it];
+        goff[ob + (long)(2 * k + 1) * P + p] = gow[it];
+        gmask[(long)n * a.dg * K * P + ((long)g * K + k) * P + p] = gm[it];
+      }
+    }
+  }
+}
+
+// x [N][C][HW] -> [N][HW][C] and w [Co][C][K] -> wT [K][C][Co] (inputs of mdcn_bwd_data_nhwc_kernel)
+__global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float *__restrict__ src,
+                                                           float *__restrict__ dst, int C, long HW) {
+  __shared__ float t[32][33];
+  const int n = blockIdx.z;
+  const long s0 = (long)blockIdx.x * 32;
+  const int c0 = blockIdx.y * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const float *sn = src + (long)n * C * HW;
+  float *dn = dst + (long)n * HW * C;
+  for (int r = ty; r < 32; r += 8) {
+    const int c = c0 + r;
+    t[r][tx] = (c < C && s0 + tx < HW) ? sn[(long)c * HW + s0 + tx] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const long sp = s0 + r;
+    if (sp < HW && c0 + tx < C) dn[sp * C + c0 + tx] = t[tx][r];
+  }
+}
+
+__global__ __launch_bounds__(256) void weight_kcco_kernel(const float *__restrict__ w,
+                                                          float *__restrict__ wT, int Co, int C, int K) {
+  const long n = (long)Co * C * K;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int co = (int)(e % Co), c = (int)((e / Co) % C), k = (int)(e / ((long)Co * C));
+    wT[e] = w[((long)co * C + c) * K + k];
+  }
+}
+
 // (2) weight gradient: gW[co][c][k] += sum_{n,p} gOut[n][co][p] * col[c*K+k][n,p].
 // Workgroup = one K chunk (tap k, <=32 channels of group g) x one range of pixels (all
 // images flattened) x one 64-wide output-channel tile.  The col chunk is re-sampled into LDS
@@ -1397,10 +1586,13 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_kernel(MdcnArgs a, const flo
 // pixel range, then one float atomic per element (grad accumulates, cpp:660-669).
 // DET: each pixel-range split writes its partial sums to part[split][co][c][k] (no atomics);
 // det_weight_reduce_kernel adds them to grad_weight in split order.
-template <int DET>
+// NR: the col chunk is sampled from the channels-last copy xh [N][H*W][C] (C, C/dg % 4 == 0):
+// thread = (pixel, channel quad), one 16-byte load per corner (8 lanes = one 128-B line).
+template <int DET, int NR = 0>
 __global__ __launch_bounds__(NT) void mdcn_bwd_weight_kernel(MdcnArgs a, const float *__restrict__ gout,
                                                              float *__restrict__ gw, int npieces,
-                                                             long range, float *__restrict__ part) {
+                                                             long range, float *__restrict__ part,
+                                                             const float *__restrict__ xh = nullptr) {
   constexpr int GP2 = PT + 2;  // A/B reads (16 rows x 4 cols per 16 lanes) conflict-free
   __shared__ __attribute__((aligned(16))) float sG[64 * GP2];
   __shared__ __attribute__((aligned(16))) float sC[KC * GP2];
@@ -1418,6 +1610,33 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_weight_kernel(MdcnArgs a, const f
   // wave w: output-channel block w (16 co), both 16-channel blocks of the chunk
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   for (long t0 = r0; t0 < r1; t0 += PT) {
+    if constexpr (NR) {
+      const int q = tid & 7;
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int pl = (tid >> 3) + 32 * it;
+        const long t = t0 + pl;
+        const bool tv = t < r1;
+        const int n = tv ? (int)(t / P) : 0;
+        const long p = tv ? t % P : 0;
+        Samp s;
+        pixel_samp(s, a, n, g, k, p, (int)(p / a.Wo), (int)(p % a.Wo));
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (tv && 4 * q < rows) {
+#pragma clang fp contract(off)
+          const float *xq = xh + (long)n * HW * C + c0 + 4 * q;
+          const f32x4 v1 = *reinterpret_cast<const f32x4 *>(xq + (long)s.i1 * C);
+          const f32x4 v2 = *reinterpret_cast<const f32x4 *>(xq + (long)s.i2 * C);
+          const f32x4 v3 = *reinterpret_cast<const f32x4 *>(xq + (long)s.i3 * C);
+          const f32x4 v4 = *reinterpret_cast<const f32x4 *>(xq + (long)s.i4 * C);
+#pragma unroll
+          for (int u = 0; u < 4; ++u)  // samp_val per channel (same products and order)
+            v[u] = (s.w1 * v1[u] + s.w2 * v2[u] + s.w3 * v3[u] + s.w4 * v4[u]) * s.m;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sC[(4 * q + u) * GP2 + pl] = v[u];
+      }
+    } else {
     const long t = t0 + lane;
     const bool tv = t < r1;
     const int n = tv ? (int)(t / P) : 0;
@@ -1431,6 +1650,7 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_weight_kernel(MdcnArgs a, const f
       float v = 0.f;
       if (cl < rows && tv) v = samp_val(xn + (long)(c0 + cl) * HW, s);
       sC[cl * GP2 + lane] = v;
+    }
     }
     for (int e = tid; e < 64 * PT; e += NT) {
       const int col = e / PT, pl = e % PT;
@@ -2036,7 +2256,7 @@ BwdPlan bwd_plan(const MdcnArgs &a) {
 
 // Deterministic-backward workspace: [grad_x as int64][weight partials][bounds, scale]
 struct DetLayout {
-  size_t gxi, part, bounds, scale, total;
+  size_t gxi, part, bounds, scale, xh, wt, total;
 };
 
 DetLayout det_layout(const MdcnArgs &a, const BwdPlan &pl) {
@@ -2048,9 +2268,26 @@ DetLayout det_layout(const MdcnArgs &a, const BwdPlan &pl) {
   L.part = up(L.gxi + nx * 8);
   L.bounds = up(L.part + (size_t)pl.nsplit * nw * 4);
   L.scale = L.bounds + 16;
-  L.total = up(L.scale + 8);
+  L.xh = up(L.scale + 8);  // channels-last x and wT[k][c][co] (mdcn_bwd_data_nhwc_kernel)
+  L.wt = up(L.xh + nx * 4);
+  L.total = up(L.wt + nw * 4);
   return L;
 }
+
+// Float-atomic workspace (aanet_mdcn_bwd_ws_f32): [grad_x NHWC accumulator][x NHWC][wT]
+DetLayout ws_layout(const MdcnArgs &a) {
+  auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+  DetLayout L{};
+  const size_t nx = (size_t)a.N * a.C * a.H * a.W;
+  const size_t nw = (size_t)a.Co * a.C * a.kh * a.kw;
+  L.gxi = 0;
+  L.xh = up(nx * 4);
+  L.wt = up(L.xh + nx * 4);
+  L.total = up(L.wt + nw * 4);
+  return L;
+}
+
+bool bwd_nhwc_reads(const MdcnArgs &a) { return a.C % 4 == 0 && (a.C / a.dg) % 4 == 0; }
 
 int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const float *weight,
                   const float *grad_out, float *grad_x, float *grad_offset, float *grad_mask,
@@ -2076,11 +2313,13 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
   // (the deterministic form always scatters into its fixed-point accumulator in NHWC order)
   const int nhs = det != 0;
   det = det == 1;
-  if (nhs && !det && (!ws || ws_bytes < (size_t)n * c * h * w * sizeof(float))) return AANET_EINVAL;
-  if (det) {
-    L = det_layout(a, pl);
+  if (det || nhs) {
+    L = det ? det_layout(a, pl) : ws_layout(a);
     if (!ws || ws_bytes < L.total) return AANET_EINVAL;
   }
+  const bool nr = nhs && bwd_nhwc_reads(a);  // channels-last reads too
+  float *xh = nhs ? reinterpret_cast<float *>(wb + L.xh) : nullptr;
+  float *wt = nhs ? reinterpret_cast<float *>(wb + L.wt) : nullptr;
   long long *gxi = det ? reinterpret_cast<long long *>(wb + L.gxi) : nullptr;
   float *part = det ? reinterpret_cast<float *>(wb + L.part) : nullptr;
   unsigned *bounds = det ? reinterpret_cast<unsigned *>(wb + L.bounds) : nullptr;
@@ -2116,16 +2355,35 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_kernel<0, 1>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_nhwc_kernel<0>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_nhwc_kernel<1>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
   (void)lds_attr;
   const dim3 gdata((unsigned)(n * host_div_up(P, PT)), (unsigned)dg);
-  if (det)
+  if (nr) {
+    const long HW = (long)h * w;
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3((unsigned)host_div_up(HW, 32), (unsigned)host_div_up(c, 32), (unsigned)n),
+                       dim3(256), 0, st, x, xh, c, HW);
+    const long nw = (long)co * c * K;
+    hipLaunchKernelGGL(weight_kcco_kernel, dim3(host_div_up(nw, 256) > 1024 ? 1024 : host_div_up(nw, 256)),
+                       dim3(256), 0, st, weight, wt, co, c, K);
+    const size_t smem2 = sizeof(float) * ((size_t)co * GP + (size_t)KC * WTP + (size_t)KC * CP + (size_t)PT * 12);
+    if (det)
+      hipLaunchKernelGGL(mdcn_bwd_data_nhwc_kernel<1>, gdata, dim3(NT), smem2, st, a, xh, wt, grad_out,
+                         grad_x, grad_offset, grad_mask, GP, WTP, gxi, scale);
+    else
+      hipLaunchKernelGGL(mdcn_bwd_data_nhwc_kernel<0>, gdata, dim3(NT), smem2, st, a, xh, wt, grad_out,
+                         reinterpret_cast<float *>(wb + L.gxi), grad_offset, grad_mask, GP, WTP,
+                         nullptr, nullptr);
+  } else if (det)
     hipLaunchKernelGGL((mdcn_bwd_data_kernel<1, 1>), gdata, dim3(NT), smem, st, a, grad_out, grad_x,
                        grad_offset, grad_mask, GP, WTP, gxi, scale);
   else if (nhs)
     hipLaunchKernelGGL((mdcn_bwd_data_kernel<0, 1>), gdata, dim3(NT), smem, st, a, grad_out,
-                       static_cast<float *>(ws), grad_offset, grad_mask, GP, WTP, nullptr, nullptr);
+                       reinterpret_cast<float *>(wb + L.gxi), grad_offset, grad_mask, GP, WTP, nullptr, nullptr);
   else
     hipLaunchKernelGGL(mdcn_bwd_data_kernel<0>, gdata, dim3(NT), smem, st, a, grad_out, grad_x,
                        grad_offset, grad_mask, GP, WTP, nullptr, nullptr);
@@ -2138,12 +2396,18 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
       hipLaunchKernelGGL(nhwc_to_nchw_kernel<long long>, gt, dim3(256), 0, st, gxi, grad_x, c, HW, scale);
     else if (nhs)
       hipLaunchKernelGGL(nhwc_to_nchw_kernel<float>, gt, dim3(256), 0, st,
-                         static_cast<const float *>(ws), grad_x, c, HW, nullptr);
+                         reinterpret_cast<const float *>(wb + L.gxi), grad_x, c, HW, nullptr);
     rc = aanet_launch_status();
     if (rc) return rc;
   }
   const dim3 gw3(pl.nchunks, (unsigned)pl.nsplit, host_div_up(co, 64));
-  if (det)
+  if (nr && det)
+    hipLaunchKernelGGL((mdcn_bwd_weight_kernel<1, 1>), gw3, dim3(NT), 0, st, a, grad_out, grad_weight,
+                       pl.npieces, pl.range, part, xh);
+  else if (nr)
+    hipLaunchKernelGGL((mdcn_bwd_weight_kernel<0, 1>), gw3, dim3(NT), 0, st, a, grad_out, grad_weight,
+                       pl.npieces, pl.range, nullptr, xh);
+  else if (det)
     hipLaunchKernelGGL(mdcn_bwd_weight_kernel<1>, gw3, dim3(NT), 0, st, a, grad_out, grad_weight,
                        pl.npieces, pl.range, part);
   else
@@ -2184,7 +2448,7 @@ extern "C" size_t aanet_mdcn_bwd_ws_workspace_size(int n, int c, int h, int w, i
   MdcnArgs a = make_args(nullptr, nullptr, -1, nullptr, -1, 0, 1.f, nullptr, nullptr, nullptr,
                          nullptr, 0, nullptr, n, c, h, w, co, kh, kw, stride, pad, dil, groups, dg);
   if (check_shapes(a)) return 0;
-  return (size_t)n * c * h * w * sizeof(float);
+  return ws_layout(a).total;
 }
 
 extern "C" int aanet_mdcn_bwd_ws_f32(const float *x, const float *offset, const float *mask,

@@ -63,6 +63,7 @@ def parse():
     ap.add_argument("--dcn-sweep", action="store_true",
                     help="C4: deform_conv2d forward + backward microbench over the aggregation / "
                          "feature-extractor DCN shapes (secondary lines, not the headline)")
+    ap.add_argument("--dcn-shapes", default=None, help="--dcn-sweep: comma-separated subset of DCN_SHAPES")
     ap.add_argument("--only", default=None,
                     help="profiling mode: run only one kernel family (corr|mdcn|regress|step)")
     return ap.parse_args()
@@ -394,7 +395,10 @@ def dcn_sweep_main(args, device, rank):
     stream = torch.cuda.current_stream()
     iters = max(args.kernel_iters, 5)
     tot = {}
+    pick = args.dcn_shapes.split(",") if args.dcn_shapes else None
     for name, C, H, W, stride in DCN_SHAPES:
+        if pick and name not in pick:
+            continue
         Ho, Wo = (H + 2 * pad - dil * (k - 1) - 1) // stride + 1, (W + 2 * pad - dil * (k - 1) - 1) // stride + 1
         x = torch.randn((B, C, H, W), device=device, generator=gen)
         off = 0.5 * torch.randn((B, 2 * dg * k * k, Ho, Wo), device=device, generator=gen)
@@ -421,6 +425,8 @@ def dcn_sweep_main(args, device, rank):
             print(json.dumps(line), flush=True)
     if rank == 0:
         for ns, names in ((1, ["agg_s0"]), (3, ["agg_s0", "agg_s1", "agg_s2"])):
+            if any(n not in tot for n in names):
+                continue
             f = sum(tot[n][0] for n in names)
             b = sum(tot[n][1] for n in names)
             print(json.dumps({"bench": "dcn_sweep (C4)", "num_scales": ns, "fwd_us": f * 1e3,
