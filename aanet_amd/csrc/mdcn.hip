@@ -642,10 +642,21 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
         if (MODE == 0) {
           v = nv[i];
         } else {
-          v = nc[i][0] * nw[i][0];
-          v = __builtin_elementwise_fma(nc[i][1], f32x4(nw[i][1]), v);
-          v = __builtin_elementwise_fma(nc[i][2], f32x4(nw[i][2]), v);
-          v = __builtin_elementwise_fma(nc[i][3], f32x4(nw[i][3]), v);
+          // Bilinear blend of the 4 corner quads: ((c0 w0 + c1 w1) + c2 w2) + c3 w3 per channel,
+          // as scalar v_mul/v_fma_f32 in asm.  The packed form the compiler picks for this
+          // (v_pk_fma_f32 with a broadcast weight) gave non-reproducible results in the split
+          // DCN tail kernel: pixels staged by lanes 48-63 read a stale broadcast weight register
+          // written by the VALU instruction just before (tools/diag_race3.py).
+          const float w0 = nw[i][0], w1 = nw[i][1], w2 = nw[i][2], w3 = nw[i][3];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            float t;
+            asm("v_mul_f32 %0, %1, %2" : "=v"(t) : "v"(nc[i][0][u]), "v"(w0));
+            asm("v_fma_f32 %0, %1, %2, %0" : "+v"(t) : "v"(nc[i][1][u]), "v"(w1));
+            asm("v_fma_f32 %0, %1, %2, %0" : "+v"(t) : "v"(nc[i][2][u]), "v"(w2));
+            asm("v_fma_f32 %0, %1, %2, %0" : "+v"(t) : "v"(nc[i][3][u]), "v"(w3));
+            v[u] = t;
+          }
         }
         if constexpr (SPL)
           put_split(sB, PTT * 32, npx[i], nq, v);
@@ -1828,11 +1839,10 @@ void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
         return;
       }
     }
-    // The deformable tail kernel with NHWC staging is excluded: on the split path it was not
-    // bit-reproducible run to run at C2 scale (B=8: ~1e3 of 2.7e7 outputs moved, only with
-    // fractional offsets; tests/test_gpu_split.py::test_fused_paths_bit_reproducible) -- the
-    // cause is not yet found, so that configuration runs the exact f32 contraction.
-    static const int allow_racy = [] { const char *e = getenv("AANET_SPLIT_DCN_TAIL"); return e ? atoi(e) : 0; }();
+    // AANET_SPLIT_DCN_TAIL=0: the deformable tail kernel with NHWC staging on the exact f32
+    // contraction (it ran so while its packed-fp32 corner blend was not reproducible, see the
+    // NHWC store_stage; A/B switch now)
+    static const int allow_racy = [] { const char *e = getenv("AANET_SPLIT_DCN_TAIL"); return e ? atoi(e) : 1; }();
     const bool racy = MODE == 1 && a.tail_w && a.layout == 1 && !allow_racy;
     if (a.split && packed && !racy) {
       if (a.tail_w) {

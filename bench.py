@@ -31,6 +31,7 @@ METRIC = "stereo-pairs/s @384x1248 D=64 fp32, 1/2/4/8 MI355X; EPE vs ref"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 = f32 vector rate
 BF16_DENSE_PEAK_TF = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
+L2_GATHER_GBPS = 17800.0     # MI355X_MICROARCH.md "Indexed rows": L2-served gather, 16.8-18.8 TB/s
 # The conv engine's split-bf16 contraction (include/aanet_mi355x.h AANET_CONV_EXACT_F32) runs an
 # fp32 MAC as six bf16 piece products on the matrix cores: its ceiling in fp32-equivalent FLOP/s
 # is the dense bf16 peak / 6.  The exact f32 engine (--exact-f32) is bounded by FP32_MFMA_PEAK_TF.
@@ -173,10 +174,15 @@ def kernel_rooflines(model, left, right, batch, iters):
     Co, Ci = dc.weight.shape[:2]
     Co2 = w3.shape[0]
     flops = 2.0 * B * H * W * (Co * Ci * 9 + Co2 * Co)
-    # (this NHWC deformable tail configuration runs the exact f32 contraction even when the
-    # split one is selected: mdcn.hip launch_fwd_f, "racy")
+    # the contraction runs on the engine's selected form (split-bf16 unless --exact-f32); its
+    # tighter bound is the corner gather: 9 taps x Ci channels x 4 corners x 4 B per output
+    # pixel, mostly L1/L2 hits, against the L2-served gather rate of MI355X_MICROARCH.md
+    gather = 4.0 * 4 * 9 * Ci * B * H * W
     res["mdcn_pw_s0"] = dict(bound="mfma", ms=ms, algo=flops, unit="TFLOP/s",
-                             achieved=flops / ms / 1e9, peak=FP32_MFMA_PEAK_TF)
+                             achieved=flops / ms / 1e9, peak=conv_peak(),
+                             gather={"bytes_per_launch": gather, "achieved_GBps": gather / ms / 1e6,
+                                     "peak_GBps": L2_GATHER_GBPS,
+                                     "frac": gather / ms / 1e6 / L2_GATHER_GBPS})
     # the plain-3x3 ISA bottleneck tail (SimpleBottleneck of fusion 0, scale 0): halo-tile conv2
     # + BN2 + ReLU -> conv3 + BN3 + identity + ReLU, with the scale-0 CSA sum
     blk0 = model.aggregation.fusions[0].branches[0][0]
@@ -360,8 +366,10 @@ def main():
                          "peak": dom["peak"], "unit": dom["unit"], "frac": dom["frac"],
                          "traffic": traffic, "ms_per_launch": dom["ms"],
                          "algorithmic_per_launch": dom["algo"],
-                         "peak_basis": peak_basis(dom)},
-            "kernels": {k: {kk: v[kk] for kk in ("bound", "ms", "achieved", "unit", "frac")}
+                         "peak_basis": peak_basis(dom),
+                         **({"gather": dom["gather"]} if "gather" in dom else {})},
+            "kernels": {k: {kk: v[kk] for kk in ("bound", "ms", "achieved", "unit", "frac", "gather")
+                            if kk in v}
                         for k, v in roof.items()},
         }
         if not args.no_cpu_baseline:

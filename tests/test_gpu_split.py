@@ -204,3 +204,29 @@ def test_fused_paths_bit_reproducible():
         ref = fn().clone()
         for _ in range(4):
             assert torch.equal(fn(), ref), name
+
+
+def test_split_dcn_tail_c2_scale_reproducible_and_exact():
+    """The NHWC deformable tail kernel on the split path at the C2 scale-0 shape (B=8, every CU
+    busy, fractional offsets), launched 10 times: bit-identical every time and within fp32
+    rounding of the exact engine.  Its packed-fp32 corner blend (v_pk_fma_f32 with a broadcast
+    weight) once moved whole pixels staged by lanes 48-63 (tools/diag_race3.py); the blend is
+    scalar v_fma_f32 now."""
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    B, C, H, W = 8, 64, 128, 416
+    x = torch.randn(B, C, H, W, device=DEV, generator=gen)
+    xn = x.contiguous(memory_format=torch.channels_last)
+    w1 = torch.randn(C, C, 1, 1, device=DEV, generator=gen) * 0.1
+    w3 = torch.randn(C, C, 3, 3, device=DEV, generator=gen) * 0.04
+    wo = torch.randn(54, 32, 3, 3, device=DEV, generator=gen) * 0.01
+    bo = torch.randn(54, device=DEV, generator=gen)
+    b = torch.randn(C, device=DEV, generator=gen)
+    p1, p3, po = ops.pack_weight_split(w1), ops.pack_weight_split(w3), ops.pack_weight_split(wo, 2)
+    om = ops.conv2d_fused(x, wo, bo, 1, 2, 2, 2, packed_weight=po)
+    fn = lambda: ops.mdcn_pw(xn, om, w3, p3, None, b, b, "relu", p1, b, None, None, 1, 2, 2, 2)  # noqa: E731
+    ref = fn().clone()
+    for _ in range(10):
+        assert torch.equal(fn(), ref)
+    with exact_f32():
+        ex = fn()
+    assert (ref - ex).abs().max().item() <= 2e-5 * (1 + ex.abs().max().item())
