@@ -112,3 +112,17 @@ def test_torch_ops_registered_and_refuse_cpu():
         assert tuple(torch.ops.aanet.disp_regress(v, False).shape) == (2, 10, 12)
     with pytest.raises(NotImplementedError):
         torch.ops.aanet.corr_volume(torch.randn(1, 4, 3, 5), torch.randn(1, 4, 3, 5), 2)
+
+
+def test_mdcn_backward_workspace_sizes():
+    """aanet_mdcn_bwd_ws_workspace_size: the NHWC grad_x accumulator + channels-last x + W^T
+    (>= 2*n*c*h*w + co*c*k floats); the deterministic layout holds its int64 accumulator too;
+    invalid shapes give 0."""
+    L = _lib.lib()
+    n, c, h, w, co = 2, 64, 12, 30, 64
+    args = (n, c, h, w, co, 3, 3, 1, 2, 2, 1, 2)
+    ws = L.aanet_mdcn_bwd_ws_workspace_size(*args)
+    det = L.aanet_mdcn_bwd_det_workspace_size(*args)
+    assert ws >= 4 * (2 * n * c * h * w + co * c * 9)
+    assert det >= 8 * n * c * h * w + 4 * (n * c * h * w + co * c * 9)
+    assert L.aanet_mdcn_bwd_ws_workspace_size(n, 63, h, w, co, 3, 3, 1, 2, 2, 1, 2) == 0  # C % dg
