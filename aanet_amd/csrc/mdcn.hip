@@ -1931,10 +1931,13 @@ int launch_fwd(const MdcnArgs &a_in, int packed, hipStream_t st) {
     if ((a.layout & 2) && (a.tail_w || Cog % 4)) return AANET_EUNSUPPORTED;
   }
   const int ncot = host_div_up(Cog, co_t);
-  // 128-pixel tiles when they still give >= 4 workgroups per CU, else 64
-  int ptt = co_t == 16 || (long)a.N * host_div_up(P, 128) * a.groups * ncot >= 1024 ? 128 : 64;
+  // 128-pixel tiles when they still give >= 2 workgroups per CU (the scale-1 convs of the C2
+  // pyramid, 832 tiles: stride-2 64->64 exchange conv 93 -> 86 us), else 64
+  static const int ptt_min = [] { const char *e = getenv("AANET_PTT128_MIN_WG"); return e ? atoi(e) : 512; }();
+  int ptt = co_t == 16 || (long)a.N * host_div_up(P, 128) * a.groups * ncot >= ptt_min ? 128 : 64;
   static const int ptt_env = [] { const char *e = getenv("AANET_PTT"); return e ? atoi(e) : 0; }();
-  if (ptt_env == 64 && co_t != 16) ptt = 64;  // A/B switch (tools/conv_microbench.py)
+  if (ptt_env == 64 && co_t != 16) ptt = 64;  // A/B switches (tools/conv_microbench.py)
+  if (ptt_env == 128) ptt = 128;
   if (full_cfg(a, MODE, co_t) == 1) ptt = 128;  // 16-channel chunks are staged 4 per thread
   static const int nohalo = [] { const char *e = getenv("AANET_NO_HALO"); return e ? atoi(e) : 0; }();
   a.halo = !nohalo && MODE == 0 && a.split && packed && (a.layout & 1) && a.kh == 3 && a.kw == 3 &&

@@ -24,6 +24,7 @@ p1, p3, po = ops.pack_weight_split(w1), ops.pack_weight_split(w3), ops.pack_weig
 if os.environ.get("AANET_PACK_F32") == "1":  # plain f32 packed weights (exact engine only)
     p1, p3, po = ops.pack_weight(w1), ops.pack_weight(w3), ops.pack_weight(wo)
 om = ops.conv2d_fused(x, wo, bo, 1, 2, 2, 2, packed_weight=po)
+p3h = ops.pack_weight_split(w3[:32].contiguous())
 xn = x.contiguous(memory_format=torch.channels_last)
 up1, up2 = res[:, :, :64, :208].contiguous(), res[:, :, :32, :104].contiguous()
 fl = torch.randn(B, 128, H, W, device=dev, generator=g)
@@ -58,6 +59,11 @@ cases = {
     "conv3x3_pw_nhwc": (lambda: ops.conv2d_pw(xn, w3, p3, b, None, None, "relu", p1, b, res, "relu", 1, 1, 1),
                         2 * B * H * W * C * C * 10),
     "csa_sum": (lambda: ops.csa_sum([x, up1, up2]), 0),
+    # the fusion layers' scale 0 -> 1 exchange convs (3x3 stride 2, NCHW input)
+    "conv3x3_s2_64": (lambda: ops.conv2d_fused(x, w3, b, 2, 1, 1, 1, "leaky", packed_weight=p3),
+                      2 * B * (H // 2) * (W // 2) * C * C * 9),
+    "conv3x3_s2_32": (lambda: ops.conv2d_fused(x, w3[:32].contiguous(), b[:32].contiguous(), 2, 1, 1, 1,
+                                               packed_weight=p3h), 2 * B * (H // 2) * (W // 2) * 32 * C * 9),
     "corr": (lambda: ops.corr_volume(fl, fr, 64), 0),
     "regress": (lambda: ops.disp_regress(vol64), 0),
     # C5 (PSMNet 4-D volume, 384x1248 -> 1/4: [B,32,96,312], D=192/4=48), B=4
