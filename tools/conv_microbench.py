@@ -27,6 +27,7 @@ om = ops.conv2d_fused(x, wo, bo, 1, 2, 2, 2, packed_weight=po)
 p3h = ops.pack_weight_split(w3[:32].contiguous())
 xn = x.contiguous(memory_format=torch.channels_last)
 up1, up2 = res[:, :, :64, :208].contiguous(), res[:, :, :32, :104].contiguous()
+up1f, up2f = up1, up2  # the CSA exchange terms of branch 0 (64 ch at 1/2 and 1/4 of the size)
 fl = torch.randn(B, 128, H, W, device=dev, generator=g)
 fr = torch.randn(B, 128, H, W, device=dev, generator=g)
 vol64 = torch.randn(B, 64, H, W, device=dev, generator=g)
@@ -59,6 +60,10 @@ cases = {
     "conv3x3_pw_nhwc": (lambda: ops.conv2d_pw(xn, w3, p3, b, None, None, "relu", p1, b, res, "relu", 1, 1, 1),
                         2 * B * H * W * C * C * 10),
     "csa_sum": (lambda: ops.csa_sum([x, up1, up2]), 0),
+    "dcn_pw_nhwc_csa": (lambda: ops.mdcn_pw(xn, om, w3, p3, None, b, b, "relu", p1, b, res, "relu", 1, 2, 2, 2,
+                                            csa_up=[up1f, up2f]), 2 * B * H * W * C * C * 10),
+    "conv3x3_pw_nhwc_csa": (lambda: ops.conv2d_pw(xn, w3, p3, b, None, None, "relu", p1, b, res, "relu", 1, 1, 1,
+                                                  csa_up=[up1f, up2f]), 2 * B * H * W * C * C * 10),
     # the fusion layers' scale 0 -> 1 exchange convs (3x3 stride 2, NCHW input)
     "conv3x3_s2_64": (lambda: ops.conv2d_fused(x, w3, b, 2, 1, 1, 1, "leaky", packed_weight=p3),
                       2 * B * (H // 2) * (W // 2) * C * C * 9),
