@@ -372,7 +372,7 @@ def main():
                             if kk in v}
                         for k, v in roof.items()},
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure only
             cb, epe, mx = cpu_baseline(model, left, right, disp)
             line["cpu_baseline"] = cb
             line["epe_vs_ref"] = epe
