@@ -22,12 +22,39 @@ def _key(*tensors):
     return tuple((t.data_ptr(), t._version) for t in tensors if t is not None)
 
 
+def _bn_tensors(bn):
+    """The tensors an eval BN's affine depends on.  A train-mode BN forward updates
+    running_mean / running_var inside the kernel WITHOUT bumping their _version, but it always
+    bumps num_batches_tracked (an in-place add_ at Python level), so that counter's version is
+    part of every cache key; clear_fold_caches() covers writes through `.data`."""
+    return (bn.weight, bn.bias, bn.running_mean, bn.running_var,
+            getattr(bn, "num_batches_tracked", None))
+
+
+def clear_fold_caches(module):
+    """Drop every folded-weight / BN-affine cache in `module`'s subtree (called on each
+    train()/eval() switch of the drop-in modules, see FoldCacheMixin)."""
+    for m in module.modules():
+        for attr in ("_aanet_fold", "_aanet_affine"):
+            if attr in m.__dict__:
+                del m.__dict__[attr]
+
+
+class FoldCacheMixin:
+    """nn.Module.train()/eval() that also invalidates the eval-path caches of the subtree, so an
+    eval -> train-mode forward (BN statistics updated in place) -> eval sequence never reuses a
+    stale folded BatchNorm."""
+
+    def train(self, mode=True):
+        clear_fold_caches(self)
+        return super().train(mode)
+
+
 def folded(conv, bn):
     """(weight, bias, packed weight) of conv followed by eval BN (bn may be None), cached on the
     conv module; the packed copy is the [kh][kw][co][cg] layout the HIP engine streams, carrying
     the split-bf16 fragments too when cg % 32 == 0 (ops.pack_weight_split)."""
-    tensors = (conv.weight, conv.bias) + ((bn.weight, bn.bias, bn.running_mean, bn.running_var)
-                                          if bn is not None else ())
+    tensors = (conv.weight, conv.bias) + (_bn_tensors(bn) if bn is not None else ())
     key = _key(*tensors)
     cache = getattr(conv, "_aanet_fold", None)
     if cache is not None and cache[0] == key:
@@ -52,7 +79,7 @@ def folded(conv, bn):
 
 def bn_affine(bn):
     """(scale, shift) of an eval BN, cached on the BN module (for kernel epilogues)."""
-    key = _key(bn.weight, bn.bias, bn.running_mean, bn.running_var)
+    key = _key(*_bn_tensors(bn))
     cache = getattr(bn, "_aanet_affine", None)
     if cache is not None and cache[0] == key:
         return cache[1], cache[2]
@@ -133,7 +160,7 @@ def run_fused_chain(mods, x):
     return x
 
 
-class FusedSequential(nn.Sequential):
+class FusedSequential(FoldCacheMixin, nn.Sequential):
     """nn.Sequential with the reference's children (same state-dict keys, nesting allowed) that
     in eval mode without autograd runs its conv/BN/activation runs as HIP engine kernels
     (run_fused_chain); training / autograd runs the children in order."""

@@ -14,6 +14,7 @@ from .aggregation import AdaptiveAggregation
 from .aggregation3d import (GCNetAggregation, PSMNetBasicAggregation, PSMNetHGAggregation,
                             StereoNetAggregation)
 from .cost import CostVolume, CostVolumePyramid
+from ._fuse import FoldCacheMixin
 from .estimation import DisparityEstimation
 from .feature import (FeaturePyramidNetwork, FeaturePyrmaid, GANetFeature, GCNetFeature,
                       PSMNetFeature, StereoNetFeature)
@@ -24,7 +25,7 @@ _REFINEMENT = {'stereonet': StereoNetRefinement, 'stereodrnet': StereoDRNetRefin
                'hourglass': HourglassRefinement}
 
 
-class AANet(nn.Module):
+class AANet(FoldCacheMixin, nn.Module):
     def __init__(self, max_disp, useFeatureAtt=1, num_downsample=2, feature_type='aanet',
                  no_feature_mdconv=False, feature_pyramid=False, feature_pyramid_network=False,
                  feature_similarity='correlation', aggregation_type='adaptive', num_scales=3,

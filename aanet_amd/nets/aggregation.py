@@ -13,11 +13,27 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from ._fuse import conv_bn_act, use_fused
+from ._fuse import FoldCacheMixin, conv_bn_act, use_fused
 from .deform import DeformSimpleBottleneck, SimpleBottleneck
 
 
-class AdaptiveAggregationModule(nn.Module):
+def csa_epilogue_ok(x0, up):
+    """Whether the tail kernels' CSA epilogue (aanet_csa_epilogue_t) takes output branch 0: at
+    most two coarser terms, each exactly 2x or 4x smaller than the (same-size) block output, and
+    quad-aligned rows (mdcn.hip launch_fwd).  Otherwise branch 0 is summed by aanet_csa_sum_f32,
+    which implements the general bilinear resize of aggregation.py:396-398."""
+    H, W = x0.shape[2], x0.shape[3]
+    if W % 4 or len(up) > 2:
+        return False
+    for t in up:
+        h, w = t.shape[2], t.shape[3]
+        r = H // h if h > 0 else 0
+        if r not in (2, 4) or h * r != H or w * r != W:
+            return False
+    return True
+
+
+class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
     def __init__(self, num_scales, num_output_branches, max_disp, num_blocks=1,
                  simple_bottleneck=False, deformable_groups=2, mdconv_dilation=2):
         super(AdaptiveAggregationModule, self).__init__()
@@ -88,7 +104,7 @@ class AdaptiveAggregationModule(nn.Module):
         for j in range(self.num_blocks - 1):
             x[0] = self.branches[0][j](x[0])
         last = self.branches[0][self.num_blocks - 1]
-        x[0], csa0 = last.forward_csa(x[0], up0)
+        x[0], csa0 = last.forward_csa(x[0], up0 if csa_epilogue_ok(x[0], up0) else None)
         return self._fuse_eval(x, {0: csa0} if csa0 is not None else {}, {(0, j): t for j, t in
                                                                          zip(range(1, S), up0)})
 
@@ -155,7 +171,7 @@ class AdaptiveAggregationModule(nn.Module):
         return x_fused
 
 
-class AdaptiveAggregation(nn.Module):
+class AdaptiveAggregation(FoldCacheMixin, nn.Module):
     """Stacked AAModules (aggregation.py:406-464)."""
 
     def __init__(self, max_disp, num_scales=3, num_fusions=6, num_stage_blocks=1,

@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from ._fuse import bn_affine, conv_bn_act, folded, use_fused
+from ._fuse import FoldCacheMixin, bn_affine, conv_bn_act, folded, use_fused
 from .deform_conv import DeformConv, ModulatedDeformConv
 
 
@@ -31,7 +31,7 @@ def conv1x1(in_planes, out_planes, stride=1):
     return nn.Conv2d(in_planes, out_planes, kernel_size=1, stride=stride, bias=False)
 
 
-class DeformConv2d(nn.Module):
+class DeformConv2d(FoldCacheMixin, nn.Module):
     """A single (modulated) deformable conv layer (nets/deform.py:17-97)."""
 
     def __init__(self, in_channels, out_channels, kernel_size=3, stride=1, dilation=2, groups=1,
@@ -98,10 +98,11 @@ class DeformConv2d(nn.Module):
         return ops.mdcn_forward_fused(x.contiguous(), offset_mask.contiguous(), dc.weight,
                                       dc.bias, ps, psh, act, dc.stride, dc.padding, dc.dilation,
                                       self.deformable_groups,
-                                      2.0 if self.double_mask else 1.0, packed_weight=wp)
+                                      2.0 if self.double_mask else 1.0, packed_weight=wp,
+                                      groups=dc.groups)
 
 
-class _BottleneckBase(nn.Module):
+class _BottleneckBase(FoldCacheMixin, nn.Module):
     def _forward_ref(self, x):
         identity = x
         out = self.conv1(x)
@@ -130,7 +131,8 @@ class _BottleneckBase(nn.Module):
         width = self.conv1.weight.shape[0]
         c2 = self.conv2
         if deform:
-            pw = c2.modulation and c2.deform_conv.stride == 1 and width <= 64 and w3.shape[0] <= 64
+            pw = c2.modulation and c2.deform_conv.stride == 1 and c2.deform_conv.groups == 1 and \
+                width <= 64 and w3.shape[0] <= 64
             cpg = width // c2.deformable_groups  # 32k-channel groups, or pairs of 16-channel ones
             nhwc = pw and width % 32 == 0 and (cpg % 32 == 0 or cpg == 16)
         else:
@@ -167,7 +169,7 @@ class _BottleneckBase(nn.Module):
     def forward_csa(self, x, csa_up):
         """Eval-only: (block output, its output branch's CSA sum or None); see _forward_fused."""
         deform = isinstance(self, DeformSimpleBottleneck) or isinstance(self, DeformBottleneck)
-        r = self._forward_fused(x, deform=deform, csa_up=list(csa_up))
+        r = self._forward_fused(x, deform=deform, csa_up=None if csa_up is None else list(csa_up))
         return r if isinstance(r, tuple) else (r, None)
 
 

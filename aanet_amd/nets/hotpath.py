@@ -12,10 +12,11 @@ import torch.nn as nn
 
 from .aggregation import AdaptiveAggregation
 from .cost import CostVolume, CostVolumePyramid
+from ._fuse import FoldCacheMixin
 from .estimation import DisparityEstimation
 
 
-class AANetHotPath(nn.Module):
+class AANetHotPath(FoldCacheMixin, nn.Module):
     def __init__(self, max_disp, feature_similarity='correlation', num_scales=3, num_fusions=6,
                  deformable_groups=2, mdconv_dilation=2, no_intermediate_supervision=False,
                  num_stage_blocks=1, num_deform_blocks=3, pyramid=True):

@@ -168,7 +168,7 @@ def mdcn_forward(x, offset, mask, weight, bias=None, stride=1, padding=0, dilati
 
 def mdcn_forward_fused(x, offset_mask, weight, bias=None, post_scale=None, post_shift=None, act=None,
                        stride=1, padding=0, dilation=1, deformable_groups=1, mask_scale=2.0,
-                       packed_weight=None):
+                       packed_weight=None, groups=1):
     """Eval fast path of DeformConv2d (nets/deform.py:78-97) + BN + activation.
 
     offset_mask is the raw offset_conv output [N, dg*3*K, Ho, Wo]: channels [0, 2*dg*K) are
@@ -178,7 +178,9 @@ def mdcn_forward_fused(x, offset_mask, weight, bias=None, post_scale=None, post_
                 names=("input", "offset_mask", "weight", "bias", "post_scale", "post_shift", "packed"),
                 nhwc_ok=(0,))
     N, C, H, W = x.shape
-    Co, _, kh, kw = weight.shape
+    Co, Cg, kh, kw = weight.shape
+    if groups < 1 or C % groups or Co % groups or Cg * groups != C:
+        raise ValueError(f"weight {tuple(weight.shape)} does not match input channels {C} / groups {groups}")
     K = kh * kw
     layout = (_lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0) | _lib.conv_flags(packed_weight)
     Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
@@ -191,8 +193,8 @@ def mdcn_forward_fused(x, offset_mask, weight, bias=None, post_scale=None, post_
     call("aanet_mdcn_fwd_fused_f32", ptr(x), ptr(offset_mask), bs, _lib.ctypes.c_void_p(mask_ptr),
          bs, 1, float(mask_scale), ptr(wsrc), int(packed_weight is not None), ptr(bias),
          ptr(post_scale), ptr(post_shift),
-         ACT[act] if not isinstance(act, int) else act, ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation, 1,
-         deformable_groups, layout, stream_of(x))
+         ACT[act] if not isinstance(act, int) else act, ptr(out), N, C, H, W, Co, kh, kw, stride,
+         padding, dilation, groups, deformable_groups, layout, stream_of(x))
     return out
 
 

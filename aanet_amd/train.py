@@ -105,21 +105,35 @@ class Trainer:
     """One optimizer step per `accumulation_steps` micro-batches (model.py:64-153)."""
 
     def __init__(self, model, lr=1e-3, weight_decay=1e-4, accumulation_steps=1,
-                 highest_loss_only=False):
+                 highest_loss_only=False, max_disp=192):
+        """max_disp: the image-resolution disparity range of the valid mask (train.py --max_disp,
+        default 192), NOT the cost-volume D."""
         self.model = model
         self.accumulation_steps = accumulation_steps
         self.highest_loss_only = highest_loss_only
+        self.max_disp = max_disp
         self.optimizer = torch.optim.Adam(param_groups(model, lr), weight_decay=weight_decay)
         self.micro = 0
 
+    def valid_mask(self, disp):
+        """model.py:71,75: 0 < d < max_disp."""
+        return (disp > 0) & (disp < self.max_disp)
+
     def step(self, left_feature, right_feature, gt_disp, mask=None, pseudo_gt=None,
              pseudo_mask=None):
-        """Forward + backward of one micro-batch; returns the (unscaled) total loss.  The
-        optimizer steps (and DDP all-reduces) on accumulation boundaries only."""
+        """Forward + backward of one micro-batch; returns the (unscaled) total loss, or None when
+        the batch has no valid pixel (model.py:78-79: skipped -- no forward, no backward, no
+        optimizer step -- but it still counts towards the accumulation index, as the reference's
+        enumerate() index does).  The optimizer steps (and DDP all-reduces) on accumulation
+        boundaries only (model.py:151-153)."""
         self.model.train()
         if mask is None:
-            mask = gt_disp > 0
+            mask = self.valid_mask(gt_disp)
+        if pseudo_gt is not None and pseudo_mask is None:
+            pseudo_mask = self.valid_mask(pseudo_gt) & ~mask  # model.py:75-76
         self.micro += 1
+        if not bool(mask.any()):
+            return None
         boundary = self.micro % self.accumulation_steps == 0
         sync_ctx = contextlib.nullcontext()
         if not boundary and isinstance(self.model, nn.parallel.DistributedDataParallel):

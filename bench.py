@@ -8,8 +8,9 @@ Features are the 1/3, 1/6, 1/12 pyramids of a 384x1248 pair: [8,128,128,416], [8
 [8,128,32,104] (BASELINE.json configs[1]).  Random-init weights of that architecture
 (offset_conv nonzero), synthetic N(0,1) features: there is no network for data/checkpoints.
 
-Launch: `python bench.py [--gpus 1 --steps K --warmup W]`; for N>1 under torch.distributed.run
-(one process per GPU, RCCL).  Pairs are sharded across ranks with no data-path collective
+Launch: `python bench.py [--gpus N --steps K --warmup W]`.  For N>1 it either runs under
+torch.distributed.run (RANK/WORLD_SIZE set) or starts the N rank processes itself
+(launch_ranks; one process per GPU, RCCL).  Pairs are sharded across ranks with no data-path collective
 (weak scaling); one all_gather of a per-rank metrics record at the end.  Rank 0 prints ONE
 JSON line.  `roofline` is measured live (HIP events on the launch stream) for the dominant
 HIP kernel; `cpu_baseline` times the CPU oracle (port of the reference path) on one pair.
@@ -65,6 +66,9 @@ def parse():
                     help="C4: deform_conv2d forward + backward microbench over the aggregation / "
                          "feature-extractor DCN shapes (secondary lines, not the headline)")
     ap.add_argument("--dcn-shapes", default=None, help="--dcn-sweep: comma-separated subset of DCN_SHAPES")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="launcher/record/gather plumbing only: gloo on CPU, a stand-in CPU step "
+                         "(tests/test_distributed.py); never a metric")
     ap.add_argument("--only", default=None,
                     help="profiling mode: run only one kernel family (corr|mdcn|regress|step)")
     return ap.parse_args()
@@ -226,31 +230,61 @@ def conv_peak():
 CPU_SAMPLE_S = 12.0  # seconds of CPU work in the cpu_baseline sample
 
 
-def cpu_baseline(model, left, right, gpu_disp):
-    """Time the CPU oracle (restated reference path) on a bounded sample of the batch's pairs
-    (pairs 0, 1, ... cyclically until >= CPU_SAMPLE_S seconds of CPU work, at least 2 pairs);
-    also EPE of the GPU output vs the oracle on pair 0."""
-    from oracle import aggregation as oagg
-    threads = torch.get_num_threads()
+def _oracle_inputs(model, left, right, count=None):
     sd = {k: v.detach().cpu().numpy() for k, v in model.aggregation.state_dict().items()}
-    B = left[0].shape[0]
+    B = left[0].shape[0] if count is None else min(count, left[0].shape[0])
     pairs = [([t[i:i + 1].cpu().numpy() for t in left], [t[i:i + 1].cpu().numpy() for t in right])
              for i in range(B)]
-    n, ref = 0, None
+    return sd, pairs
+
+
+def _oracle_disp(sd, pair):
+    from oracle import aggregation as oagg  # checker only
+    return oagg.hot_path(pair[0], pair[1], sd, MAXD, intermediate_supervision=False)[0]
+
+
+def parity_vs_oracle(model, left, right, gpu_disp):
+    """SURVEY.md §8(e) per-rank parity payload: this rank's GPU disparity of its pair 0 against
+    the CPU oracle (restated reference path) on the same input -> (sum|dd|, max|dd|, n_px,
+    oracle seconds)."""
+    sd, pairs = _oracle_inputs(model, left, right, count=1)
     t0 = time.perf_counter()
-    while n < 2 or time.perf_counter() - t0 < CPU_SAMPLE_S:
-        lp, rp = pairs[n % B]
-        r = oagg.hot_path(lp, rp, sd, MAXD, intermediate_supervision=False)[0]
-        if n == 0:
-            ref = r
-        n += 1
+    ref = _oracle_disp(sd, pairs[0])
     dt = time.perf_counter() - t0
     ours = gpu_disp[:1].cpu().numpy()
     diff = np.abs(ours.astype(np.float64) - ref.astype(np.float64))
+    return float(diff.sum()), float(diff.max()), float(diff.size), dt
+
+
+def host_cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(model, left, right):
+    """Time the CPU oracle (restated reference path) on a bounded sample of the batch's pairs
+    (pairs 0, 1, ... cyclically until >= CPU_SAMPLE_S seconds of CPU work, at least 2 pairs), on
+    the host threads torch uses (the box's CPU share: OMP_NUM_THREADS)."""
+    threads = torch.get_num_threads()
+    sd, pairs = _oracle_inputs(model, left, right)
+    n = 0
+    t0 = time.perf_counter()
+    while n < 2 or time.perf_counter() - t0 < CPU_SAMPLE_S:
+        _oracle_disp(sd, pairs[n % len(pairs)])
+        n += 1
+    dt = time.perf_counter() - t0
     return dict(value=n / dt, unit="stereo-pairs/s", cores=threads, kind="port",
+                cpu_model=host_cpu_model(), affinity_cores=len(os.sched_getaffinity(0)),
                 sample=f"{n} pairs of the C2 workload (features 128x128x416 pyramid, D=64), "
-                       f"{dt:.1f} s: oracle/ C restatement (cost volume, DCN, regression) + "
-                       "torch-CPU convs", seconds=dt), float(diff.mean()), float(diff.max())
+                       f"{dt:.1f} s on {threads} threads: oracle/ C restatement (cost volume, DCN, "
+                       "regression) + torch-CPU convs", seconds=dt)
 
 
 def timed_run(step, args, world):
@@ -289,13 +323,56 @@ def timed_run(step, args, world):
     return out, time.perf_counter() - t0, graph
 
 
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without an external launcher: start N rank processes of this script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on 127.0.0.1), one per GPU, the
+    way torch.distributed.run would (reference: train.py:113-123 under torch.distributed.launch).
+    The parent never touches the GPU.  Rank 0 prints the JSON line (inherited stdout).  If one
+    rank fails, the others are terminated (exact PIDs) so no rank waits in a collective forever.
+    -> exit code (the first non-zero child code, else 0)."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:  # a dead rank leaves the others blocked in a collective
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if args.plumbing:
+        plumbing_main(args, rank, world)
+        return
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
     if world > 1:
@@ -327,10 +404,14 @@ def main():
     out, elapsed, graph = timed_run(step, args, world)
     disp = out  # graph output buffer (or last eager output)
 
+    # per-rank parity payload (this rank's pair 0 vs the CPU oracle), outside the timed region
+    sum_err, max_err, n_px, _ = parity_vs_oracle(model, left, right, disp)
     from aanet_amd import dist as adist
     record = adist.make_record(device, pairs=args.batch * args.steps, elapsed_s=elapsed,
+                               sum_abs_err=sum_err, max_abs_err=max_err, n_px=n_px,
                                disp_min=float(disp.min()), disp_max=float(disp.max()))
-    summary = adist.summarize(adist.gather_records(record))  # the one collective (metrics only)
+    records = adist.gather_records(record)  # the one collective (metrics only)
+    summary = adist.summarize(records)
     total_pairs, t_max = summary["pairs"], summary["elapsed_max_s"]
 
     if rank == 0:
@@ -371,13 +452,48 @@ def main():
             "kernels": {k: {kk: v[kk] for kk in ("bound", "ms", "achieved", "unit", "frac", "gather")
                             if kk in v}
                         for k, v in roof.items()},
+            # EPE vs ref: mean / max |dd| of every rank's pair 0 against the CPU oracle
+            "epe_vs_ref": summary["epe"],
+            "max_abs_disp_err_vs_ref": summary["max_abs_err"],
+            "parity_pairs": len(records),
+            "per_rank": [{"pairs": r[0], "elapsed_s": r[1], "max_abs_err": r[3]}
+                         for r in records.tolist()],
         }
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure only
-            cb, epe, mx = cpu_baseline(model, left, right, disp)
-            line["cpu_baseline"] = cb
-            line["epe_vs_ref"] = epe
-            line["max_abs_disp_err_vs_ref"] = mx
+            line["cpu_baseline"] = cpu_baseline(model, left, right)
         print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def plumbing_main(args, rank, world):
+    """--plumbing: the multi-rank launch, per-rank record, all_gather and max-over-ranks clock of
+    the real bench, on CPU with gloo and a stand-in step (a CPU matmul per pair), so the N>1
+    path is covered where there is no GPU (tests/test_distributed.py).  Not a measurement."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    if os.environ.get("AANET_PLUMBING_FAIL_RANK") == str(rank):  # launcher failure test
+        raise SystemExit(3)
+    from aanet_amd import dist as adist
+    g = torch.Generator().manual_seed(1234 + rank)
+    a = torch.randn(64, 64, generator=g)
+    t0 = time.perf_counter()
+    for _ in range(args.warmup + args.steps):
+        for _ in range(args.batch):
+            a = torch.tanh(a @ a)
+    elapsed = time.perf_counter() - t0 + 0.01 * rank  # distinct per rank: the max must win
+    rec = adist.make_record("cpu", pairs=args.batch * args.steps, elapsed_s=elapsed,
+                            sum_abs_err=0.0, max_abs_err=1e-6 * (rank + 1), n_px=1.0)
+    records = adist.gather_records(rec)
+    summary = adist.summarize(records)
+    if rank == 0:
+        print(json.dumps({"metric": "plumbing (not a measurement)", "n_gpus": world,
+                          "value": summary["pairs"] / summary["elapsed_max_s"],
+                          "pairs": summary["pairs"], "elapsed_max_s": summary["elapsed_max_s"],
+                          "max_abs_disp_err_vs_ref": summary["max_abs_err"],
+                          "per_rank": [{"pairs": r[0], "elapsed_s": r[1]} for r in records.tolist()]}),
+              flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

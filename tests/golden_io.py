@@ -68,3 +68,36 @@ def synthetic_pair(B, H, W, seed):
     left = torch.rand(B, 3, H, W, generator=gm) * 2 - 1
     right = torch.roll(left, shifts=-6, dims=3) + 0.05 * torch.randn(B, 3, H, W, generator=gm)
     return left, right
+
+
+def synthetic_pyramid(B, C, H, W, seed, num_scales=3):
+    """Seeded N(0,1) feature pyramids (left, right) at H>>s x W>>s, s < num_scales (torch CPU
+    generator), for the production-configuration fixtures: the test rebuilds them from the seed,
+    so the fixture carries outputs only."""
+    import torch
+    g = torch.Generator().manual_seed(5000 + seed)
+    left = [torch.randn(B, C, H >> s, W >> s, generator=g) for s in range(num_scales)]
+    right = [torch.randn(B, C, H >> s, W >> s, generator=g) for s in range(num_scales)]
+    return left, right
+
+
+def production_case(tag):
+    """(fixture, numpy state dict of `aggregation.*` without the prefix, left pyramid, right
+    pyramid) of a make_production_golden.py fixture: the weights are rebuilt by name on our own
+    module tree (so a key mismatch with the reference fails here) and the inputs from the seed."""
+    import torch
+
+    from aanet_amd.nets import AANetHotPath
+    g = golden(tag)
+    B, C, H, W = (int(v) for v in g["shape"])
+    seed, max_disp = int(g["seed"]), int(g["max_disp"])
+    m = AANetHotPath(max_disp, no_intermediate_supervision=True, num_deform_blocks=3)
+    names = fill_synthetic(m.aggregation, seed)
+    assert [n for n, _ in names] == list(g["names"]), "state-dict keys differ from the reference"
+    sd = {k: v.numpy() for k, v in m.aggregation.state_dict().items()}
+    checksum = sum(float(torch.from_numpy(v).double().abs().sum()) for v in sd.values())
+    assert abs(checksum - float(g["checksum"])) <= 1e-9 * abs(checksum), "weight fill differs"
+    left, right = synthetic_pyramid(B, C, H, W, seed)
+    feat = sum(float(t.double().abs().sum()) for t in left + right)
+    assert abs(feat - float(g["feat_checksum"])) <= 1e-9 * abs(feat), "feature fill differs"
+    return g, sd, m, left, right

@@ -69,3 +69,42 @@ def test_single_process_gather_is_identity():
     recs = adist.gather_records(rec)
     assert recs.shape == (1, len(adist.RECORD_FIELDS))
     assert adist.summarize(recs)["pairs_per_s"] == 16.0
+
+
+def test_bench_self_launch_two_ranks_gloo():
+    """`bench.py --gpus 2` with no external launcher starts its own 2 rank processes (the path the
+    GPU run takes when WORLD_SIZE is unset), gathers one record per rank and reports whole-job
+    pairs over the MAX elapsed over ranks -- exercised with the --plumbing stand-in step on CPU."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    res = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2",
+                          "--plumbing", "--steps", "3", "--warmup", "1", "--batch", "4"],
+                         env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-2000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout  # rank 0 prints ONE line
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2
+    assert len(line["per_rank"]) == 2
+    assert line["pairs"] == 2 * 4 * 3 == sum(r["pairs"] for r in line["per_rank"])
+    assert line["elapsed_max_s"] == max(r["elapsed_s"] for r in line["per_rank"])
+    assert line["value"] == pytest.approx(line["pairs"] / line["elapsed_max_s"])
+    assert line["max_abs_disp_err_vs_ref"] == pytest.approx(2e-6)  # max over ranks
+
+
+def test_bench_self_launch_propagates_rank_failure():
+    """A failing rank makes the launcher exit non-zero (and the other rank is not left hanging)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["AANET_PLUMBING_FAIL_RANK"] = "1"  # rank 1 exits; rank 0 would wait in all_gather
+    res = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2",
+                          "--plumbing", "--steps", "2", "--warmup", "0"],
+                         env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode == 3
+    assert not [ln for ln in res.stdout.splitlines() if ln.startswith("{")]

@@ -1,0 +1,167 @@
+"""GPU parity of the hot path in the configurations that production (and bench.py) runs.
+
+The round-1 end-to-end goldens run AdaptiveAggregation at max_disp=16, where no scale is 32
+channels wide, so they exercise the exact-f32 NCHW engine only.  Here:
+
+* hotpath_d64 -- the reference graph's own output at max_disp=64 (the C2 width), features
+  [2,128,32,96]: scale widths 64/32/16, i.e. the split-bf16 contraction, the NHWC bottleneck
+  tails (DCN + conv3 and 3x3 + conv3) and the CSA epilogue -- the kernels bench.py times;
+* hotpath_c1 -- BASELINE configs[0] (288x576, D=24): features [1,128,96,192];
+* C2 pair 0 at full size ([1,128,128,416] pyramid, D=64) against the CPU oracle (which the
+  d64 fixture pins to the reference at the same widths);
+* the eval-cache, CSA-epilogue-precondition and grouped-DCN regressions of ADVICE round 1.
+
+Tolerances: disparity 2e-4 px max abs (north-star bar 1e-3); aggregated cost 1e-4 x its scale.
+"""
+import numpy as np
+import pytest
+import torch
+
+from aanet_amd import nets
+from aanet_amd.nets._fuse import folded
+from aanet_amd.nets.aggregation import csa_epilogue_ok
+from oracle import aggregation as oagg
+from tests.golden_io import fill_synthetic, production_case, synthetic_pyramid
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+DISP_TOL = 2e-4
+
+
+def _model(tag, fuse=True):
+    g, sd, m, left, right = production_case(tag)
+    m = m.to(DEV).eval()
+    for mod in m.modules():
+        mod.aanet_fuse = fuse
+    return g, sd, m, [t.to(DEV) for t in left], [t.to(DEV) for t in right]
+
+
+def _production_kernels_engaged(m):
+    """The d64 configuration must run the split-bf16 weight buffers at every scale-0/1 conv of
+    the bottlenecks, with NHWC-capable widths and an accepted CSA epilogue."""
+    blk = m.aggregation.fusions[5].branches[0][0]        # DeformSimpleBottleneck, scale 0
+    assert getattr(folded(blk.conv2.deform_conv, None)[2], "_aanet_split", False)
+    assert getattr(folded(blk.conv3, blk.bn3)[2], "_aanet_split", False)
+    blk0 = m.aggregation.fusions[0].branches[0][0]       # SimpleBottleneck, scale 0
+    assert getattr(folded(blk0.conv2, blk0.bn2)[2], "_aanet_split", False)
+    assert blk0.conv1.weight.shape[0] % 32 == 0 and blk.conv1.weight.shape[0] % 32 == 0
+
+
+@pytest.mark.parametrize("fuse", [True, False])
+def test_hotpath_d64_vs_reference(fuse):
+    g, _, m, left, right = _model("hotpath_d64", fuse)
+    with torch.no_grad():
+        vols = m.cost_volume(left, right)
+        assert csa_epilogue_ok(vols[0], [vols[1], vols[2]])
+        agg0 = m.aggregation(list(vols))[0]
+        disps = m(left, right)
+    if fuse:
+        _production_kernels_engaged(m)
+    a0 = agg0.cpu().numpy().ravel()
+    scale = np.abs(g["agg0_sample"]).max()
+    aerr = np.abs(a0[g["agg0_idx"]] - g["agg0_sample"]).max()
+    assert aerr <= 1e-4 * scale, f"aggregated cost: {aerr:.3g} (scale {scale:.3g})"
+    assert len(disps) == 1
+    d = disps[0].cpu().numpy()
+    err = np.abs(d - g["disp0"])
+    print(f"hotpath_d64 fuse={fuse}: max|dd| {err.max():.3g} px, mean {err.mean():.3g}, "
+          f"reference fp32 vs fp64 max {np.abs(g['disp0'] - g['disp64_0']).max():.3g}")
+    assert err.max() <= DISP_TOL, f"max |dd| {err.max():.3g} px"
+
+
+def test_hotpath_c1_vs_reference():
+    """BASELINE configs[0]: 288x576 pair, D=24 (max_disp 72), B=1 -- on the MI355X."""
+    g, _, m, left, right = _model("hotpath_c1")
+    with torch.no_grad():
+        disps = m(left, right)
+    d = disps[0].cpu().numpy()
+    assert d.shape == g["disp0"].shape == (1, 96, 192)
+    err = np.abs(d - g["disp0"])
+    print(f"hotpath_c1: max|dd| {err.max():.3g} px, mean {err.mean():.3g}")
+    assert err.max() <= DISP_TOL, f"max |dd| {err.max():.3g} px"
+
+
+def test_c2_pair0_full_size_vs_oracle():
+    """C2 at full size: one 384x1248 pair ([1,128,128,416] / [64,208] / [32,104] pyramid, D=64),
+    the bench configuration's kernels, against the CPU oracle on the same input."""
+    torch.manual_seed(0)
+    m = nets.AANetHotPath(64, no_intermediate_supervision=True, num_deform_blocks=3)
+    fill_synthetic(m.aggregation, 2)
+    sd = {k: v.numpy().copy() for k, v in m.aggregation.state_dict().items()}
+    m = m.to(DEV).eval()
+    left, right = synthetic_pyramid(1, 128, 128, 416, 2)
+    with torch.no_grad():
+        d = m([t.to(DEV) for t in left], [t.to(DEV) for t in right])[0].cpu().numpy()
+    ref = oagg.hot_path([t.numpy() for t in left], [t.numpy() for t in right], sd, 64,
+                        intermediate_supervision=False)[0]
+    err = np.abs(d.astype(np.float64) - ref)
+    print(f"C2 pair 0 vs oracle: max|dd| {err.max():.3g} px, mean {err.mean():.3g}")
+    assert d.shape == (1, 128, 416)
+    assert err.max() <= DISP_TOL, f"max |dd| {err.max():.3g} px"
+
+
+def test_eval_after_train_mode_forward_refolds_bn():
+    """eval forward -> train-mode forward (BN running statistics updated in place, no _version
+    bump) -> eval forward must fold the NEW statistics (stale folded-BN cache)."""
+    g, _, m, left, right = _model("hotpath_d64")
+    with torch.no_grad():
+        m(left, right)                      # populates the folded-weight caches
+        m.train()
+        m(left, right)                      # batch-statistics BN: running stats move
+        m.eval()
+        fused = m(left, right)[0]
+        for mod in m.modules():
+            mod.aanet_fuse = False
+        unfused = m(left, right)[0]         # reference op order, BN modules as they are now
+    err = (fused - unfused).abs().max().item()
+    assert err <= DISP_TOL, err
+
+
+def test_eval_bn_cache_sees_direct_running_stat_writes_in_train_mode():
+    """A train-mode BN forward WITHOUT a train()/eval() switch in between (the module left in
+    training state but its BN layers in eval): num_batches_tracked moves the cache key."""
+    bn = torch.nn.BatchNorm2d(8).to(DEV)
+    from aanet_amd.nets._fuse import bn_affine
+    bn.eval()
+    s0, _ = bn_affine(bn)
+    s0 = s0.clone()
+    bn.train()
+    with torch.no_grad():
+        bn(torch.randn(4, 8, 5, 5, device=DEV) * 3)
+    bn.training = False                     # flip the flag without going through .eval()
+    s1, _ = bn_affine(bn)
+    assert not torch.equal(s0, s1)
+
+
+def test_csa_epilogue_precondition_falls_back_on_odd_width():
+    """Scale-0 width 42 (not a multiple of 4): the tail kernel's CSA epilogue cannot take branch
+    0, so it is summed by the general resize kernel instead of raising."""
+    torch.manual_seed(1)
+    m = nets.AANetHotPath(64, no_intermediate_supervision=True, num_deform_blocks=3)
+    fill_synthetic(m.aggregation, 3)
+    sd = {k: v.numpy().copy() for k, v in m.aggregation.state_dict().items()}
+    m = m.to(DEV).eval()
+    left, right = synthetic_pyramid(1, 32, 16, 42, 3)
+    with torch.no_grad():
+        vols = m.cost_volume([t.to(DEV) for t in left], [t.to(DEV) for t in right])
+        assert not csa_epilogue_ok(vols[0], [vols[1], vols[2]])
+        d = m([t.to(DEV) for t in left], [t.to(DEV) for t in right])[0].cpu().numpy()
+    ref = oagg.hot_path([t.numpy() for t in left], [t.numpy() for t in right], sd, 64,
+                        intermediate_supervision=False)[0]
+    assert np.abs(d - ref).max() <= DISP_TOL
+
+
+def test_grouped_deform_conv_fused_matches_autograd_path():
+    """DeformConv2d(groups=2) in eval: the fused kernel must contract per group (the
+    fused entry point was called with groups=1)."""
+    torch.manual_seed(4)
+    dc = nets.DeformConv2d(64, 64, groups=2, deformable_groups=2).to(DEV)
+    with torch.no_grad():
+        dc.offset_conv.weight.normal_(0, 0.05)
+        dc.offset_conv.bias.normal_(0, 0.5)
+    dc.eval()
+    x = torch.randn(2, 64, 12, 20, device=DEV)
+    with torch.no_grad():
+        fused = dc(x)
+    ref = dc(x.clone().requires_grad_()).detach()   # autograd path (ModulatedDeformConvFunction)
+    assert (fused - ref).abs().max().item() <= 2e-4 * (1 + ref.abs().max().item())

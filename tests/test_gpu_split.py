@@ -210,7 +210,7 @@ def test_split_dcn_tail_c2_scale_reproducible_and_exact():
     """The NHWC deformable tail kernel on the split path at the C2 scale-0 shape (B=8, every CU
     busy, fractional offsets), launched 10 times: bit-identical every time and within fp32
     rounding of the exact engine.  Its packed-fp32 corner blend (v_pk_fma_f32 with a broadcast
-    weight) once moved whole pixels staged by lanes 48-63 (tools/diag_race3.py); the blend is
+    weight) once moved whole pixels staged by lanes 48-63 (tools/repro_packed_fp32_hazard.py); the blend is
     scalar v_fma_f32 now."""
     gen = torch.Generator(device=DEV).manual_seed(3)
     B, C, H, W = 8, 64, 128, 416

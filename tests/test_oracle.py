@@ -256,3 +256,23 @@ def test_disp_warp_bwd_vs_torch_autograd_f64():
     (out * go).sum().backward()
     ref = oracle.disp_warp_bwd(g["img"], g["disp"], go.numpy())
     assert np.abs(ref - disp.grad.numpy()).max() <= 1e-9
+
+
+@pytest.mark.parametrize("tag", ["hotpath_d64", "hotpath_c1"])
+def test_production_config_oracle_matches_reference(tag):
+    """The oracle at the production widths (max_disp 64: C2's; 24: C1's) against the reference
+    graph's own output (tests/golden/make_production_golden.py)."""
+    from tests.golden_io import production_case
+    g, sd, _, left, right = production_case(tag)
+    L = [t.numpy() for t in left]
+    R = [t.numpy() for t in right]
+    max_disp = int(g["max_disp"])
+    vols = oagg.oracle.cost_volume_pyramid(L, R, max_disp)
+    agg0 = oagg.adaptive_aggregation(vols, sd, intermediate_supervision=False)[0].detach().numpy()
+    a0 = agg0.ravel()
+    scale = np.abs(g["agg0_sample"]).max()
+    np.testing.assert_allclose(a0[g["agg0_idx"]], g["agg0_sample"], atol=1e-5 * scale, rtol=0)
+    assert abs(a0.astype(np.float64).sum() - g["agg0_sum"]) <= 1e-5 * g["agg0_abs_sum"]
+    disp = oagg.oracle.disp_regress(agg0)
+    err = np.abs(disp - g["disp0"]).max()
+    assert err <= 1e-4, f"{tag}: oracle vs reference {err:.3g} px"

@@ -176,3 +176,32 @@ def test_ddp_accumulation_gloo_world2():
 def test_wrap_is_identity_without_process_group():
     m = TinyPath()
     assert train.wrap_data_parallel(m, torch.device("cpu")) is m
+
+
+def test_default_mask_is_bounded_by_max_disp():
+    """model.py:71: mask = (gt > 0) & (gt < max_disp) -- disparities at or past max_disp are
+    excluded from the loss."""
+    t = train.Trainer(TinyPath(), max_disp=8)
+    gt = torch.tensor([[[0.0, 0.5, 7.9, 8.0, 9.0, -1.0]]])
+    assert t.valid_mask(gt).tolist() == [[[False, True, True, False, False, False]]]
+
+
+def test_all_invalid_batch_is_skipped_like_the_reference():
+    """model.py:78-79: a batch without one valid pixel is skipped -- no backward, no optimizer
+    step, no NaN written into the weights (a masked mean over zero pixels would be 0/0) -- but it
+    still counts towards the accumulation index (enumerate's i)."""
+    torch.manual_seed(3)
+    m = TinyPath()
+    t = train.Trainer(m, lr=1e-2, max_disp=8, accumulation_steps=2)
+    l, r, _ = _features(2)
+    before = [p.detach().clone() for p in m.parameters()]
+    bad_gt = torch.full((2, 32, 64), 50.0)   # every pixel >= max_disp
+    assert t.step(l, r, bad_gt) is None
+    assert all(torch.equal(a, b) for a, b in zip(before, m.parameters()))
+    assert all(p.grad is None for p in m.parameters())
+    # the skipped batch was micro-step 1, so this one is the boundary and steps the optimizer
+    good_gt = torch.rand(2, 32, 64) * 6 + 0.5
+    loss = t.step(l, r, good_gt)
+    assert loss is not None and torch.isfinite(loss)
+    assert not all(torch.equal(a, b) for a, b in zip(before, m.parameters()))
+    assert all(torch.isfinite(p).all() for p in m.parameters())
