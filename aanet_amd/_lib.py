@@ -106,6 +106,7 @@ def is_nhwc(t):
 LAYOUT_IN_NHWC, LAYOUT_OUT_NHWC = 1, 2  # AANET_LAYOUT_* (include/aanet_mi355x.h)
 CONV_EXACT_F32 = 8  # AANET_CONV_EXACT_F32: exact f32 MFMA instead of the split-bf16 contraction
 CONV_WEIGHTS_SPLIT = 16  # AANET_CONV_WEIGHTS_SPLIT: weight buffers carry bf16 piece fragments
+CONV_GENERIC_DCN = 32  # AANET_CONV_GENERIC_DCN: generic engine instead of the LDS-window DCN tail
 
 _exact_f32 = os.environ.get("AANET_EXACT_F32", "0") == "1"
 

@@ -1,0 +1,479 @@
+// dcn_tile.hip -- the deformable bottleneck tail of the cost aggregation (nets/deform.py:207-236:
+// DeformConv2d + BN2 + ReLU -> conv3 1x1 + BN3 + identity + ReLU, and the scale-0 cross-scale
+// sum of nets/aggregation.py:387-400) in its "window" form, for gfx950.
+//
+// Why a second DCN kernel.  The generic engine (mdcn.hip conv_fwd_kernel, MODE 1) gathers the
+// four bilinear corners of every (pixel, tap, channel quad) straight from L2: 9.2 KB per output
+// pixel, 3.9 GB per C2 scale-0 launch, and it ran at about half the L2-served gather rate with
+// the matrix pipe 80 % idle.  Here a workgroup owns an 8 x 16 pixel tile and, per
+// 32-channel deformable group, stages the tile's input WINDOW once in LDS: every sample whose
+// offset lies in [-2, 2) reads its corners from the window (9 taps x 4 corners from one 48 KB
+// copy), so L2 sees each input line about three times per launch instead of ~36.  Samples outside
+// the window (large offsets) read their corners from global memory, so any offset is handled.
+//
+// Work split.  Wave w owns tile row w (16 output pixels) and all 64 output channels: lane
+// (kr = lane / 16, jj = lane % 16) blends pixel jj's channels 8kr..8kr+7 -- exactly the B fragment
+// of v_mfma_f32_16x16x32_bf16 -- so the deformable im2col never goes through LDS and needs no
+// per-chunk hand-off between waves.  The A fragments (pre-split weights of one tap) are staged
+// through registers into a double-buffered LDS slot, one tap ahead.  The sampling state (window position + four mask-folded
+// corner weights) of 4 taps is computed at once (lane group kr takes tap t0+kr) and handed to the
+// lanes of the other taps with ds_bpermute.
+//
+// Numerics are those of the generic engine: corner positions, validity and weights follow
+// kernel.cu:467-497 / make_samp4 bit for bit (fp contraction off); the blend is
+// ((c0 w0 + c1 w1) + c2 w2) + c3 w3 with the mask folded into the weights; the contraction is the
+// split-bf16 one (three exact bf16 pieces, six products, fp32 accumulation; mdcn.hip split3).
+#include "dcn_tile.h"
+
+#include <stdlib.h>
+
+namespace {
+
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int NT = 512;          // 8 waves, one tile row each
+constexpr int TR = 8, TC = 16;   // tile: 8 rows x 16 columns of output pixels
+constexpr int RW = 2;            // window margin beyond the taps: offsets in [-RW, RW) stay inside
+constexpr int K = 9;             // 3x3 taps
+constexpr int ABUF = 12 * 1024;  // one tap's A fragments: 4 co blocks x 3 pieces x 64 lanes x 16 B
+constexpr int OP = TR * TC + 4;  // epilogue tile pitch (floats)
+
+// ---- split-bf16 contraction (same scheme as mdcn.hip split3 / mfma_split6) -------------------
+__device__ __forceinline__ unsigned hi_pair(float a, float b) {
+  return __builtin_amdgcn_perm(__builtin_bit_cast(unsigned, b), __builtin_bit_cast(unsigned, a), 0x07060302u);
+}
+__device__ __forceinline__ float trunc16(float a) {
+  return __builtin_bit_cast(float, __builtin_bit_cast(unsigned, a) & 0xffff0000u);
+}
+// 8 values -> their three exact bf16 pieces (x = h + m + l)
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8 (&b)[3]) {
+  u32x4 hh, mm, ll;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float x0 = v[2 * i], x1 = v[2 * i + 1];
+    hh[i] = hi_pair(x0, x1);
+    const float r0 = x0 - trunc16(x0), r1 = x1 - trunc16(x1);
+    mm[i] = hi_pair(r0, r1);
+    ll[i] = hi_pair(r0 - trunc16(r0), r1 - trunc16(r1));
+  }
+  b[0] = __builtin_bit_cast(bf16x8, hh);
+  b[1] = __builtin_bit_cast(bf16x8, mm);
+  b[2] = __builtin_bit_cast(bf16x8, ll);
+}
+__device__ __forceinline__ f32x4 mfma_split6(const bf16x8 (&A)[3], const bf16x8 (&B)[3], f32x4 t) {
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1], B[1], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[2], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[2], B[0], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[1], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1], B[0], t, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[0], t, 0, 0, 0);
+}
+
+__device__ __forceinline__ float act_f(float v, int act) {
+  if (act == 1) return v > 0.f ? v : 0.f;
+  if (act == 2) return v > 0.f ? v : 0.2f * v;
+  return v;
+}
+
+// Sampling state of one (pixel, tap, deformable group): the window position of the top-left
+// corner (-1: a corner lies outside the window -> global gather) and the four corner weights with
+// the modulation mask folded in.  Same float steps as mdcn.hip finish_params + make_samp4.
+struct TapState {
+  int pos;
+  float w0, w1, w2, w3;
+};
+
+template <int DIL, int WR, int WC>
+__device__ __forceinline__ TapState tap_state(float oh, float ow, float ml, int yy, int xx, bool pv,
+                                              int t, int H, int W, int wy0, int wx0,
+                                              int mask_logits, float mask_scale) {
+#pragma clang fp contract(off)
+  const int i = t / 3, j = t - 3 * (t / 3);
+  float m = mask_logits ? mask_scale * __builtin_amdgcn_rcpf(1.f + __expf(-ml)) : ml;
+  if (!pv) m = 0.f;
+  const float h = (float)(yy - DIL + i * DIL) + oh;
+  const float w = (float)(xx - DIL + j * DIL) + ow;
+  const bool valid = h > -1.f && w > -1.f && h < (float)H && w < (float)W;
+  const int hl = (int)floorf(h), wl = (int)floorf(w);
+  const float lh = h - (float)hl, lw = w - (float)wl;
+  const float hh = 1.f - lh, hw = 1.f - lw;
+  const bool ok1 = valid && hl >= 0 && wl >= 0;
+  const bool ok2 = valid && hl >= 0 && wl + 1 <= W - 1;
+  const bool ok3 = valid && hl + 1 <= H - 1 && wl >= 0;
+  const bool ok4 = valid && hl + 1 <= H - 1 && wl + 1 <= W - 1;
+  TapState s;
+  s.w0 = (ok1 ? hh * hw : 0.f) * m;
+  s.w1 = (ok2 ? hh * lw : 0.f) * m;
+  s.w2 = (ok3 ? lh * hw : 0.f) * m;
+  s.w3 = (ok4 ? lh * lw : 0.f) * m;
+  const int rh = hl - wy0, rw = wl - wx0;
+  const bool inwin = (unsigned)rh <= (unsigned)(WR - 2) && (unsigned)rw <= (unsigned)(WC - 2);
+  // an invalid sample has four zero weights: any in-window position will do
+  s.pos = !valid ? 0 : (inwin ? rh * WC + rw : -1);
+  return s;
+}
+
+template <int DIL>
+__global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
+  constexpr int MG = DIL + RW;                     // window margin around the tile
+  constexpr int WR = TR + 2 * MG, WC = TC + 2 * MG;
+  constexpr int NPOS = (WR * WC + 63) / 64 * 64;   // positions per quad plane (multiple of 64)
+  constexpr int NWI = NPOS / 64;                   // window quads staged per thread (8*NPOS/512)
+  constexpr int WIN = 8 * NPOS * 16;               // window bytes: [8 channel quads][NPOS][16 B]
+  static_assert(WIN >= 64 * OP * 4, "epilogue tile must fit the window");
+  // Three LDS objects: the compiler orders a ds_read after an outstanding LDS-DMA only when they
+  // may alias, so the DMA of tap c+1's weights into one A slot never holds reads of the window or
+  // of the other slot.
+  __shared__ __attribute__((aligned(16))) char sWin[WIN];
+  __shared__ __attribute__((aligned(16))) char sA0[ABUF];
+  __shared__ __attribute__((aligned(16))) char sA1[ABUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kr = lane >> 4, jj = lane & 15;
+  const int H = a.H, W = a.W, C = a.C;
+  const int tx = (W + TC - 1) / TC, ntiles = tx * ((H + TR - 1) / TR);
+  // XCD-aware bijective remap: each XCD walks a contiguous range of tiles (shared window rows)
+  const int nwg = gridDim.x, b0 = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b0 & 7;
+  const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b0 >> 3);
+  const int n = bid / ntiles, tile = bid % ntiles;
+  const int y0 = (tile / tx) * TR, x0 = (tile % tx) * TC;
+  const int wy0 = y0 - MG, wx0 = x0 - MG;
+  const int py = y0 + wave, px = x0 + jj;  // this lane's output pixel
+  const bool pv = py < H && px < W;
+  const int P = H * W;
+  const int p4 = (pv ? py * W + px : 0) * 4;
+  const int img_bytes = C * P * 4;
+
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void *)(a.x + (long)n * C * P), (short)0, img_bytes, 0x00020000);
+  const auto offr = __builtin_amdgcn_make_buffer_rsrc((void *)(a.offset + (long)n * a.off_bs), (short)0, 0x7ffffff0, 0x00020000);
+  const auto mskr = __builtin_amdgcn_make_buffer_rsrc((void *)(a.mask + (long)n * a.mask_bs), (short)0, 0x7ffffff0, 0x00020000);
+
+  // ---- window staging: quad q of window position pos -> LDS [q][pos]; 8 consecutive lanes take
+  // one quad of 8 consecutive positions (each wave-instruction covers 8 whole 128-B lines of x,
+  // and 8 consecutive lanes write 8 different LDS banks quads).  Outside the image: zeros.
+  f32x4 wv[NWI];
+  auto load_window = [&](int g) {
+#pragma unroll
+    for (int i = 0; i < NWI; ++i) {
+      const int e = tid + NT * i, q = (e >> 3) & 7, pos = (e & 7) | ((e >> 6) << 3);
+      const int wy = wy0 + pos / WC, wx = wx0 + pos % WC;
+      const bool ok = pos < WR * WC && wy >= 0 && wy < H && wx >= 0 && wx < W;
+      const int off = ok ? ((wy * W + wx) * C + 4 * q) * 4 : img_bytes;
+      wv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, g * 128, 0));
+    }
+  };
+  auto store_window = [&]() {
+#pragma unroll
+    for (int i = 0; i < NWI; ++i) {
+      const int e = tid + NT * i, q = (e >> 3) & 7, pos = (e & 7) | ((e >> 6) << 3);
+      *reinterpret_cast<f32x4 *>(sWin + (q * NPOS + pos) * 16) = wv[i];
+    }
+  };
+
+  // ---- A fragments of chunk c = (group g, tap k): 12 KB, lane-linear, by LDS-DMA one tap ahead
+  const char *wsp = reinterpret_cast<const char *>(a.wsplit);
+  const int ncc = C / 32;
+  auto issue_a = [&](int c, char *dst) {
+    const int g = c / K, k = c - K * (c / K);
+    const char *src = wsp + (long)((k * ncc + g) * 12) * 1024 + lane * 16;
+    for (int pc = wave; pc < 12; pc += 8)
+      __builtin_amdgcn_global_load_lds((const void *)(src + pc * 1024), (lds_void *)(dst + pc * 1024), 16, 0, 0);
+  };
+
+  // ---- sampling state: lane group kr computes tap t0 + kr of this lane's pixel -----------------
+  float poh = 0.f, pow_ = 0.f, pml = 0.f;  // prefetched offsets / mask of the next pass
+  auto load_pass = [&](int g, int t0) {
+    const int t = min(t0 + kr, K - 1);
+    const int oplane = (g * 2 * K + 2 * t) * P * 4, mplane = (g * K + t) * P * 4;
+    poh = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, p4 + oplane, 0, 0));
+    pow_ = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, p4 + oplane + P * 4, 0, 0));
+    pml = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mskr, p4 + mplane, 0, 0));
+  };
+  TapState ps;  // this lane's state for tap t0 + kr
+  auto compute_pass = [&](int t0) {
+    ps = tap_state<DIL, WR, WC>(poh, pow_, pml, py, px, pv, min(t0 + kr, K - 1), H, W, wy0, wx0,
+                                a.mask_logits, a.mask_scale);
+  };
+  auto get_state = [&](int k, int t0) -> TapState {
+    const int src = ((((k - t0) << 4) | jj)) << 2;
+    TapState s;
+    s.pos = __builtin_amdgcn_ds_bpermute(src, ps.pos);
+    s.w0 = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, ps.w0)));
+    s.w1 = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, ps.w1)));
+    s.w2 = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, ps.w2)));
+    s.w3 = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, ps.w3)));
+    return s;
+  };
+
+  f32x4 acc[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // one tap of one group: corners -> blend -> split -> 24 MFMAs
+  auto tap = [&](int g, int k, const char *sAc, const TapState &s) {
+    f32x4 cq[4][2];  // corners TL, TR, BL, BR x channel quads 2kr, 2kr+1
+    const int lpos = (s.pos < 0 || (a.dbg & 2)) ? 0 : s.pos;
+    const char *base = sWin + (lpos + kr * 2 * NPOS) * 16;
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      cq[0][h2] = *reinterpret_cast<const f32x4 *>(base + h2 * NPOS * 16);
+      cq[1][h2] = *reinterpret_cast<const f32x4 *>(base + h2 * NPOS * 16 + 16);
+      cq[2][h2] = *reinterpret_cast<const f32x4 *>(base + h2 * NPOS * 16 + WC * 16);
+      cq[3][h2] = *reinterpret_cast<const f32x4 *>(base + h2 * NPOS * 16 + (WC + 1) * 16);
+    }
+    float v[8];
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float t = cq[0][h2][u] * s.w0;
+        t = __builtin_fmaf(cq[1][h2][u], s.w1, t);
+        t = __builtin_fmaf(cq[2][h2][u], s.w2, t);
+        t = __builtin_fmaf(cq[3][h2][u], s.w3, t);
+        v[4 * h2 + u] = t;
+      }
+    if (!(a.dbg & 4) && __builtin_amdgcn_ballot_w64(s.pos < 0)) {  // wave-uniform: some sample left the window
+      if (s.pos < 0) {
+        // global gather of this lane's corners (blended here, so no load is pending at the join)
+#pragma clang fp contract(off)
+        const int oplane = (g * 2 * K + 2 * k) * P * 4;
+        const float oh = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, p4 + oplane, 0, 0));
+        const float ow = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, p4 + oplane + P * 4, 0, 0));
+        const int i = k / 3, j = k - 3 * (k / 3);
+        const float h = (float)(py - DIL + i * DIL) + oh;
+        const float w = (float)(px - DIL + j * DIL) + ow;
+        const int hl = (int)floorf(h), wl = (int)floorf(w);
+        // pos < 0 only for valid samples; corners outside the image carry weight 0, read as 0
+        const int rb = C * 4, qo = (g * 8 + 2 * kr) * 16;
+        int o[4];
+        o[0] = (hl >= 0 && wl >= 0) ? (hl * W + wl) * rb + qo : img_bytes;
+        o[1] = (hl >= 0 && wl + 1 <= W - 1) ? (hl * W + wl + 1) * rb + qo : img_bytes;
+        o[2] = (hl + 1 <= H - 1 && wl >= 0) ? ((hl + 1) * W + wl) * rb + qo : img_bytes;
+        o[3] = (hl + 1 <= H - 1 && wl + 1 <= W - 1) ? ((hl + 1) * W + wl + 1) * rb + qo : img_bytes;
+        f32x4 gq[4][2];
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2)
+            gq[cc][h2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o[cc], h2 * 16, 0));
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            float t = gq[0][h2][u] * s.w0;
+            t = __builtin_fmaf(gq[1][h2][u], s.w1, t);
+            t = __builtin_fmaf(gq[2][h2][u], s.w2, t);
+            t = __builtin_fmaf(gq[3][h2][u], s.w3, t);
+            v[4 * h2 + u] = t;
+          }
+      }
+    }
+    bf16x8 B[3];
+    split8(v, B);
+    const char *ab = sAc + lane * 16;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      bf16x8 A[3];
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc) A[pc] = *reinterpret_cast<const bf16x8 *>(ab + (m * 3 + pc) * 1024);
+      if (!(a.dbg & 1)) acc[m] = mfma_split6(A, B, acc[m]);
+    }
+  };
+
+  // ---- main loop: 2 deformable groups x 9 taps = 18 chunks, one barrier per chunk --------------
+  // L2 warm-up loads (one dword per 128-B line, results unused): the next group's window lines
+  // during group 0, the epilogue's identity rows during group 1, so those loads hit L2.
+  float pf_win = 0.f, pf_res = 0.f;
+  auto step = [&](int c, const char *cur, char *nxt) {
+    const int g = c >= K ? 1 : 0, k = c - K * g, t0 = k & ~3;
+    if (k == 0) {  // group start: its window (loaded in the chunk before) and pass-0 states
+      if (g == 1) asm volatile("" ::"v"(pf_win));
+      store_window();
+      compute_pass(0);
+      load_pass(g, 4);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of A(c) landed
+      __syncthreads();
+    } else if (k == 4 || k == 8) {
+      compute_pass(k);
+      if (k == 4) load_pass(g, 8);
+    }
+    if (c + 1 < 2 * K) issue_a(c + 1, nxt);
+    if (c == 3 && tid < WR * WC) {
+      const int wy = wy0 + tid / WC, wx = wx0 + tid % WC;
+      const bool ok = wy >= 0 && wy < H && wx >= 0 && wx < W;
+      pf_win = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+          xr, ok ? (wy * W + wx) * C * 4 : img_bytes, 128, 0));
+    }
+    if (c == 12 && a.residual) {
+      const int yy = min(y0 + (tid & 7), H - 1), co2 = min(tid >> 3, a.Co2 - 1);
+      pf_res = a.residual[((long)(n * a.Co2 + co2) * H + yy) * W + x0];
+    }
+    const TapState s = get_state(k, t0);
+    tap(g, k, cur, s);
+    if (c == K - 1) {  // the next group's window and first offsets, behind the MFMAs
+      __builtin_amdgcn_sched_barrier(0);
+      load_window(1);
+      load_pass(1, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of A(c+1) landed ...
+    if (!(a.dbg & 8)) __syncthreads();                 // ... and every other wave's
+  };
+  load_window(0);
+  issue_a(0, sA0);
+  load_pass(0, 0);
+#pragma unroll 1
+  for (int c = 0; c < 2 * K; c += 2) {
+    step(c, sA0, sA1);
+    step(c + 1, sA1, sA0);
+  }
+  asm volatile("" ::"v"(pf_res));
+
+  // ---- tail: BN2 + act -> conv3 (pointwise, split-bf16) ----------------------------------------
+  // conv3's A fragments (24 KB, standard fragment order) by LDS-DMA into the two A slots: K chunk
+  // h2 = 0 (pieces 0-11) into sA0, h2 = 1 into sA1.
+  {
+    const char *src = reinterpret_cast<const char *>(a.tail_wsplit) + lane * 16;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int pc = wave + 8 * r;
+      char *dst = pc < 12 ? sA0 + pc * 1024 : sA1 + (pc - 12) * 1024;
+      __builtin_amdgcn_global_load_lds((const void *)(src + pc * 1024), (lds_void *)dst, 16, 0, 0);
+    }
+  }
+  // The accumulator of co block m holds channels 16m + 4kr + r of pixel jj: for the conv3 K chunk
+  // h2 (channels 32h2..32h2+31) lane group kr supplies {32h2 + 4kr + r, 32h2 + 16 + 4kr + r}, a
+  // permutation of the chunk's K index that the A fragments below are read in.
+  bf16x8 B2[2][3];
+#pragma unroll
+  for (int h2 = 0; h2 < 2; ++h2) {
+    float v[8];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int m = 2 * h2 + half, co = 16 * m + 4 * kr;
+      const f32x4 bs = a.bias ? *reinterpret_cast<const f32x4 *>(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 sc = a.post_scale ? *reinterpret_cast<const f32x4 *>(a.post_scale + co) : f32x4{1.f, 1.f, 1.f, 1.f};
+      const f32x4 sh = a.post_scale ? *reinterpret_cast<const f32x4 *>(a.post_shift + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[4 * half + r] = act_f((acc[m][r] + bs[r]) * sc[r] + sh[r], a.act);
+    }
+    split8(v, B2[h2]);
+  }
+  f32x4 acc2[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) acc2[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed ...
+  __syncthreads();                                   // ... and every other wave's
+  {
+    // standard fragment (cc = h2, blk = m2, piece pc): lane l holds row 16 m2 + (l & 15), channels
+    // 32 h2 + 8 (l >> 4) + 0..7.  Channels 32h2 + 4kr + 0..3 are lane (kr/2)*16 + jj, bytes
+    // 8 (kr & 1); channels 32h2 + 16 + 4kr + 0..3 the same 32 lanes further.
+    const int tl = (((kr >> 1) << 4) | jj) * 16 + 8 * (kr & 1);
+#pragma unroll
+    for (int m2 = 0; m2 < 4; ++m2)
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        bf16x8 A[3];
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) {
+          const char *f = (h2 ? sA1 : sA0) + tl + (m2 * 3 + pc) * 1024;
+          const u32x2 lo = *reinterpret_cast<const u32x2 *>(f);
+          const u32x2 hi = *reinterpret_cast<const u32x2 *>(f + 512);
+          A[pc] = __builtin_bit_cast(bf16x8, u32x4{lo.x, lo.y, hi.x, hi.y});
+        }
+        acc2[m2] = mfma_split6(A, B2[h2], acc2[m2]);
+      }
+  }
+  // ---- epilogue: tile -> LDS [co2][px] -> 16-byte row quads (+ bias, identity, act, CSA) ------
+  float *sO = reinterpret_cast<float *>(sWin);
+#pragma unroll
+  for (int m2 = 0; m2 < 4; ++m2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sO[(16 * m2 + 4 * kr + r) * OP + wave * 16 + jj] = acc2[m2][r];
+  __syncthreads();
+  constexpr int EPT = 64 * TR * (TC / 4) / NT;  // items (4 pixels x 1 channel) per thread
+  const int Co2 = a.Co2;
+  f32x4 ev[EPT], er[EPT];
+  long eo[EPT];
+  bool eok[EPT];
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int e = tid + NT * i, co2 = e >> 5, qi = e & 31, yy = y0 + (qi >> 2), xx = x0 + 4 * (qi & 3);
+    eok[i] = co2 < Co2 && yy < H && xx < W;
+    eo[i] = ((long)(n * Co2 + co2) * H + yy) * W + xx;
+    ev[i] = *reinterpret_cast<const f32x4 *>(sO + co2 * OP + (qi >> 2) * 16 + 4 * (qi & 3));
+    if (eok[i] && a.residual) er[i] = *reinterpret_cast<const f32x4 *>(a.residual + eo[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    if (!eok[i]) continue;
+    const int e = tid + NT * i, co2 = e >> 5, qi = e & 31, yy = y0 + (qi >> 2), xx = x0 + 4 * (qi & 3);
+    const float tb = a.tail_b ? a.tail_b[co2] : 0.f;
+    f32x4 v = ev[i];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float t = v[u] + tb;
+      if (a.residual) t += er[i][u];
+      v[u] = act_f(t, a.tail_act);
+    }
+    *reinterpret_cast<f32x4 *>(a.out + eo[i]) = v;
+    if (a.csa_out) {
+      const long plane = (long)n * Co2 + co2;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (j >= a.num_up) break;
+        const int ih = a.up_h[j], iw = a.up_w[j];
+        v += upsample_quad(a.up[j] + plane * ih * iw, ih, iw, (float)ih / (float)H, a.up_r[j], yy, xx >> 2);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = act_f(v[u], a.csa_act);
+      *reinterpret_cast<f32x4 *>(a.csa_out + eo[i]) = v;
+    }
+  }
+}
+
+int window_enabled() {
+  static const int on = [] {
+    const char *e = getenv("AANET_DCN_WINDOW");
+    return e ? atoi(e) : 1;
+  }();
+  return on;
+}
+
+}  // namespace
+
+int dcn_tile_supported(int c, int co, int co2, int kh, int kw, int stride, int pad, int dil,
+                       int dg, int groups, int w) {
+  return window_enabled() && c == 64 && co == 64 && co2 == 64 && kh == 3 && kw == 3 &&
+         stride == 1 && pad == dil && dil == 2 && dg == 2 && groups == 1 && w % 4 == 0;
+}
+
+int dcn_tile_launch(const DcnTileArgs &a, hipStream_t stream) {
+  if (!dcn_tile_supported(a.C, a.Co, a.Co2, 3, 3, 1, a.dil, a.dil, a.dg, 1, a.W))
+    return AANET_EUNSUPPORTED;
+  if (!a.x || !a.offset || !a.mask || !a.wsplit || !a.tail_wsplit || !a.out) return AANET_EINVAL;
+  if (a.post_scale && !a.post_shift) return AANET_EINVAL;
+  if (a.csa_out) {
+    if (a.num_up < 0 || a.num_up > 2) return AANET_EUNSUPPORTED;
+    for (int j = 0; j < a.num_up; ++j) {
+      const int r = a.up_r[j];
+      if (!a.up[j] || (r != 2 && r != 4) || a.up_h[j] * r != a.H || a.up_w[j] * r != a.W)
+        return AANET_EUNSUPPORTED;
+    }
+  }
+  const long P = (long)a.H * a.W;
+  // 32-bit buffer offsets: one image of x, and the offset/mask planes of one image
+  if ((long)a.C * P * 4 >= (1L << 31) || (long)(2 * a.dg * 27) * P * 4 >= (1L << 31))
+    return AANET_EUNSUPPORTED;
+  const long tiles = (long)host_div_up(a.W, TC) * host_div_up(a.H, TR);
+  static const int dbg = [] { const char *e = getenv("AANET_DCN_DBG"); return e ? atoi(e) : 0; }();
+  DcnTileArgs b = a;
+  b.dbg = dbg;
+  hipLaunchKernelGGL(dcn_tile_kernel<2>, dim3((unsigned)(a.N * tiles)), dim3(NT), 0, stream, b);
+  return aanet_launch_status();
+}

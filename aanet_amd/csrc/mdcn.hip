@@ -14,6 +14,7 @@
 // floor / bilinear follow kernel.cu:467-497 with fp contraction disabled, so im2col values
 // and sampling indices equal the CPU oracle's bit for bit (tests/test_gpu_mdcn.py).
 #include "common.h"
+#include "dcn_tile.h"
 
 #include <stdlib.h>
 
@@ -2150,7 +2151,8 @@ extern "C" int aanet_mdcn_pw_f32(const float *x, const float *offset, long offse
                                  aanet_stream_t stream) {
   if (act < 0 || act > 2 || pw_act < 0 || pw_act > 2 || !pw_weight_packed) return AANET_EINVAL;
   const int flags = layout;
-  layout &= ~(AANET_CONV_EXACT_F32 | AANET_CONV_WEIGHTS_SPLIT);
+  const bool generic = (layout & AANET_CONV_GENERIC_DCN) != 0;
+  layout &= ~(AANET_CONV_EXACT_F32 | AANET_CONV_WEIGHTS_SPLIT | AANET_CONV_GENERIC_DCN);
   if (layout != 0 && layout != 1) return AANET_EINVAL;
   MdcnArgs a = make_args(x, offset, offset_batch_stride, mask, mask_batch_stride, mask_logits,
                          mask_scale, weight_packed, bias, post_scale, post_shift, act, out, n, c,
@@ -2164,6 +2166,48 @@ extern "C" int aanet_mdcn_pw_f32(const float *x, const float *offset, long offse
   a.Co2 = co2;
   a.residual = residual;
   set_split(a, flags, 1);
+  // the deformable bottleneck tail of the aggregation: LDS-window form (dcn_tile.hip)
+  if (!generic && a.split && layout == 1 && a.Ho == h && a.Wo == w &&
+      dcn_tile_supported(c, co, co2, kh, kw, stride, pad, dil, dg, 1, w)) {
+    DcnTileArgs t;
+    t.x = x;
+    t.offset = a.offset;
+    t.off_bs = a.off_bs;
+    t.mask = a.mask;
+    t.mask_bs = a.mask_bs;
+    t.mask_logits = mask_logits;
+    t.mask_scale = mask_scale;
+    t.wsplit = a.wsplit;
+    t.bias = bias;
+    t.post_scale = post_scale;
+    t.post_shift = post_shift;
+    t.act = act;
+    t.tail_wsplit = a.tail_wsplit;
+    t.tail_b = pw_bias;
+    t.tail_act = pw_act;
+    t.residual = residual;
+    t.out = out;
+    t.csa_out = a.csa_out;
+    t.num_up = a.csa_out ? a.num_up : 0;
+    t.csa_act = a.csa_act;
+    for (int j = 0; j < 2; ++j) {
+      t.up[j] = a.up[j];
+      t.up_h[j] = a.up_h[j];
+      t.up_w[j] = a.up_w[j];
+      t.up_r[j] = a.up_r[j];
+    }
+    t.N = n;
+    t.C = c;
+    t.H = h;
+    t.W = w;
+    t.Co = co;
+    t.Co2 = co2;
+    t.dil = dil;
+    t.dg = dg;
+    t.dbg = 0;
+    const int rc2 = (a.csa_out && a.num_up > 2) ? AANET_EUNSUPPORTED : dcn_tile_launch(t, as_hip(stream));
+    if (rc2 != AANET_EUNSUPPORTED) return rc2;
+  }
   return launch_fwd<1>(a, 1, as_hip(stream));
 }
 

@@ -304,9 +304,10 @@ def conv2d_pw(x, weight, packed_weight, bias, post_scale, post_shift, act, pw_pa
 
 def mdcn_pw(x, offset_mask, weight, packed_weight, bias, post_scale, post_shift, act, pw_packed,
             pw_bias, residual=None, pw_act=None, stride=1, padding=0, dilation=1,
-            deformable_groups=1, mask_scale=2.0, csa_up=None, csa_act="leaky"):
+            deformable_groups=1, mask_scale=2.0, csa_up=None, csa_act="leaky", generic_dcn=False):
     """DCN (offset/mask read in place from offset_conv's output) + fused pointwise tail.
-    x may be channels_last (NHWC corner loads); the output is NCHW.  csa_up: as conv2d_pw."""
+    x may be channels_last (NHWC corner loads); the output is NCHW.  csa_up: as conv2d_pw.
+    generic_dcn: keep the generic engine where the LDS-window tail would run (A/B, tests)."""
     require_gpu(x, offset_mask, packed_weight, bias, post_scale, post_shift, pw_packed, pw_bias,
                 residual, nhwc_ok=(0,))
     N, C, H, W = x.shape
@@ -325,7 +326,8 @@ def mdcn_pw(x, offset_mask, weight, packed_weight, bias, post_scale, post_shift,
          ACT[act], ptr(pw_packed), ptr(pw_bias), ptr(residual), ACT[pw_act], Co2, ptr(out), N, C,
          H, W, Co, kh, kw, stride, padding, dilation, deformable_groups,
          None if desc is None else _lib.ctypes.byref(desc),
-         (_lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0) | _lib.conv_flags(packed_weight, pw_packed),
+         (_lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0) | _lib.conv_flags(packed_weight, pw_packed)
+         | (_lib.CONV_GENERIC_DCN if generic_dcn else 0),
          stream_of(x))
     return out if desc is None else (out, csa_out)
 

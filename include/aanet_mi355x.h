@@ -46,7 +46,12 @@ enum {
   /* The weight buffers (weight_packed, and pw_weight_packed of the tail kernels) come from
    * aanet_conv_weight_pack_split_f32: the f32 packed weights followed by their bf16 piece
    * fragments.  Without it the engine runs the exact f32 contraction. */
-  AANET_CONV_WEIGHTS_SPLIT = 16
+  AANET_CONV_WEIGHTS_SPLIT = 16,
+  /* aanet_mdcn_pw_f32 only: run the generic implicit-GEMM engine even where the LDS-window
+   * deformable tail (3x3, stride 1, pad = dil = 2, 64 channels in two 32-channel deformable
+   * groups, NHWC input, split weights) would take the shape.  Same results to
+   * fp32 rounding; for A/B measurements and parity tests. */
+  AANET_CONV_GENERIC_DCN = 32
 };
 
 int aanet_version(void);

@@ -62,6 +62,9 @@ cases = {
     "csa_sum": (lambda: ops.csa_sum([x, up1, up2]), 0),
     "dcn_pw_nhwc_csa": (lambda: ops.mdcn_pw(xn, om, w3, p3, None, b, b, "relu", p1, b, res, "relu", 1, 2, 2, 2,
                                             csa_up=[up1f, up2f]), 2 * B * H * W * C * C * 10),
+    "dcn_pw_nhwc_csa_generic": (lambda: ops.mdcn_pw(xn, om, w3, p3, None, b, b, "relu", p1, b, res, "relu", 1, 2,
+                                                    2, 2, csa_up=[up1f, up2f], generic_dcn=True),
+                                2 * B * H * W * C * C * 10),
     "conv3x3_pw_nhwc_csa": (lambda: ops.conv2d_pw(xn, w3, p3, b, None, None, "relu", p1, b, res, "relu", 1, 1, 1,
                                                   csa_up=[up1f, up2f]), 2 * B * H * W * C * C * 10),
     # the fusion layers' scale 0 -> 1 exchange convs (3x3 stride 2, NCHW input)
