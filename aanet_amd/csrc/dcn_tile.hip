@@ -157,7 +157,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   // ---- window staging: quad q of window position pos -> LDS [q][pos]; 8 consecutive lanes take
   // one quad of 8 consecutive positions (each wave-instruction covers 8 whole 128-B lines of x,
   // and 8 consecutive lanes write 8 different LDS banks quads).  Outside the image: zeros.
-  f32x4 wv[NWI];
+  f32x4 wv[NWI] = {};
   auto load_window = [&](int g) {
 #pragma unroll
     for (int i = 0; i < NWI; ++i) {
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       const int wy = wy0 + pos / WC, wx = wx0 + pos % WC;
       const bool ok = pos < WR * WC && wy >= 0 && wy < H && wx >= 0 && wx < W;
       const int off = ok ? ((wy * W + wx) * C + 4 * q) * 4 : img_bytes;
-      wv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, g * 128, 0));
+      if (!(a.dbg & 32)) wv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, g * 128, 0));
     }
   };
   auto store_window = [&]() {
@@ -180,6 +180,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   const char *wsp = reinterpret_cast<const char *>(a.wsplit);
   const int ncc = C / 32;
   auto issue_a = [&](int c, char *dst) {
+    if (a.dbg & 64) return;
     const int g = c / K, k = c - K * (c / K);
     const char *src = wsp + (long)((k * ncc + g) * 12) * 1024 + lane * 16;
     for (int pc = wave; pc < 12; pc += 8)
@@ -407,11 +408,15 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
     eok[i] = co2 < Co2 && yy < H && xx < W;
     eo[i] = ((long)(n * Co2 + co2) * H + yy) * W + xx;
     ev[i] = *reinterpret_cast<const f32x4 *>(sO + co2 * OP + (qi >> 2) * 16 + 4 * (qi & 3));
-    if (eok[i] && a.residual) er[i] = *reinterpret_cast<const f32x4 *>(a.residual + eo[i]);
+    if (eok[i] && a.residual && !(a.dbg & 16)) er[i] = *reinterpret_cast<const f32x4 *>(a.residual + eo[i]);
   }
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
     if (!eok[i]) continue;
+    if (a.dbg & 16) {  // no epilogue traffic (keeps the work alive)
+      if (ev[i][0] == 12345.f) a.out[eo[i]] = ev[i][1];
+      continue;
+    }
     const int e = tid + NT * i, co2 = e >> 5, qi = e & 31, yy = y0 + (qi >> 2), xx = x0 + 4 * (qi & 3);
     const float tb = a.tail_b ? a.tail_b[co2] : 0.f;
     f32x4 v = ev[i];

@@ -852,24 +852,26 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   }
 
   if constexpr (HALO) {
-    const int d = a.dil;
-    const int hw = 16 + 2 * d, npos = (8 + 2 * d) * hw;
+    constexpr int d = HALO;  // the dilation (= padding): halo geometry is compile-time
+    constexpr int hw = 16 + 2 * d, npos = (8 + 2 * d) * hw;
     const int hy = hy0 - d, hx = hx0 - d;
-    constexpr int HIT = 4;  // halo quads per thread: npos * 8 <= 4 * FNT for d <= 2
-    int hoff[HIT];
-#pragma unroll
-    for (int i = 0; i < HIT; ++i) {
-      const int e = tid + FNT * i, pos = e >> 3;
-      const int yy = hy + pos / hw, xx = hx + pos % hw;
-      const bool ok = pos < npos && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
-      hoff[i] = ok ? ((yy * a.W + xx) * a.C + 4 * (e & 7)) * 4 : img_bytes;  // zero padding: OOB
-    }
+    constexpr int HIT = (npos * 8 + FNT - 1) / FNT;  // halo quads per thread
     f32x4 hv[HIT];
+    // 64-channel tiles recompute the halo quad offsets per chunk (a few VALU) rather than hold
+    // them across the chunk loop: held, they were spilled to scratch and re-read every chunk
+    // (76 B/lane at the 128-VGPR cap).  32-channel tiles have the registers to hold them.
     auto load_halo = [&](int c0) {
       const int soff = __builtin_amdgcn_readfirstlane(c0 * 4);
+      int t = tid;
+      if constexpr (CO_T >= 64) asm volatile("" : "+v"(t));  // keep the arithmetic in the loop
 #pragma unroll
-      for (int i = 0; i < HIT; ++i)
-        hv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, hoff[i], soff, 0));
+      for (int i = 0; i < HIT; ++i) {
+        const int e = t + FNT * i, pos = e >> 3;
+        const int yy = hy + pos / hw, xx = hx + pos % hw;
+        const bool ok = pos < npos && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+        const int off = ok ? ((yy * a.W + xx) * a.C + 4 * (e & 7)) * 4 : img_bytes;  // zero padding: OOB
+        hv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, soff, 0));
+      }
     };
     bf16x8 ha0[NCB][3], ha1[NCB][3];  // A fragments of two taps (double buffer)
     // A fragments by buffer loads: per-lane offset lane*16 (one VGPR), everything else in the
@@ -1830,13 +1832,22 @@ void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
       return;
     }
     if constexpr (MODE == 0 && PTT == 128) {
-      if (a.split && packed && a.halo) {  // 3x3 stride-1 halo-tile form (NHWC input)
-        if (a.tail_w)
-          hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 1, 1, 1, 1, CFG, 1, 1>), grid, blk, 0, st, a);
-        else if (a.layout == 3)
-          hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 0, 1, 1, 3, CFG, 1, 1>), grid, blk, 0, st, a);
-        else
-          hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 0, 1, 1, 1, CFG, 1, 1>), grid, blk, 0, st, a);
+      if (a.split && packed && a.halo) {  // 3x3 stride-1 halo-tile form (NHWC input), HALO = dil
+        if (a.dil == 1) {
+          if (a.tail_w)
+            hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 1, 1, 1, 1, CFG, 1, 1>), grid, blk, 0, st, a);
+          else if (a.layout == 3)
+            hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 0, 1, 1, 3, CFG, 1, 1>), grid, blk, 0, st, a);
+          else
+            hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 0, 1, 1, 1, CFG, 1, 1>), grid, blk, 0, st, a);
+        } else {
+          if (a.tail_w)
+            hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 1, 1, 1, 1, CFG, 1, 2>), grid, blk, 0, st, a);
+          else if (a.layout == 3)
+            hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 0, 1, 1, 3, CFG, 1, 2>), grid, blk, 0, st, a);
+          else
+            hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 0, 1, 1, 1, CFG, 1, 2>), grid, blk, 0, st, a);
+        }
         return;
       }
     }
