@@ -399,16 +399,38 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   __syncthreads();
   constexpr int EPT = 64 * TR * (TC / 4) / NT;  // items (4 pixels x 1 channel) per thread
   const int Co2 = a.Co2;
-  f32x4 ev[EPT], er[EPT];
+  // every global load of the thread's items (identity, bias, the CSA terms' source segments) is
+  // issued before the first use: the item loop would otherwise pay one L2/HBM round trip per
+  // item and term (the stores may alias the sources, so the compiler cannot hoist them)
+  f32x4 ev[EPT], er[EPT], eu[EPT][2][2];
+  float eb[EPT];
   long eo[EPT];
   bool eok[EPT];
+  const bool res = a.residual && !(a.dbg & 16), csa = a.csa_out && !(a.dbg & 16);
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
     const int e = tid + NT * i, co2 = e >> 5, qi = e & 31, yy = y0 + (qi >> 2), xx = x0 + 4 * (qi & 3);
     eok[i] = co2 < Co2 && yy < H && xx < W;
     eo[i] = ((long)(n * Co2 + co2) * H + yy) * W + xx;
     ev[i] = *reinterpret_cast<const f32x4 *>(sO + co2 * OP + (qi >> 2) * 16 + 4 * (qi & 3));
-    if (eok[i] && a.residual && !(a.dbg & 16)) er[i] = *reinterpret_cast<const f32x4 *>(a.residual + eo[i]);
+    if (!eok[i]) continue;
+    eb[i] = a.tail_b ? a.tail_b[co2] : 0.f;
+    if (res) er[i] = *reinterpret_cast<const f32x4 *>(a.residual + eo[i]);
+    if (csa) {
+      const long plane = (long)n * Co2 + co2;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (j >= a.num_up) break;
+        const int ih = a.up_h[j], iw = a.up_w[j], r = a.up_r[j];
+        float hr = ((float)ih / (float)H) * ((float)yy + 0.5f) - 0.5f;
+        hr = hr < 0.f ? 0.f : hr;
+        const int h1 = (int)hr, h1p = h1 < ih - 1 ? 1 : 0;
+        const float *im = a.up[j] + plane * ih * iw;
+        const int s0 = r == 2 ? 2 * (xx >> 2) - 1 : (xx >> 2) - 1;
+        eu[i][j][0] = load_seg(im + (long)h1 * iw, iw, s0);
+        eu[i][j][1] = load_seg(im + (long)(h1 + h1p) * iw, iw, s0);
+      }
+    }
   }
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
@@ -417,23 +439,24 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       if (ev[i][0] == 12345.f) a.out[eo[i]] = ev[i][1];
       continue;
     }
-    const int e = tid + NT * i, co2 = e >> 5, qi = e & 31, yy = y0 + (qi >> 2), xx = x0 + 4 * (qi & 3);
-    const float tb = a.tail_b ? a.tail_b[co2] : 0.f;
+    const int e = tid + NT * i, qi = e & 31, yy = y0 + (qi >> 2);
     f32x4 v = ev[i];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      float t = v[u] + tb;
-      if (a.residual) t += er[i][u];
+      float t = v[u] + eb[i];
+      if (res) t += er[i][u];
       v[u] = act_f(t, a.tail_act);
     }
     *reinterpret_cast<f32x4 *>(a.out + eo[i]) = v;
-    if (a.csa_out) {
-      const long plane = (long)n * Co2 + co2;
+    if (csa) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         if (j >= a.num_up) break;
-        const int ih = a.up_h[j], iw = a.up_w[j];
-        v += upsample_quad(a.up[j] + plane * ih * iw, ih, iw, (float)ih / (float)H, a.up_r[j], yy, xx >> 2);
+        const int ih = a.up_h[j];
+        float hr = ((float)ih / (float)H) * ((float)yy + 0.5f) - 0.5f;
+        hr = hr < 0.f ? 0.f : hr;
+        const float h1l = hr - (float)(int)hr, h0l = 1.f - h1l;
+        v += h0l * hlerp(eu[i][j][0], a.up_r[j]) + h1l * hlerp(eu[i][j][1], a.up_r[j]);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) v[u] = act_f(v[u], a.csa_act);
