@@ -48,18 +48,20 @@ struct CorrSmem {
 // two stages (24 KB per workgroup) are in flight.  L is read once: non-temporal loads; the
 // volume is written once: non-temporal stores (tools/corr_lab.hip: -6 % vs default policy).
 // R keeps the default policy, because the neighbouring tile re-reads half of its window from L2.
+__device__ __forceinline__ int xcd_remap(int nwg, int b0) {  // bijective for any grid size
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b0 & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b0 >> 3);
+}
+
+// One workgroup of the correlation: work item `id` of one volume (x tile fastest, then d chunk,
+// row, image).  smem: CorrSmem<NJ>::BYTES.
 template <int NJ, int VEC>
-__global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
-    const float *__restrict__ L, const float *__restrict__ R, float *__restrict__ out, int C,
-    int H, int W, int D, int dchunk, int ntx, int nchunks) {
+__device__ __forceinline__ void corr_tile(const float *__restrict__ L, const float *__restrict__ R,
+                                          float *__restrict__ out, int C, int H, int W, int D,
+                                          int dchunk, int ntx, int nchunks, int id, float *smem) {
   using S = CorrSmem<NJ>;
   constexpr int RW = S::RW;
-  __shared__ __attribute__((aligned(16))) float smem[S::BYTES / 4];
-
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nwg = gridDim.x, b0 = blockIdx.x;
-  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b0 & 7;
-  int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b0 >> 3);
   const int tx = id % ntx;
   id /= ntx;
   const int chunk = id % nchunks;
@@ -219,6 +221,63 @@ __global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
         __builtin_nontemporal_store(sO[dl * S::OUTP + xl],
                                     out + (((long)b * D + d0 + dl) * H + y) * W + x0 + xl);
     }
+  }
+}
+
+template <int NJ, int VEC>
+__global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
+    const float *__restrict__ L, const float *__restrict__ R, float *__restrict__ out, int C,
+    int H, int W, int D, int dchunk, int ntx, int nchunks) {
+  __shared__ __attribute__((aligned(16))) float smem[CorrSmem<NJ>::BYTES / 4];
+  corr_tile<NJ, VEC>(L, R, out, C, H, W, D, dchunk, ntx, nchunks, xcd_remap(gridDim.x, blockIdx.x),
+                     smem);
+}
+
+// The whole pyramid (nets/cost.py:58-76) in ONE launch: a scale-major work list (scale 0's
+// tiles first), XCD-contiguous as in the single-volume kernel; a workgroup runs the tile code
+// instantiated for its scale's band width, so the coarse scales fill the chip while scale 0's
+// last tiles drain instead of running as separate, under-filled launches.
+constexpr int MAXS = 4;
+struct CorrPyramid {
+  const float *L[MAXS], *R[MAXS];
+  float *out[MAXS];
+  int C[MAXS], H[MAXS], W[MAXS], D[MAXS], dchunk[MAXS], ntx[MAXS], nchunks[MAXS], nj[MAXS];
+  int start[MAXS + 1];
+  int ns;
+};
+
+__global__ __launch_bounds__(NTHREADS) void corr_pyramid_kernel(CorrPyramid p) {
+  __shared__ __attribute__((aligned(16))) float smem[CorrSmem<5>::BYTES / 4];
+  const int id = xcd_remap(gridDim.x, blockIdx.x);
+  int s = 0;
+  while (s + 1 < p.ns && id >= p.start[s + 1]) ++s;
+  const int local = id - p.start[s];
+#define AANET_CORR_CASE(J) \
+  case J: corr_tile<J, 1>(p.L[s], p.R[s], p.out[s], p.C[s], p.H[s], p.W[s], p.D[s], p.dchunk[s], \
+                          p.ntx[s], p.nchunks[s], local, smem); break;
+  switch (p.nj[s]) {
+    AANET_CORR_CASE(1)
+    AANET_CORR_CASE(2)
+    AANET_CORR_CASE(3)
+    AANET_CORR_CASE(4)
+    default: corr_tile<5, 1>(p.L[s], p.R[s], p.out[s], p.C[s], p.H[s], p.W[s], p.D[s], p.dchunk[s],
+                             p.ntx[s], p.nchunks[s], local, smem);
+  }
+#undef AANET_CORR_CASE
+}
+
+int corr_nj(int max_disp) {
+  const int dneed = max_disp < 64 ? max_disp : 64;
+  return dneed <= 1 ? 1 : 1 + (dneed - 1 + 15) / 16;
+}
+
+int corr_dchunk(int nj) {
+  switch (nj) {
+    case 1: return CorrSmem<1>::DC;
+    case 2: return CorrSmem<2>::DC;
+    case 3: return CorrSmem<3>::DC;
+    case 4: return CorrSmem<4>::DC;
+    default: return CorrSmem<5>::DC;
   }
 }
 
@@ -445,7 +504,40 @@ extern "C" int aanet_corr_pyramid_f32(int num_scales, const float *const *left,
                                       const float *const *right, float *const *out, const int *c,
                                       const int *h, const int *w, int n, int max_disp,
                                       aanet_stream_t stream) {
-  AANET_HOST_CHECK(num_scales > 0 && left && right && out && c && h && w);
+  AANET_HOST_CHECK(num_scales > 0 && left && right && out && c && h && w && n > 0);
+  // one launch when every scale takes the vector tile path (w % 4 == 0, 32-bit offsets)
+  bool one = num_scales <= MAXS;
+  CorrPyramid p;
+  p.ns = num_scales;
+  long total = 0;
+  for (int s = 0; one && s < num_scales; ++s) {
+    const int d = max_disp >> s;
+    AANET_HOST_CHECK(left[s] && right[s] && out[s] && c[s] > 0 && h[s] > 0 && w[s] > 0 && d > 0);
+    if (w[s] % 4 || (long)c[s] * h[s] * w[s] * 4 >= 0x7fffffffL) {
+      one = false;
+      break;
+    }
+    p.L[s] = left[s];
+    p.R[s] = right[s];
+    p.out[s] = out[s];
+    p.C[s] = c[s];
+    p.H[s] = h[s];
+    p.W[s] = w[s];
+    p.D[s] = d;
+    p.nj[s] = corr_nj(d);
+    p.dchunk[s] = corr_dchunk(p.nj[s]);
+    p.nchunks[s] = host_div_up(d, p.dchunk[s]);
+    p.ntx[s] = host_div_up(w[s], TX);
+    p.start[s] = (int)total;
+    total += (long)p.ntx[s] * p.nchunks[s] * h[s] * n;
+    if (total > 0x7fffffffL) one = false;
+  }
+  if (one) {
+    p.start[num_scales] = (int)total;
+    hipLaunchKernelGGL(corr_pyramid_kernel, dim3((unsigned)total), dim3(NTHREADS), 0,
+                       as_hip(stream), p);
+    return aanet_launch_status();
+  }
   for (int s = 0; s < num_scales; ++s) {
     const int d = max_disp >> s;
     const int rc = aanet_corr_volume_f32(left[s], right[s], out[s], n, c[s], h[s], w[s], d, stream);

@@ -6,7 +6,7 @@ Same constructor signatures, defaults, forward arity and return types as the ref
 """
 import torch.nn as nn
 
-from ..ops import CorrelationVolumeFunction, ShiftVolumeFunction
+from ..ops import CorrelationPyramidFunction, CorrelationVolumeFunction, ShiftVolumeFunction
 
 
 class CostVolume(nn.Module):
@@ -35,8 +35,12 @@ class CostVolumePyramid(nn.Module):
         self.feature_similarity = feature_similarity
 
     def forward(self, left_feature_pyramid, right_feature_pyramid):
-        """nets/cost.py:64-76: scale s uses max_disp // 2**s; returns [H/3, H/6, H/12]."""
+        """nets/cost.py:64-76: scale s uses max_disp // 2**s; returns [H/3, H/6, H/12].
+        Correlation: all scales in one launch (aanet_corr_pyramid_f32)."""
         num_scales = len(left_feature_pyramid)
+        if self.feature_similarity == 'correlation' and num_scales > 0:
+            return list(CorrelationPyramidFunction.apply(
+                self.max_disp, num_scales, *left_feature_pyramid, *right_feature_pyramid))
         cost_volume_pyramid = []
         for s in range(num_scales):
             max_disp = self.max_disp // (2 ** s)

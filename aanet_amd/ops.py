@@ -29,6 +29,27 @@ def corr_volume(left, right, max_disp, out=None):
     return out
 
 
+def corr_pyramid(lefts, rights, max_disp):
+    """nets/cost.py:58-76 (correlation): scale s -> [B, max_disp >> s, H_s, W_s], every scale in
+    ONE launch (aanet_corr_pyramid_f32)."""
+    ns = len(lefts)
+    if ns == 0 or len(rights) != ns:
+        raise ValueError("left/right pyramids must have the same, non-zero number of scales")
+    require_gpu(*lefts, *rights)
+    B = lefts[0].shape[0]
+    outs = []
+    for s, (l, r) in enumerate(zip(lefts, rights)):
+        if l.shape != r.shape or l.shape[0] != B:
+            raise ValueError("left/right feature shapes differ")
+        outs.append(torch.empty((B, max_disp >> s) + tuple(l.shape[2:]), device=l.device, dtype=l.dtype))
+    arr = lambda ts: (_lib.ctypes.c_void_p * ns)(*[t.data_ptr() for t in ts])  # noqa: E731
+    ints = lambda vals: (_lib.ctypes.c_int * ns)(*vals)  # noqa: E731
+    call("aanet_corr_pyramid_f32", ns, arr(lefts), arr(rights), arr(outs),
+         ints([l.shape[1] for l in lefts]), ints([l.shape[2] for l in lefts]),
+         ints([l.shape[3] for l in lefts]), B, max_disp, stream_of(lefts[0]))
+    return outs
+
+
 def shift_volume(left, right, max_disp, concat):
     """nets/cost.py:22-38 (difference / concat) -> [B, C', D, H, W]."""
     require_gpu(left, right, names=("left", "right"))
@@ -59,6 +80,40 @@ class CorrelationVolumeFunction(Function):
         call("aanet_corr_volume_bwd_f32", ptr(left), ptr(right), ptr(grad_out), ptr(gl), ptr(gr),
              B, C, H, W, ctx.max_disp, stream_of(left))
         return gl, gr, None
+
+
+class CorrelationPyramidFunction(Function):
+    """CostVolumePyramid (correlation) forward in one launch; backward per scale
+    (aanet_corr_volume_bwd_f32).  apply(max_disp, ns, *lefts, *rights) -> ns volumes."""
+
+    @staticmethod
+    def forward(ctx, max_disp, ns, *feats):
+        lefts = [t.contiguous() for t in feats[:ns]]
+        rights = [t.contiguous() for t in feats[ns:]]
+        ctx.save_for_backward(*lefts, *rights)
+        ctx.max_disp, ctx.ns = max_disp, ns
+        return tuple(corr_pyramid(lefts, rights, max_disp))
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, *grads):
+        saved = ctx.saved_tensors
+        ns = ctx.ns
+        gls, grs = [], []
+        for s in range(ns):
+            left, right = saved[s], saved[ns + s]
+            if grads[s] is None:
+                gls.append(None)
+                grs.append(None)
+                continue
+            g = grads[s].contiguous()
+            gl, gr = torch.empty_like(left), torch.empty_like(right)
+            B, C, H, W = left.shape
+            call("aanet_corr_volume_bwd_f32", ptr(left), ptr(right), ptr(g), ptr(gl), ptr(gr),
+                 B, C, H, W, ctx.max_disp >> s, stream_of(left))
+            gls.append(gl)
+            grs.append(gr)
+        return (None, None, *gls, *grs)
 
 
 class ShiftVolumeFunction(Function):

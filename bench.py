@@ -151,6 +151,12 @@ def kernel_rooflines(model, left, right, batch, iters):
     ms = time_events(lambda: ops.corr_volume(left[0], right[0], MAXD), iters, stream)
     res["corr_volume_s0"] = dict(bound="hbm", ms=ms, algo=corr_bytes, unit="GB/s",
                                  achieved=corr_bytes / ms / 1e6, peak=HBM_PEAK_GBS)
+    # the whole correlation pyramid in one launch (CostVolumePyramid, nets/cost.py:58-76)
+    pyr_bytes = sum(4 * (2 * B * C * (H >> s) * (W >> s) + B * (MAXD >> s) * (H >> s) * (W >> s))
+                    for s in range(len(left)))
+    ms = time_events(lambda: ops.corr_pyramid(left, right, MAXD), iters, stream)
+    res["corr_pyramid"] = dict(bound="hbm", ms=ms, algo=pyr_bytes, unit="GB/s",
+                               achieved=pyr_bytes / ms / 1e6, peak=HBM_PEAK_GBS)
     # regression, scale 0
     vol = ops.corr_volume(left[0], right[0], MAXD)
     reg_bytes = 4 * (B * MAXD * H * W + B * H * W)
@@ -689,6 +695,8 @@ def profile_only(args, model, left, right, step):
         fn = step
     elif args.only == "corr":
         fn = lambda: ops.corr_volume(left[0], right[0], MAXD)  # noqa: E731
+    elif args.only == "pyramid":
+        fn = lambda: ops.corr_pyramid(left, right, MAXD)  # noqa: E731
     elif args.only == "regress":
         vol = ops.corr_volume(left[0], right[0], MAXD)
         fn = lambda: ops.disp_regress(vol)  # noqa: E731
