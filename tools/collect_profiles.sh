@@ -3,7 +3,7 @@
 # (2) separate PMC passes (FETCH_SIZE / WRITE_SIZE, SQ counters) over the per-kernel roofline loop.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${TAG:-r01}
+TAG=${TAG:-r02}
 OUT=$R/gpurun_out/profiles_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
