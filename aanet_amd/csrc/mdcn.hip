@@ -66,6 +66,7 @@ struct Samp {
   float w1, w2, w3, w4;
   float m;
   float lh, lw;   // fractional parts (backward)
+  int hl, wl;     // floor of the sampling position (backward window form)
   int valid;
   int ok;         // corner validity bits (backward)
 };
@@ -91,6 +92,8 @@ __device__ __forceinline__ void make_samp(Samp &s, float h, float w, int H, int 
   s.m = m;
   s.lh = lh;
   s.lw = lw;
+  s.hl = hl;
+  s.wl = wl;
   s.valid = valid;
   s.ok = (ok1 ? 1 : 0) | (ok2 ? 2 : 0) | (ok3 ? 4 : 0) | (ok4 ? 8 : 0);
 }
@@ -1564,6 +1567,222 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_nhwc_kernel(MdcnArgs a, cons
   }
 }
 
+// Window form of mdcn_bwd_data_nhwc_kernel (stride 1, <= 32 channels per deformable group): the
+// workgroup owns an 8 x 8 output tile and accumulates its grad_x corner contributions for one
+// deformable group in an LDS copy of the tile's input window (rows/cols [origin, origin + WR/WC),
+// the corners of every offset in [-R, R)) with LDS atomics, then adds the window to the global
+// NHWC accumulator once: one global atomic per window element instead of one per (pixel, tap,
+// corner, channel) -- 9 x 4 x 64 / (WR x WC) times fewer.  Corners outside the window take the
+// global atomic directly.  DET: the same integer fixed-point contributions as the atomic form,
+// summed in int64 (LDS and global), so the result stays independent of the order.
+// dynamic LDS: sG [Co][GP], sWt [KC][WTP], sCg [KC][CP], sS [PT][16], window [WR*WC][cpg]
+template <int DET>
+__global__ __launch_bounds__(NT) void mdcn_bwd_data_win_kernel(MdcnArgs a, const float *__restrict__ xh,
+                                                               const float *__restrict__ wT,
+                                                               const float *__restrict__ gout,
+                                                               float *__restrict__ gx,
+                                                               float *__restrict__ goff,
+                                                               float *__restrict__ gmask, int GP,
+                                                               int WTP, long long *__restrict__ gxi,
+                                                               const double *__restrict__ det_scale,
+                                                               int WR, int WCc, int R) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int Co = a.Co;
+  float *sG = sm;                       // [Co][GP]      gOut tile
+  float *sWt = sG + Co * GP;            // [KC][WTP]     W^T chunk
+  float *sCg = sWt + KC * WTP;          // [KC][CP]      colg chunk
+  float *sS = sCg + KC * CP;            // [PT][16]      per-pixel corners, weights, mask, window pos
+  void *sAcc = sS + PT * 16;            // [WR*WC][cpg]  float or int64 window accumulator
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long P = (long)a.Ho * a.Wo;
+  const int ttx = (a.Wo + 7) / 8, tpi = ttx * ((a.Ho + 7) / 8);
+  const int n = blockIdx.x / tpi, tile = blockIdx.x % tpi, g = blockIdx.y;
+  const int ty0 = (tile / ttx) * 8, tx0 = (tile % ttx) * 8;
+  const int K = a.kh * a.kw, cpg = a.C / a.dg, C = a.C;
+  const long HW = (long)a.H * a.W;
+  const double scale = DET ? *det_scale : 1.0;
+  const float *xn = xh + (long)n * HW * C;
+  const int wy0 = ty0 - a.pad - R, wx0 = tx0 - a.pad - R;  // window origin (stride 1)
+  const int nwin = WR * WCc * cpg;
+  auto pix = [&](int pl) -> long {  // linear output pixel of tile pixel pl, or -1
+    const int y = ty0 + (pl >> 3), x = tx0 + (pl & 7);
+    return (y < a.Ho && x < a.Wo) ? (long)y * a.Wo + x : -1;
+  };
+  for (int e = tid; e < nwin; e += NT) {
+    if (DET)
+      reinterpret_cast<long long *>(sAcc)[e] = 0;
+    else
+      reinterpret_cast<float *>(sAcc)[e] = 0.f;
+  }
+  for (int e = tid; e < Co * PT; e += NT) {
+    const int co = e / PT, pl = e % PT;
+    const long pp = pix(pl);
+    sG[co * GP + pl] = pp >= 0 ? gout[((long)n * Co + co) * P + pp] : 0.f;
+  }
+  const int kr = lane >> 4, jj = lane & 15;
+  const int q = tid & 7;  // channel quad of the gradient role; pixels (tid >> 3) + 32 it
+  for (int k = 0; k < K; ++k) {
+    if (k) __syncthreads();  // every wave is done scattering tap k-1 (it reads sS)
+    if (wave == 0) {  // published for the chunk loop (its first barrier orders it)
+#pragma clang fp contract(off)
+      const long p = pix(lane);
+      const bool pvalid = p >= 0;
+      Samp s;
+      pixel_samp(s, a, n, g, k, pvalid ? p : 0, pvalid ? (int)(p / a.Wo) : 0, pvalid ? (int)(p % a.Wo) : 0);
+      const bool on = pvalid && s.valid;
+      const float hh = 1.f - s.lh, hw = 1.f - s.lw;
+      float *qq = sS + lane * 16;
+      qq[0] = __builtin_bit_cast(float, on && (s.ok & 1) ? s.i1 : -1);
+      qq[1] = __builtin_bit_cast(float, on && (s.ok & 2) ? s.i2 : -1);
+      qq[2] = __builtin_bit_cast(float, on && (s.ok & 4) ? s.i3 : -1);
+      qq[3] = __builtin_bit_cast(float, on && (s.ok & 8) ? s.i4 : -1);
+      qq[4] = hh * hw, qq[5] = hh * s.lw, qq[6] = s.lh * hw, qq[7] = s.lh * s.lw;
+      qq[8] = s.m, qq[9] = s.lh, qq[10] = s.lw, qq[11] = on ? 1.f : 0.f;
+      // window position of the 2x2 corner block (top-left), or -1: global atomics
+      int wpos = -1;
+      if (on) {
+        const int rh = s.hl - wy0, rw = s.wl - wx0;
+        if ((unsigned)rh <= (unsigned)(WR - 2) && (unsigned)rw <= (unsigned)(WCc - 2)) wpos = rh * WCc + rw;
+      }
+      qq[12] = __builtin_bit_cast(float, wpos);
+    }
+    float gm[2] = {0.f, 0.f}, goh[2] = {0.f, 0.f}, gow[2] = {0.f, 0.f};
+    for (int c0 = g * cpg; c0 < (g + 1) * cpg; c0 += KC) {
+      const int rows = min(KC, (g + 1) * cpg - c0);
+      __syncthreads();  // previous chunk's sCg / sWt readers are done
+      for (int e = tid; e < KC * Co; e += NT) {
+        const int co = e % Co, cl = e / Co;
+        sWt[cl * WTP + co] = cl < rows ? wT[((long)k * C + c0 + cl) * Co + co] : 0.f;
+      }
+      __syncthreads();
+      f32x4 cacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      for (int ks = 0; ks < Co / 4; ++ks) {
+        const float bv = sG[(4 * ks + kr) * GP + 16 * wave + jj];
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const float av = sWt[(16 * cb + jj) * WTP + 4 * ks + kr];
+          cacc[cb] = mfma16x16x4(av, bv, cacc[cb]);
+        }
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sCg[(16 * cb + 4 * kr + r) * CP + 16 * wave + jj] = cacc[cb][r];
+      __syncthreads();
+      // offset / mask partials: (pixel, channel quad)
+      if (4 * q < rows) {
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+#pragma clang fp contract(off)
+          const int px = (tid >> 3) + 32 * it;
+          const float *qq = sS + px * 16;
+          const f32x4 qi = *reinterpret_cast<const f32x4 *>(qq);
+          const float qi0 = qi[0], qi1 = qi[1], qi2 = qi[2], qi3 = qi[3];
+          const int i1 = __builtin_bit_cast(int, qi0), i2 = __builtin_bit_cast(int, qi1);
+          const int i3 = __builtin_bit_cast(int, qi2), i4 = __builtin_bit_cast(int, qi3);
+          const float m = qq[8], lh = qq[9], lw = qq[10];
+          const float hh = 1.f - lh, hw = 1.f - lw;
+          const int cq = c0 + 4 * q;
+          const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+          const f32x4 v1 = i1 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i1 * C + cq) : z;
+          const f32x4 v2 = i2 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i2 * C + cq) : z;
+          const f32x4 v3 = i3 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i3 * C + cq) : z;
+          const f32x4 v4 = i4 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i4 * C + cq) : z;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float cg = sCg[(4 * q + u) * CP + px];
+            const float val = hh * hw * v1[u] + hh * lw * v2[u] + lh * hw * v3[u] + lh * lw * v4[u];
+            gm[it] += cg * val;
+            const float wh = -hw * v1[u] - lw * v2[u] + hw * v3[u] + lw * v4[u];
+            const float ww = -hh * v1[u] + hh * v2[u] - lh * v3[u] + lh * v4[u];
+            const float top = cg * m;
+            goh[it] += wh * top;
+            gow[it] += ww * top;
+          }
+        }
+      }
+      // grad_x: lanes 0-31 channel cl of pixel 16w + 2t, lanes 32-63 of pixel 16w + 2t + 1; the
+      // window channel index is c0 + cl - g*cpg (< cpg <= 32: one chunk per group)
+      const int cl = lane & 31;
+      if (cl < rows) {
+        const long cbase = (long)n * HW * C + c0 + cl;
+        const int wc = c0 + cl - g * cpg;
+        auto gadd = [&](int i, float v) {
+          if (DET)
+            atomicAdd(reinterpret_cast<unsigned long long *>(gxi + cbase + (long)i * C),
+                      (unsigned long long)__double2ll_rn((double)v * scale));
+          else
+            atomicAdd(gx + cbase + (long)i * C, v);
+        };
+        auto wadd = [&](int wp, float v) {
+          if (DET)
+            atomicAdd(reinterpret_cast<unsigned long long *>(sAcc) + (long)wp * cpg + wc,
+                      (unsigned long long)__double2ll_rn((double)v * scale));
+          else
+            atomicAdd(reinterpret_cast<float *>(sAcc) + wp * cpg + wc, v);
+        };
+#pragma unroll 2
+        for (int t = 0; t < 8; ++t) {
+#pragma clang fp contract(off)
+          const int px = 16 * wave + 2 * t + (lane >> 5);
+          const float *qq = sS + px * 16;
+          const f32x4 qi = *reinterpret_cast<const f32x4 *>(qq);
+          const f32x4 qw = *reinterpret_cast<const f32x4 *>(qq + 4);
+          const float top = sCg[cl * CP + px] * qq[8];
+          const float qi0 = qi[0], qi1 = qi[1], qi2 = qi[2], qi3 = qi[3], q12 = qq[12];
+          const int i1 = __builtin_bit_cast(int, qi0), i2 = __builtin_bit_cast(int, qi1);
+          const int i3 = __builtin_bit_cast(int, qi2), i4 = __builtin_bit_cast(int, qi3);
+          const int wp = __builtin_bit_cast(int, q12);
+          if (wp >= 0) {  // corners outside the image have index -1 (skipped), as below
+            if (i1 >= 0) wadd(wp, qw[0] * top);
+            if (i2 >= 0) wadd(wp + 1, qw[1] * top);
+            if (i3 >= 0) wadd(wp + WCc, qw[2] * top);
+            if (i4 >= 0) wadd(wp + WCc + 1, qw[3] * top);
+          } else {
+            if (i1 >= 0) gadd(i1, qw[0] * top);
+            if (i2 >= 0) gadd(i2, qw[1] * top);
+            if (i3 >= 0) gadd(i3, qw[2] * top);
+            if (i4 >= 0) gadd(i4, qw[3] * top);
+          }
+        }
+      }
+    }
+    // reduce the 8 channel quads of each pixel (lanes 8j .. 8j+7), fixed order
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+#pragma unroll
+      for (int msk = 1; msk < 8; msk <<= 1) {
+        gm[it] += __shfl_xor(gm[it], msk);
+        goh[it] += __shfl_xor(goh[it], msk);
+        gow[it] += __shfl_xor(gow[it], msk);
+      }
+      const long p = pix((tid >> 3) + 32 * it);
+      if (q == 0 && p >= 0) {
+        const long ob = (long)n * a.dg * 2 * K * P + (long)g * 2 * K * P;
+        goff[ob + (long)(2 * k) * P + p] = goh[it];
+        goff[ob + (long)(2 * k + 1) * P + p] = gow[it];
+        gmask[(long)n * a.dg * K * P + ((long)g * K + k) * P + p] = gm[it];
+      }
+    }
+  }
+  __syncthreads();  // the window is complete
+  // add the window to the global accumulator: consecutive threads take consecutive channels of a
+  // position (one 128-byte line per 32 lanes); untouched (zero) elements are skipped
+  for (int e = tid; e < nwin; e += NT) {
+    const int pos = e / cpg, wc = e - pos * cpg;
+    const int gy = wy0 + pos / WCc, gxp = wx0 + pos % WCc;
+    if (gy < 0 || gy >= a.H || gxp < 0 || gxp >= a.W) continue;
+    const long o = ((long)n * HW + (long)gy * a.W + gxp) * C + g * cpg + wc;
+    if (DET) {
+      const long long v = reinterpret_cast<long long *>(sAcc)[e];
+      if (v) atomicAdd(reinterpret_cast<unsigned long long *>(gxi + o), (unsigned long long)v);
+    } else {
+      const float v = reinterpret_cast<float *>(sAcc)[e];
+      if (v != 0.f) atomicAdd(gx + o, v);
+    }
+  }
+}
+
 // x [N][C][HW] -> [N][HW][C] and w [Co][C][K] -> wT [K][C][Co] (inputs of mdcn_bwd_data_nhwc_kernel)
 __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float *__restrict__ src,
                                                            float *__restrict__ dst, int C, long HW) {
@@ -2439,7 +2658,35 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
     hipLaunchKernelGGL(weight_kcco_kernel, dim3(host_div_up(nw, 256) > 1024 ? 1024 : host_div_up(nw, 256)),
                        dim3(256), 0, st, weight, wt, co, c, K);
     const size_t smem2 = sizeof(float) * ((size_t)co * GP + (size_t)KC * WTP + (size_t)KC * CP + (size_t)PT * 12);
-    if (det)
+    // window form (stride 1, <= 32 channels per deformable group): grad_x summed per 8x8 tile in
+    // LDS.  Deterministic form only by default: there it is 11-22 % faster (int64 LDS atomics
+    // replace int64 global ones); with float atomics the global-atomic kernel is faster (agg_s0
+    // 5.1 vs 7.9 ms: the 75 KB of LDS halve the waves that hide the per-tap gather latency).
+    // AANET_DCN_BWD_WINDOW: 0 never, 1 deterministic only, 2 both.
+    const char *bwd_env = getenv("AANET_DCN_BWD_WINDOW");  // read per call (tests switch it)
+    const int bwd_win = bwd_env ? atoi(bwd_env) : 1;
+    const int cpg = c / dg, R = 2;
+    const int WR = 8 + (kh - 1) * dil + 2 * R, WCw = 8 + (kw - 1) * dil + 2 * R;
+    const size_t smem3 = sizeof(float) * ((size_t)co * GP + (size_t)KC * WTP + (size_t)KC * CP + (size_t)PT * 16) +
+                         (size_t)WR * WCw * cpg * (det ? 8 : 4);
+    if ((bwd_win == 2 || (bwd_win == 1 && det)) && stride == 1 && cpg <= KC && smem3 <= 160 * 1024) {
+      static const bool win_attr = [] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_win_kernel<0>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_win_kernel<1>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        return true;
+      }();
+      (void)win_attr;
+      const dim3 gwin((unsigned)(n * host_div_up(a.Wo, 8) * host_div_up(a.Ho, 8)), (unsigned)dg);
+      if (det)
+        hipLaunchKernelGGL(mdcn_bwd_data_win_kernel<1>, gwin, dim3(NT), smem3, st, a, xh, wt, grad_out,
+                           grad_x, grad_offset, grad_mask, GP, WTP, gxi, scale, WR, WCw, R);
+      else
+        hipLaunchKernelGGL(mdcn_bwd_data_win_kernel<0>, gwin, dim3(NT), smem3, st, a, xh, wt, grad_out,
+                           reinterpret_cast<float *>(wb + L.gxi), grad_offset, grad_mask, GP, WTP,
+                           nullptr, nullptr, WR, WCw, R);
+    } else if (det)
       hipLaunchKernelGGL(mdcn_bwd_data_nhwc_kernel<1>, gdata, dim3(NT), smem2, st, a, xh, wt, grad_out,
                          grad_x, grad_offset, grad_mask, GP, WTP, gxi, scale);
     else

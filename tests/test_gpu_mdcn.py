@@ -286,3 +286,25 @@ def test_deterministic_mode_reaches_shim_and_torch_ops():
             assert torch.equal(a_, b_)
     finally:
         torch.use_deterministic_algorithms(prev)
+
+
+@pytest.mark.parametrize("case", BWD_CASES)
+@pytest.mark.parametrize("window", ["2", "0"])
+def test_mdcn_backward_window_form_vs_oracle(case, window, monkeypatch):
+    """The LDS-window grad_x form (mdcn_bwd_data_win_kernel, stride 1, <= 32 channels per
+    deformable group) with float atomics (AANET_DCN_BWD_WINDOW=2; by default it runs only for the
+    deterministic form) and the global-atomic form it replaces (=0), against the oracle, with
+    offsets large enough that some corners fall outside the window."""
+    monkeypatch.setenv("AANET_DCN_BWD_WINDOW", window)
+    N, C, H, W, Co, k, s, p, d, dg = case
+    x, off, msk, w, b = make_case(9, N, C, H, W, Co, k, s, p, d, dg, off_scale=2.5)
+    Ho, Wo = off.shape[2:]
+    go = np.random.default_rng(10).standard_normal((N, Co, Ho, Wo)).astype(np.float32)
+    for det in (False, True):
+        got = ops.mdcn_backward(g2t(x), g2t(off), g2t(msk), g2t(w), g2t(go), True, s, p, d, 1, dg,
+                                deterministic=det)
+        ref = oracle.mdcn_backward(x, off, msk, w, go, True, s, p, d, 1, dg)
+        for name, gt, r in zip(("grad_input", "grad_offset", "grad_mask", "grad_weight", "grad_bias"), got, ref):
+            err = np.abs(t2n(gt) - r)
+            scale = np.abs(r).max() + 1e-12
+            assert err.max() <= 1e-4 * scale + 1e-6, f"{name} det={det}: max err {err.max():.3g}"
