@@ -35,6 +35,8 @@ _SIGNATURES = {
     "aanet_mdcn_bwd_f32": [_P] * 10 + [_I] * 12 + [_P],
     "aanet_mdcn_bwd_det_f32": [_P] * 10 + [_I] * 12 + [_P, ctypes.c_size_t, _P],
     "aanet_mdcn_bwd_ws_f32": [_P] * 10 + [_I] * 12 + [_P, ctypes.c_size_t, _P],
+    "aanet_conv2d_wgrad_f32": [_P] * 4 + [_I] * 12 + [_P, ctypes.c_size_t, _P],
+    "aanet_resize_bilinear_bwd_f32": [_P, _P, _L] + [_I] * 4 + [_P],
     "aanet_conv2d_fused_f32": [_P] * 6 + [_I, _I, _P] + [_I] * 12 + [_P],
     "aanet_conv_weight_pack_f32": [_P, _P, _I, _I, _I, _I, _P],
     "aanet_conv_weight_pack_split_f32": [_P, _P, _I, _I, _I, _I, _I, _P],
@@ -72,6 +74,8 @@ def lib():
         L.aanet_mdcn_bwd_det_workspace_size.restype = ctypes.c_size_t
         L.aanet_mdcn_bwd_ws_workspace_size.argtypes = [_I] * 12
         L.aanet_mdcn_bwd_ws_workspace_size.restype = ctypes.c_size_t
+        L.aanet_conv2d_wgrad_workspace_size.argtypes = [_I] * 11
+        L.aanet_conv2d_wgrad_workspace_size.restype = ctypes.c_size_t
         L.aanet_version.restype = _I
         L.aanet_conv_weight_pack_split_bytes.argtypes = [_I] * 5
         L.aanet_conv_weight_pack_split_bytes.restype = _L
@@ -81,7 +85,7 @@ def lib():
 
 def exported_symbols():
     return (["aanet_version", "aanet_status_string", "aanet_mdcn_bwd_det_workspace_size",
-             "aanet_mdcn_bwd_ws_workspace_size",
+             "aanet_mdcn_bwd_ws_workspace_size", "aanet_conv2d_wgrad_workspace_size",
              "aanet_conv_weight_pack_split_bytes"] + list(_SIGNATURES))
 
 

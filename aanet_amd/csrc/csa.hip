@@ -130,7 +130,64 @@ __global__ __launch_bounds__(256) void csa_sum_scalar_kernel(CsaArgs a) {
   }
 }
 
+// Weight of input index i in output index o along one axis (the align_corners=False rule of
+// bilinear_resize): lambda0 if i is o's lower tap, lambda1 if its upper one (both at the edge).
+__device__ __forceinline__ float bilinear_axis_weight(int o, int i, float s, int in) {
+  float r = s * ((float)o + 0.5f) - 0.5f;
+  r = r < 0.f ? 0.f : r;
+  const int i1 = (int)r, i1p = i1 < in - 1 ? 1 : 0;
+  const float l1 = r - (float)i1, l0 = 1.f - l1;
+  return (i1 == i ? l0 : 0.f) + (i1 + i1p == i ? l1 : 0.f);
+}
+
+// Backward of the resize as a gather: each input element sums, in a fixed order, the output
+// gradients of the outputs whose 2x2 stencil covers it (source coordinate in (i-1, i+1)).
+// torch's CUDA backward scatters with atomics (and under deterministic algorithms falls back to a
+// sort-based index_put); this form is bit-reproducible and atomic-free.
+__global__ __launch_bounds__(256) void resize_bilinear_bwd_kernel(const float *__restrict__ go,
+                                                                  float *__restrict__ gi,
+                                                                  long planes, int ih, int iw,
+                                                                  int oh, int ow, float sh,
+                                                                  float sw) {
+  const long total = planes * ih * iw;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int x = (int)(e % iw);
+    const long t = e / iw;
+    const int y = (int)(t % ih);
+    const long plane = t / ih;
+    const int ylo = max(0, (int)floorf(((float)y - 0.5f) / sh - 0.5f) - 1);
+    const int yhi = min(oh - 1, (int)ceilf(((float)y + 1.5f) / sh - 0.5f) + 1);
+    const int xlo = max(0, (int)floorf(((float)x - 0.5f) / sw - 0.5f) - 1);
+    const int xhi = min(ow - 1, (int)ceilf(((float)x + 1.5f) / sw - 0.5f) + 1);
+    const float *gp = go + plane * oh * ow;
+    float acc = 0.f;
+    for (int oy = ylo; oy <= yhi; ++oy) {
+      const float wy = bilinear_axis_weight(oy, y, sh, ih);
+      if (wy == 0.f) continue;
+      float rs = 0.f;
+      for (int ox = xlo; ox <= xhi; ++ox)
+        rs += bilinear_axis_weight(ox, x, sw, iw) * gp[(long)oy * ow + ox];
+      acc += wy * rs;
+    }
+    gi[e] = acc;
+  }
+}
+
 }  // namespace
+
+extern "C" int aanet_resize_bilinear_bwd_f32(const float *grad_out, float *grad_in, long planes,
+                                             int in_h, int in_w, int out_h, int out_w,
+                                             aanet_stream_t stream) {
+  AANET_HOST_CHECK(grad_out && grad_in && planes > 0 && in_h > 0 && in_w > 0 && out_h > 0 &&
+                   out_w > 0);
+  const long total = planes * in_h * in_w;
+  long g = (total + 255) / 256;
+  if (g > 65536) g = 65536;
+  hipLaunchKernelGGL(resize_bilinear_bwd_kernel, dim3((unsigned)g), dim3(256), 0, as_hip(stream),
+                     grad_out, grad_in, planes, in_h, in_w, out_h, out_w,
+                     (float)in_h / (float)out_h, (float)in_w / (float)out_w);
+  return aanet_launch_status();
+}
 
 extern "C" int aanet_csa_sum_f32(float *out, int n, int c, int h, int w, int num_inputs,
                                  const float *const *inputs, const int *in_h, const int *in_w,

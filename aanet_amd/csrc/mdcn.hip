@@ -1821,7 +1821,10 @@ __global__ __launch_bounds__(256) void weight_kcco_kernel(const float *__restric
 // det_weight_reduce_kernel adds them to grad_weight in split order.
 // NR: the col chunk is sampled from the channels-last copy xh [N][H*W][C] (C, C/dg % 4 == 0):
 // thread = (pixel, channel quad), one 16-byte load per corner (8 lanes = one 128-B line).
-template <int DET, int NR = 0>
+// PLAIN: the weight gradient of an ordinary (grouped) convolution (aanet_conv2d_wgrad_f32): the
+// col chunk is the tap's shifted window of x (zero outside), a.dg carries the conv's groups,
+// grad_weight is [Co][C/groups][K] and output-channel tiles stay inside the chunk's group.
+template <int DET, int NR = 0, int PLAIN = 0>
 __global__ __launch_bounds__(NT) void mdcn_bwd_weight_kernel(MdcnArgs a, const float *__restrict__ gout,
                                                              float *__restrict__ gw, int npieces,
                                                              long range, float *__restrict__ part,
@@ -1836,13 +1839,67 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_weight_kernel(MdcnArgs a, const f
   const int k = chunk / (a.dg * npieces), rem = chunk % (a.dg * npieces);
   const int g = rem / npieces, piece = rem % npieces;
   const int c0 = g * cpg + piece * KC, rows = min(KC, (g + 1) * cpg - c0);
-  const int co0 = blockIdx.z * 64;
+  const int cog = PLAIN ? Co / a.dg : Co;  // output channels of the chunk's group
+  const int co0 = (PLAIN ? g * cog : 0) + blockIdx.z * 64, coE = PLAIN ? (g + 1) * cog : Co;
+  const int Cw = PLAIN ? cpg : C, cw0 = PLAIN ? c0 - g * cpg : c0;  // grad_weight's [co][c] view
   const long r0 = (long)blockIdx.y * range, r1 = min(r0 + range, T);
   const long HW = (long)a.H * a.W;
   const int kr = lane >> 4, jj = lane & 15;
   // wave w: output-channel block w (16 co), both 16-channel blocks of the chunk
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-  for (long t0 = r0; t0 < r1; t0 += PT) {
+  if constexpr (PLAIN) {
+    // software-pipelined: the next sub-tile's column values and grad_out tile are loaded into
+    // registers while the MFMAs of the current one run from LDS
+    float rc[KC / 4], rg[64 * PT / NT];
+    const int ki = (k / a.kw) * a.dil - a.pad, kj = (k % a.kw) * a.dil - a.pad;
+    auto load = [&](long t0) {
+      const long t = t0 + lane;
+      const int n = t < r1 ? (int)(t / P) : 0;
+      const long p = t < r1 ? t % P : 0;
+      const int hi = (int)(p / a.Wo) * a.stride + ki, wi = (int)(p % a.Wo) * a.stride + kj;
+      const bool ok = t < r1 && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+      const float *xn = a.x + (long)n * C * HW + (long)hi * a.W + wi;
+#pragma unroll
+      for (int ii = 0; ii < KC / 4; ++ii) {
+        const int cl = wave + 4 * ii;
+        rc[ii] = (cl < rows && ok) ? xn[(long)(c0 + cl) * HW] : 0.f;
+      }
+      const float *gp = gout + (long)n * Co * P + p;  // thread = pixel lane, rows wave + 4i
+#pragma unroll
+      for (int i = 0; i < 64 * PT / NT; ++i) {
+        const int co = co0 + wave + 4 * i;
+        rg[i] = (t < r1 && co < coE) ? gp[(long)co * P] : 0.f;
+      }
+    };
+    auto store = [&]() {
+#pragma unroll
+      for (int ii = 0; ii < KC / 4; ++ii) sC[(wave + 4 * ii) * GP2 + lane] = rc[ii];
+#pragma unroll
+      for (int i = 0; i < 64 * PT / NT; ++i) sG[(wave + 4 * i) * GP2 + lane] = rg[i];
+    };
+    load(r0);
+    store();
+    __syncthreads();
+    for (long t0 = r0; t0 < r1; t0 += PT) {
+      const bool more = t0 + PT < r1;
+      if (more) load(t0 + PT);
+#pragma unroll 4
+      for (int ks = 0; ks < PT / 4; ++ks) {
+        const float av = sG[(16 * wave + jj) * GP2 + 4 * ks + kr];
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const float bv = sC[(16 * cb + jj) * GP2 + 4 * ks + kr];
+          acc[cb] = mfma16x16x4(av, bv, acc[cb]);
+        }
+      }
+      __syncthreads();
+      if (more) {
+        store();
+        __syncthreads();
+      }
+    }
+  }
+  for (long t0 = r0; t0 < r1 && !PLAIN; t0 += PT) {
     if constexpr (NR) {
       const int q = tid & 7;
 #pragma unroll
@@ -1890,7 +1947,7 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_weight_kernel(MdcnArgs a, const f
       const long tt = t0 + pl;
       const int co = co0 + col;
       float v = 0.f;
-      if (tt < r1 && co < Co) v = gout[((long)(tt / P) * Co + co) * P + tt % P];
+      if (tt < r1 && co < coE) v = gout[((long)(tt / P) * Co + co) * P + tt % P];
       sG[col * GP2 + pl] = v;
     }
     __syncthreads();
@@ -1911,27 +1968,39 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_weight_kernel(MdcnArgs a, const f
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int co = co0 + 16 * wave + 4 * kr + r, cl = 16 * cb + jj;
-      if (co < Co && cl < rows) {
-        const long e = ((long)co * C + c0 + cl) * K + k;
+      if (co < coE && cl < rows) {
+        const long e = ((long)co * Cw + cw0 + cl) * K + k;
         if (DET)
-          part[(long)blockIdx.y * Co * C * K + e] = acc[cb][r];
+          part[(long)blockIdx.y * Co * Cw * K + e] = acc[cb][r];
         else
           atomicAdd(gw + e, acc[cb][r]);
       }
     }
 }
 
-__global__ __launch_bounds__(256) void bias_grad_kernel(const float *__restrict__ gout,
-                                                        float *__restrict__ gb, int N, int Co,
-                                                        long P) {
+// gb[co] += sum over n, p of gout[n][co][p]: one 1024-thread workgroup per channel, 16-byte
+// loads when P % 4 == 0, fixed-order tree reduction (bit-reproducible).
+__global__ __launch_bounds__(1024) void bias_grad_kernel(const float *__restrict__ gout,
+                                                         float *__restrict__ gb, int N, int Co,
+                                                         long P) {
   const int co = blockIdx.x;
   float s = 0.f;
-  for (int n = 0; n < N; ++n)
-    for (long p = threadIdx.x; p < P; p += 256) s += gout[((long)n * Co + co) * P + p];
-  __shared__ float red[256];
+  if ((P & 3) == 0 && (reinterpret_cast<uintptr_t>(gout) & 15) == 0) {
+    for (int n = 0; n < N; ++n) {
+      const f32x4 *g4 = reinterpret_cast<const f32x4 *>(gout + ((long)n * Co + co) * P);
+      for (long q = threadIdx.x; q < (P >> 2); q += 1024) {
+        const f32x4 v = g4[q];
+        s += (v[0] + v[1]) + (v[2] + v[3]);
+      }
+    }
+  } else {
+    for (int n = 0; n < N; ++n)
+      for (long p = threadIdx.x; p < P; p += 1024) s += gout[((long)n * Co + co) * P + p];
+  }
+  __shared__ float red[1024];
   red[threadIdx.x] = s;
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
+  for (int w = 512; w > 0; w >>= 1) {
     if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
@@ -2206,13 +2275,29 @@ __global__ __launch_bounds__(256) void det_wbound_kernel(const float *__restrict
   }
 }
 
+// max |v| into *slot (as the uint bits of a non-negative float): 16-byte loads when v is
+// 16-byte aligned, one atomic per workgroup (a few hundred workgroups: per-wave atomics on one
+// address serialise at the L2 and dominated this kernel).
 __global__ __launch_bounds__(256) void det_absmax_kernel(const float *__restrict__ v, long n,
                                                          unsigned *__restrict__ slot) {
+  __shared__ float red[4];
   float m = 0.f;
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256)
-    m = fmaxf(m, fabsf(v[e]));
+  const long stride = (long)gridDim.x * 256, t0 = (long)blockIdx.x * 256 + threadIdx.x;
+  long tail = 0;
+  if ((reinterpret_cast<uintptr_t>(v) & 15) == 0) {
+    const long n4 = n >> 2;
+    for (long q = t0; q < n4; q += stride) {
+      const f32x4 x = reinterpret_cast<const f32x4 *>(v)[q];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+    }
+    tail = n4 << 2;
+  }
+  for (long e = tail + t0; e < n; e += stride) m = fmaxf(m, fabsf(v[e]));
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0) atomicMax(slot, __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(slot, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
 // scale = 2^(38 - ceil(log2 bound)): a single contribution stays below 2^38, so up to 2^25 of
@@ -2224,14 +2309,31 @@ __global__ void det_scale_kernel(const unsigned *__restrict__ bounds, double *__
   *scale = (b > 0.0 && isfinite(b)) ? ldexp(1.0, 38 - (int)ceil(log2(b))) : 1.0;
 }
 
+// gw[e] += sum over the splits of part[split][e], in a fixed order: workgroup = 64 consecutive
+// elements x 4 split lanes (lane l sums splits l, l+4, ... in order, 4 loads in flight), then the
+// 4 lane sums are added in lane order -- bit-reproducible for a given nsplit.
 __global__ __launch_bounds__(256) void det_weight_reduce_kernel(const float *__restrict__ part,
                                                                 float *__restrict__ gw, long n,
                                                                 int nsplit) {
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
-    float s = 0.f;
-    for (int y = 0; y < nsplit; ++y) s += part[(long)y * n + e];
-    gw[e] += s;
+  __shared__ float red[4][64];
+  const int ex = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const long e = (long)blockIdx.x * 64 + ex;
+  float s = 0.f;
+  if (e < n) {
+    int y = sl;
+    for (; y + 12 < nsplit; y += 16) {
+      const float v0 = part[(long)y * n + e], v1 = part[(long)(y + 4) * n + e];
+      const float v2 = part[(long)(y + 8) * n + e], v3 = part[(long)(y + 12) * n + e];
+      s += v0;
+      s += v1;
+      s += v2;
+      s += v3;
+    }
+    for (; y < nsplit; y += 4) s += part[(long)y * n + e];
   }
+  red[sl][ex] = s;
+  __syncthreads();
+  if (sl == 0 && e < n) gw[e] += ((red[0][ex] + red[1][ex]) + red[2][ex]) + red[3][ex];
 }
 
 __global__ void pack_weight_kernel(const float *__restrict__ w, float *__restrict__ wp, int Co,
@@ -2620,9 +2722,9 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
     hipLaunchKernelGGL(det_wbound_kernel, dim3(host_div_up((long)c * K, 256)), dim3(256), 0, st,
                        weight, co, c * K, bounds);
     const long ng = (long)n * co * P, nm = (long)n * dg * K * P;
-    hipLaunchKernelGGL(det_absmax_kernel, dim3(host_div_up(ng, 256) > 2048 ? 2048 : host_div_up(ng, 256)),
+    hipLaunchKernelGGL(det_absmax_kernel, dim3(host_div_up(ng, 1024) > 512 ? 512 : host_div_up(ng, 1024)),
                        dim3(256), 0, st, grad_out, ng, bounds + 1);
-    hipLaunchKernelGGL(det_absmax_kernel, dim3(host_div_up(nm, 256) > 2048 ? 2048 : host_div_up(nm, 256)),
+    hipLaunchKernelGGL(det_absmax_kernel, dim3(host_div_up(nm, 1024) > 512 ? 512 : host_div_up(nm, 1024)),
                        dim3(256), 0, st, mask, nm, bounds + 2);
     hipLaunchKernelGGL(det_scale_kernel, dim3(1), dim3(1), 0, st, bounds, scale);
   } else {
@@ -2732,19 +2834,79 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
   if (rc) return rc;
   if (det) {
     const long nw = (long)co * c * K;
-    hipLaunchKernelGGL(det_weight_reduce_kernel, dim3(host_div_up(nw, 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(det_weight_reduce_kernel, dim3(host_div_up(nw, 64)), dim3(256), 0, st,
                        part, grad_weight, nw, pl.nsplit);
     rc = aanet_launch_status();
     if (rc) return rc;
   }
   if (grad_bias) {
-    hipLaunchKernelGGL(bias_grad_kernel, dim3(co), dim3(256), 0, st, grad_out, grad_bias, n, co, P);
+    hipLaunchKernelGGL(bias_grad_kernel, dim3(co), dim3(1024), 0, st, grad_out, grad_bias, n, co, P);
+    rc = aanet_launch_status();
+  }
+  return rc;
+}
+
+// aanet_conv2d_wgrad_f32: the weight kernel in PLAIN form (a.dg = groups), then for det the
+// fixed-order reduction of the per-split partials; the bias gradient is a per-channel sum in a
+// fixed order either way.
+int conv_wgrad_impl(const float *x, const float *grad_out, float *grad_weight, float *grad_bias,
+                    int n, int c, int h, int w, int co, int kh, int kw, int stride, int pad,
+                    int dil, int groups, int det, void *ws, size_t ws_bytes, hipStream_t st) {
+  MdcnArgs a = make_args(x, nullptr, -1, nullptr, -1, 0, 1.f, nullptr, nullptr, nullptr, nullptr,
+                         0, nullptr, n, c, h, w, co, kh, kw, stride, pad, dil, groups, groups);
+  int rc = check_shapes(a);
+  if (rc) return rc;
+  if (!x || !grad_out || !grad_weight) return AANET_EINVAL;
+  const BwdPlan pl = bwd_plan(a);
+  const long nw = (long)co * (c / groups) * kh * kw;
+  float *part = nullptr;
+  if (det) {
+    if (!ws || ws_bytes < (size_t)pl.nsplit * nw * 4) return AANET_EINVAL;
+    part = static_cast<float *>(ws);
+  }
+  const dim3 gw3(pl.nchunks, (unsigned)pl.nsplit, host_div_up(co / groups, 64));
+  if (det)
+    hipLaunchKernelGGL((mdcn_bwd_weight_kernel<1, 0, 1>), gw3, dim3(NT), 0, st, a, grad_out,
+                       grad_weight, pl.npieces, pl.range, part, nullptr);
+  else
+    hipLaunchKernelGGL((mdcn_bwd_weight_kernel<0, 0, 1>), gw3, dim3(NT), 0, st, a, grad_out,
+                       grad_weight, pl.npieces, pl.range, nullptr, nullptr);
+  rc = aanet_launch_status();
+  if (rc) return rc;
+  if (det) {
+    hipLaunchKernelGGL(det_weight_reduce_kernel, dim3(host_div_up(nw, 64)), dim3(256), 0, st,
+                       part, grad_weight, nw, pl.nsplit);
+    rc = aanet_launch_status();
+    if (rc) return rc;
+  }
+  if (grad_bias) {
+    hipLaunchKernelGGL(bias_grad_kernel, dim3(co), dim3(1024), 0, st, grad_out, grad_bias, n, co,
+                       (long)a.Ho * a.Wo);
     rc = aanet_launch_status();
   }
   return rc;
 }
 
 }  // namespace
+
+extern "C" size_t aanet_conv2d_wgrad_workspace_size(int n, int c, int h, int w, int co, int kh,
+                                                    int kw, int stride, int pad, int dil,
+                                                    int groups) {
+  MdcnArgs a = make_args(nullptr, nullptr, -1, nullptr, -1, 0, 1.f, nullptr, nullptr, nullptr,
+                         nullptr, 0, nullptr, n, c, h, w, co, kh, kw, stride, pad, dil, groups,
+                         groups);
+  if (check_shapes(a)) return 0;
+  return (size_t)bwd_plan(a).nsplit * co * (c / groups) * kh * kw * 4;
+}
+
+extern "C" int aanet_conv2d_wgrad_f32(const float *x, const float *grad_out, float *grad_weight,
+                                      float *grad_bias, int n, int c, int h, int w, int co, int kh,
+                                      int kw, int stride, int pad, int dil, int groups,
+                                      int deterministic, void *workspace, size_t workspace_bytes,
+                                      aanet_stream_t stream) {
+  return conv_wgrad_impl(x, grad_out, grad_weight, grad_bias, n, c, h, w, co, kh, kw, stride, pad,
+                         dil, groups, deterministic, workspace, workspace_bytes, as_hip(stream));
+}
 
 extern "C" int aanet_mdcn_bwd_f32(const float *x, const float *offset, const float *mask,
                                   const float *weight, const float *grad_out, float *grad_x,

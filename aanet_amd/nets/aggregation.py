@@ -10,7 +10,6 @@ kernel; training mode runs the reference op sequence with autograd.
 The 3D-conv aggregators (StereoNet/PSMNet/GCNet) are out of scope.
 """
 import torch.nn as nn
-import torch.nn.functional as F
 
 from .. import ops
 from ._fuse import FoldCacheMixin, conv_bn_act, use_fused
@@ -162,8 +161,7 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
                 else:
                     exchange = self.fuse_layers[i][j](x[j])
                     if exchange.size()[2:] != x_fused[i].size()[2:]:
-                        exchange = F.interpolate(exchange, size=x_fused[i].size()[2:],
-                                                 mode='bilinear', align_corners=False)
+                        exchange = ops.resize_bilinear(exchange, x_fused[i].size()[2:])
                     x_fused[i] = x_fused[i] + exchange
 
         for i in range(len(x_fused)):

@@ -67,8 +67,8 @@ class DeformConv2d(FoldCacheMixin, nn.Module):
         training step); on the GPU each deformable group runs as its own ungrouped conv."""
         oc = self.offset_conv
         g = oc.groups
-        if g == 1 or not x.is_cuda or oc.dilation == (1, 1):
-            return oc(x)
+        if g == 1 or not x.is_cuda or oc.dilation == (1, 1) or getattr(oc, "_aanet_engine", False):
+            return oc(x)  # (train.use_engine_convs: the HIP engine takes grouped dilated convs)
         cin, cout = x.shape[1] // g, oc.out_channels // g
         return torch.cat([F.conv2d(x[:, i * cin:(i + 1) * cin], oc.weight[i * cout:(i + 1) * cout],
                                    oc.bias[i * cout:(i + 1) * cout], oc.stride, oc.padding,

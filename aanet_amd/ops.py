@@ -403,6 +403,38 @@ def csa_sum(inputs, act="leaky"):
     return out
 
 
+class ResizeBilinearFunction(Function):
+    """F.interpolate(x, size, mode='bilinear', align_corners=False) whose backward is the HIP
+    gather (aanet_resize_bilinear_bwd_f32): atomic-free and bit-reproducible, where torch's CUDA
+    backward scatters with atomics (or, under deterministic algorithms, sorts for index_put)."""
+
+    @staticmethod
+    def forward(ctx, x, size):
+        ctx.in_hw = tuple(x.shape[2:])
+        return torch.nn.functional.interpolate(x, size=size, mode="bilinear", align_corners=False)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_out):
+        grad_out = grad_out.contiguous()
+        require_gpu(grad_out, names=("grad_output",))
+        N, C, oh, ow = grad_out.shape
+        ih, iw = ctx.in_hw
+        gx = grad_out.new_empty((N, C, ih, iw))
+        call("aanet_resize_bilinear_bwd_f32", ptr(grad_out), ptr(gx), N * C, ih, iw, oh, ow,
+             stream_of(grad_out))
+        return gx, None
+
+
+def resize_bilinear(x, size):
+    """Bilinear resize (align_corners=False) of [N, C, h, w] to `size`; on the GPU its backward
+    is ResizeBilinearFunction's HIP gather."""
+    size = tuple(int(v) for v in size)
+    if not x.is_cuda:
+        return torch.nn.functional.interpolate(x, size=size, mode="bilinear", align_corners=False)
+    return ResizeBilinearFunction.apply(x, size)
+
+
 def mdcn_backward(x, offset, mask, weight, grad_out, with_bias, stride, padding, dilation, groups,
                   deformable_groups, deterministic=None, nchw_scatter=False):
     """deform_conv_cuda.cpp:571-685 -> (gX, gOffset, gMask, gW, gB or None).
@@ -447,6 +479,61 @@ def mdcn_backward(x, offset, mask, weight, grad_out, with_bias, stride, padding,
          ptr(gx), ptr(goff), ptr(gm), ptr(gw), ptr(gb), N, C, H, W, Co, kh, kw, stride, padding,
          dilation, groups, deformable_groups, ptr(ws), nbytes, stream_of(x))
     return gx, goff, gm, gw, gb
+
+
+def conv2d_wgrad(x, grad_out, weight_shape, with_bias, stride=1, padding=0, dilation=1, groups=1,
+                 deterministic=None):
+    """(grad_weight, grad_bias or None) of an ordinary convolution (aanet_conv2d_wgrad_f32):
+    the DCN weight-gradient kernel with the tap's shifted window as its column.
+    deterministic (default: torch.are_deterministic_algorithms_enabled()): per-split partials
+    reduced in a fixed order instead of float atomics."""
+    require_gpu(x, grad_out, names=("input", "grad_output"))
+    N, C, H, W = x.shape
+    Co, _, kh, kw = weight_shape
+    if kh != kw:
+        raise ValueError("square kernels only")
+    gw = x.new_zeros(tuple(weight_shape))
+    gb = x.new_zeros((Co,)) if with_bias else None
+    if deterministic is None:
+        deterministic = torch.are_deterministic_algorithms_enabled()
+    ws, nbytes = None, 0
+    if deterministic:
+        nbytes = _lib.lib().aanet_conv2d_wgrad_workspace_size(N, C, H, W, Co, kh, kw, stride, padding,
+                                                               dilation, groups)
+        if nbytes == 0:
+            raise ValueError("aanet_conv2d_wgrad_workspace_size: invalid shape")
+        ws = torch.empty((nbytes,), device=x.device, dtype=torch.uint8)
+    call("aanet_conv2d_wgrad_f32", ptr(x), ptr(grad_out), ptr(gw), ptr(gb), N, C, H, W, Co, kh, kw,
+         stride, padding, dilation, groups, int(bool(deterministic)), ptr(ws), nbytes, stream_of(x))
+    return gw, gb
+
+
+def conv2d_dgrad(grad_out, weight, input_hw, stride=1, padding=0, dilation=1, groups=1):
+    """Data gradient of an ordinary convolution as a forward conv on the engine
+    (aanet_conv2d_fused_f32): the weight transposed per group and flipped, padding
+    dil*(k-1) - pad; stride s > 1 first spreads grad_out onto every s-th pixel of a zero plane
+    (plus the rows/columns the forward's floor division dropped)."""
+    require_gpu(grad_out, weight, names=("grad_output", "weight"))
+    Co, Cg, kh, kw = weight.shape
+    if kh != kw:
+        raise ValueError("square kernels only")
+    pad_t = dilation * (kh - 1) - padding
+    if pad_t < 0:
+        raise ValueError("padding > dilation*(k-1) has no engine data gradient")
+    N, _, Ho, Wo = grad_out.shape
+    H, W = input_hw
+    wt = (weight.view(groups, Co // groups, Cg, kh, kw).transpose(1, 2)
+          .reshape(groups * Cg, Co // groups, kh, kw).flip(-2, -1).contiguous())
+    if stride > 1:
+        rh = H + 2 * padding - dilation * (kh - 1) - 1 - (Ho - 1) * stride
+        rw = W + 2 * padding - dilation * (kw - 1) - 1 - (Wo - 1) * stride
+        dz = grad_out.new_zeros((N, Co, (Ho - 1) * stride + 1 + rh, (Wo - 1) * stride + 1 + rw))
+        dz[:, :, : (Ho - 1) * stride + 1 : stride, : (Wo - 1) * stride + 1 : stride] = grad_out
+        grad_out = dz
+    gx = conv2d_fused(grad_out.contiguous(), wt, padding=pad_t, dilation=dilation, groups=groups)
+    if tuple(gx.shape[2:]) != (H, W):
+        raise RuntimeError(f"dgrad shape {tuple(gx.shape)} != input {(H, W)}")
+    return gx
 
 
 def mdcn_im2col(x, offset, mask, kh, kw, stride, padding, dilation, deformable_groups):

@@ -29,6 +29,8 @@ import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import ops
+
 # model.py:98-107: pyramid weights by pyramid length
 PYRAMID_WEIGHTS = {5: [1 / 3, 2 / 3, 1.0, 1.0, 1.0],  # AANet and AANet+
                    4: [1 / 3, 2 / 3, 1.0, 1.0],
@@ -68,8 +70,8 @@ def disparity_loss(pred_pyramid, gt_disp, mask, weights=None, pseudo_gt=None, ps
     total, per_scale = 0.0, []
     for pred, w in zip(pred_pyramid, weights):
         if pred.size(-1) != gt_disp.size(-1):
-            pred = F.interpolate(pred.unsqueeze(1), size=gt_disp.shape[-2:], mode="bilinear",
-                                 align_corners=False) * (gt_disp.size(-1) / pred.size(-1))
+            pred = ops.resize_bilinear(pred.unsqueeze(1), gt_disp.shape[-2:]) * \
+                (gt_disp.size(-1) / pred.size(-1))
             pred = pred.squeeze(1)
         loss = (F.smooth_l1_loss(pred, gt_disp, reduction="none") * maskf).sum() / count
         total = total + w * loss
@@ -101,13 +103,81 @@ def wrap_data_parallel(model, device, sync_bn=True, bucket_cap_mb=32):
                                                gradient_as_bucket_view=True)
 
 
+class EngineConv2dFunction(torch.autograd.Function):
+    """An nn.Conv2d on the HIP engine end to end: forward aanet_conv2d_fused_f32, data gradient
+    as the engine's forward conv of grad_out (ops.conv2d_dgrad), weight/bias gradient
+    aanet_conv2d_wgrad_f32 -- deterministic (fixed-order partial sums) under
+    torch.use_deterministic_algorithms(True), where MIOpen would fall back to its naive
+    kernels."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, padding, dilation, groups):
+        from . import ops
+        x = x.contiguous()
+        ctx.save_for_backward(x, weight)
+        ctx.conf = (bias is not None, stride, padding, dilation, groups)
+        return ops.conv2d_fused(x, weight.contiguous(), bias, stride, padding, dilation, groups)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, grad_out):
+        from . import ops
+        x, weight = ctx.saved_tensors
+        with_bias, stride, padding, dilation, groups = ctx.conf
+        grad_out = grad_out.contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = ops.conv2d_dgrad(grad_out, weight.contiguous(), x.shape[2:], stride, padding,
+                                  dilation, groups)
+        if ctx.needs_input_grad[1] or (with_bias and ctx.needs_input_grad[2]):
+            gw, gb = ops.conv2d_wgrad(x, grad_out, weight.shape, with_bias, stride, padding,
+                                      dilation, groups)
+        return gx, gw, gb, None, None, None, None
+
+
+def _engine_conv_ok(m):
+    if type(m) is not nn.Conv2d:
+        return False
+    k, s, p, d = m.kernel_size, m.stride, m.padding, m.dilation
+    return (m.padding_mode == "zeros" and not isinstance(p, str)
+            and k[0] == k[1] and s[0] == s[1] and p[0] == p[1] and d[0] == d[1]
+            and p[0] <= d[0] * (k[0] - 1))
+
+
+def _engine_conv_forward(m, x):
+    if x.dtype != torch.float32 or not x.is_cuda:
+        raise RuntimeError("engine convs take fp32 CUDA tensors")
+    return EngineConv2dFunction.apply(x, m.weight, m.bias, m.stride[0], m.padding[0],
+                                      m.dilation[0], m.groups)
+
+
+def use_engine_convs(model):
+    """Route every nn.Conv2d of `model` that the engine takes (square kernel, symmetric
+    stride/padding/dilation, zero padding) through EngineConv2dFunction; returns how many.
+    The module type and parameters are unchanged (state_dict, DDP and the eval-mode folding of
+    nets/_fuse.py see the same module)."""
+    n = 0
+    for m in model.modules():
+        if _engine_conv_ok(m) and "forward" not in m.__dict__:
+            m.forward = _engine_conv_forward.__get__(m)
+            m._aanet_engine = True
+            n += 1
+    return n
+
+
 class Trainer:
     """One optimizer step per `accumulation_steps` micro-batches (model.py:64-153)."""
 
     def __init__(self, model, lr=1e-3, weight_decay=1e-4, accumulation_steps=1,
-                 highest_loss_only=False, max_disp=192):
+                 highest_loss_only=False, max_disp=192, engine_convs=None):
         """max_disp: the image-resolution disparity range of the valid mask (train.py --max_disp,
-        default 192), NOT the cost-volume D."""
+        default 192), NOT the cost-volume D.  engine_convs: run the plain convs on the HIP engine
+        (use_engine_convs); default: when torch.use_deterministic_algorithms(True) is on, where
+        MIOpen has only its naive deterministic kernels."""
+        if engine_convs is None:
+            engine_convs = torch.are_deterministic_algorithms_enabled()
+        if engine_convs:
+            use_engine_convs(model)
         self.model = model
         self.accumulation_steps = accumulation_steps
         self.highest_loss_only = highest_loss_only

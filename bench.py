@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--train", action="store_true",
                     help="time the training step (fwd+bwd+Adam, SyncBN+DDP for N>1) instead")
     ap.add_argument("--train-batch", type=int, default=4, help="training pairs per GPU")
+    ap.add_argument("--engine-convs", choices=("auto", "on", "off"), default="auto",
+                    help="--train: plain convs on the HIP engine (auto: with --deterministic)")
     ap.add_argument("--deterministic", action="store_true",
                     help="--train with torch.use_deterministic_algorithms (det DCN backward)")
     ap.add_argument("--model", default=None, choices=sorted(FULL_MODELS),
@@ -633,10 +635,14 @@ def train_main(args, device, rank, world):
     collective).  Secondary line: not the headline metric."""
     from aanet_amd import train as atrain
     if args.deterministic:
-        torch.use_deterministic_algorithms(True, warn_only=True)  # torch's upsample bwd: warn
+        torch.use_deterministic_algorithms(True, warn_only=True)
+        # the NaN fill of every torch.empty is a debugging aid, not part of determinism (the
+        # kernels overwrite their outputs; tests keep it on): ~2.5k fill launches per step
+        torch.utils.deterministic.fill_uninitialized_memory = False
     model = build_model(device, intermediate_supervision=True).train()
     model = atrain.wrap_data_parallel(model, device)
-    trainer = atrain.Trainer(model, lr=1e-3)
+    trainer = atrain.Trainer(model, lr=1e-3, engine_convs={"auto": None, "on": True,
+                                                           "off": False}[args.engine_convs])
     left, right = make_features(args.train_batch, rank, device, args.features, TRAIN_IMG)
     gen = torch.Generator(device=device).manual_seed(99 + rank)
     gt = torch.rand((args.train_batch,) + TRAIN_IMG, device=device, generator=gen) * (MAXD_IMG - 1)
@@ -672,7 +678,8 @@ def train_main(args, device, rank, world):
                        "batch_per_gpu": args.train_batch,
                        "global_batch": args.train_batch * world,
                        "parallelism": f"dp{world} (SyncBN + DDP all-reduce)" if world > 1
-                       else "dp1", "deterministic": bool(args.deterministic)},
+                       else "dp1", "deterministic": bool(args.deterministic),
+                       "engine_convs": args.engine_convs},
             "final_loss": float(loss)}), flush=True)
     if world > 1:
         dist.barrier()

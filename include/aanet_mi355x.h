@@ -218,6 +218,13 @@ int aanet_csa_sum_f32(float *out, int n, int c, int h, int w, int num_inputs,
                       const float *const *inputs, const int *in_h, const int *in_w, int act,
                       aanet_stream_t stream);
 
+/* Backward of F.interpolate(x, size=(out_h, out_w), mode='bilinear', align_corners=False)
+ * (aggregation.py:395-396 in training; the loss's upsampling, model.py:115-117):
+ * grad_in [planes, in_h, in_w] is OVERWRITTEN with the gather-form sum over grad_out
+ * [planes, out_h, out_w] -- fixed summation order, no atomics (bit-reproducible). */
+int aanet_resize_bilinear_bwd_f32(const float *grad_out, float *grad_in, long planes, int in_h,
+                                  int in_w, int out_h, int out_w, aanet_stream_t stream);
+
 /* deform_conv_cuda.cpp:571-685 (modulated_deform_conv_cuda_backward) + kernel.cu:635-767.
  * grad_x, grad_offset, grad_mask are OVERWRITTEN; grad_weight and grad_bias (may be NULL)
  * ACCUMULATE, as in the reference (cpp:660-671). */
@@ -254,6 +261,21 @@ int aanet_mdcn_bwd_det_f32(const float *x, const float *offset, const float *mas
                            float *grad_bias, int n, int c, int h, int w, int co, int kh, int kw,
                            int stride, int pad, int dil, int groups, int dg, void *workspace,
                            size_t workspace_bytes, aanet_stream_t stream);
+
+/* Weight (and bias) gradient of an ordinary convolution -- the wgrad of every nn.Conv2d of the
+ * ISA/CSA blocks in training (nets/deform.py:6-14, 70-72; nets/aggregation.py:354-370, 447),
+ * which the reference leaves to cuDNN.  x [n, c, h, w]; grad_out [n, co, ho, wo] (NCHW);
+ * grad_weight [co, c/groups, kh, kw] and grad_bias [co] (may be NULL) ACCUMULATE.
+ * deterministic != 0: per-split partial sums reduced in a fixed order (bit-reproducible), with
+ * `workspace` (device) of aanet_conv2d_wgrad_workspace_size(...) bytes; 0: float atomics, no
+ * workspace.  The data gradient is a forward conv on aanet_conv2d_fused_f32 (flipped,
+ * transposed weight; zero-inserted grad_out for stride 2) -- aanet_amd/train.py. */
+size_t aanet_conv2d_wgrad_workspace_size(int n, int c, int h, int w, int co, int kh, int kw,
+                                         int stride, int pad, int dil, int groups);
+int aanet_conv2d_wgrad_f32(const float *x, const float *grad_out, float *grad_weight,
+                           float *grad_bias, int n, int c, int h, int w, int co, int kh, int kw,
+                           int stride, int pad, int dil, int groups, int deterministic,
+                           void *workspace, size_t workspace_bytes, aanet_stream_t stream);
 
 /* Debug exports for bit-exact checks (SURVEY.md §8c pin 6):
  * im2col of ONE image, kernel.cu:570-633: col [c*kh*kw, ho*wo]. */
