@@ -9,11 +9,32 @@ implicit-GEMM kernel (BN folded) and each CSA output branch is one fused resize+
 kernel; training mode runs the reference op sequence with autograd.
 The 3D-conv aggregators (StereoNet/PSMNet/GCNet) are out of scope.
 """
+import contextlib
+import os
+
+import torch
 import torch.nn as nn
 
 from .. import ops
 from ._fuse import FoldCacheMixin, conv_bn_act, use_fused
 from .deform import DeformSimpleBottleneck, SimpleBottleneck
+
+
+_SIDE_STREAMS = {}
+
+
+def side_stream(device):
+    """The second HIP stream of the concurrent-scale schedule (one per device, created outside
+    any graph capture: the first eval forward is a warm-up)."""
+    s = _SIDE_STREAMS.get(device)
+    if s is None:
+        s = _SIDE_STREAMS[device] = torch.cuda.Stream(device=device)
+    return s
+
+
+def concurrent_scales():
+    """AANET_CONCURRENT_SCALES=0 runs the whole eval aggregation on one stream (A/B switch)."""
+    return os.environ.get("AANET_CONCURRENT_SCALES", "1") != "0"
 
 
 def csa_epilogue_ok(x0, up):
@@ -89,23 +110,44 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
         layer = self.fuse_layers[i][j]
         return conv_bn_act(x[j], layer[0], layer[1], None)
 
-    def _forward_eval(self, x):
+    def _forward_eval(self, x, side=None, keep=None):
         """Eval ISA + CSA.  The coarser scales run first, so that their exchange terms for output
         branch 0 exist when the scale-0 bottleneck runs: its tail kernel then writes both the
         block output and the cross-scale sum of branch 0 (aanet_csa_epilogue_t), which removes
         the scale-0 resize-sum kernel.  The in-place list mutation of aggregation.py:382 and the
-        term order of aggregation.py:388-400 are unchanged (the branches are independent)."""
+        term order of aggregation.py:388-400 are unchanged (the branches are independent).
+
+        side (a second HIP stream, AdaptiveAggregation): the coarse-scale work -- the scale 1..S-1
+        blocks, the exchange terms of branch 0, and after the scale-0 block the CSA of branches
+        1..S-1 -- is issued on `side`, concurrently with the scale-0 chain on the current stream
+        (conv1 -> offset conv -> tail kernel, which joins `side` just before it launches).  The
+        scale-0 kernels are latency-bound, so the coarse scales fill the CUs they leave idle.
+        Tensors read across the two streams are appended to `keep` (alive until the caller joins
+        the streams, so the caching allocator cannot hand their memory to the other stream)."""
         S = len(self.branches)
-        for i in range(1, S):
-            for j in range(self.num_blocks):
-                x[i] = self.branches[i][j](x[i])
-        up0 = [self._exchange_up(x, 0, j) for j in range(1, S)]
+        main = torch.cuda.current_stream(x[0].device) if side is not None else None
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            for i in range(1, S):
+                for j in range(self.num_blocks):
+                    x[i] = self.branches[i][j](x[i])
+            up0 = [self._exchange_up(x, 0, j) for j in range(1, S)]
+        terms = {(0, j): t for j, t in zip(range(1, S), up0)}
         for j in range(self.num_blocks - 1):
             x[0] = self.branches[0][j](x[0])
         last = self.branches[0][self.num_blocks - 1]
-        x[0], csa0 = last.forward_csa(x[0], up0 if csa_epilogue_ok(x[0], up0) else None)
-        return self._fuse_eval(x, {0: csa0} if csa0 is not None else {}, {(0, j): t for j, t in
-                                                                         zip(range(1, S), up0)})
+        join = (lambda: main.wait_stream(side)) if side is not None else None
+        x[0], csa0 = last.forward_csa(x[0], up0 if csa_epilogue_ok(x[0], up0) else None,
+                                      before_tail=join)
+        if side is None:
+            return self._fuse_eval(x, {0: csa0} if csa0 is not None else {}, terms)
+        keep.extend(up0)
+        keep.append(x[0])
+        if csa0 is None:  # no tail epilogue: the whole CSA on the current stream, after a join
+            main.wait_stream(side)
+            return self._fuse_eval(x, {}, terms)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            return self._fuse_eval(x, {0: csa0}, terms)
 
     def _fuse_eval(self, x, done=None, terms_cache=None):
         """Eval CSA: each exchange conv (+BN folded, +LeakyReLU inside strided chains) is one HIP
@@ -137,11 +179,14 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
             x_fused.append(ops.csa_sum([t.contiguous() for t in terms], act="leaky"))
         return x_fused
 
-    def forward(self, x):
-        """aggregation.py:375-402."""
+    def forward(self, x, side=None, keep=None):
+        """aggregation.py:375-402.  side / keep: the concurrent-scale schedule of
+        AdaptiveAggregation (eval only, see _forward_eval)."""
         assert len(self.branches) == len(x)
         if self.num_scales > 1 and use_fused(self, x[0]) and getattr(self, "aanet_fuse_csa", True):
-            return self._forward_eval(x)
+            return self._forward_eval(x, side, keep)
+        if side is not None:  # reference op sequence: one stream
+            torch.cuda.current_stream(x[0].device).wait_stream(side)
         for i in range(len(self.branches)):
             branch = self.branches[i]
             for j in range(self.num_blocks):
@@ -207,11 +252,20 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
     def forward(self, cost_volume):
         """aggregation.py:452-464 (final 1x1 conv with bias on the HIP conv engine in eval)."""
         assert isinstance(cost_volume, list)
+        fused = use_fused(self, cost_volume[0])
+        side = None
+        if fused and cost_volume[0].is_cuda and self.num_scales > 1 and concurrent_scales():
+            side = side_stream(cost_volume[0].device)
+            main = torch.cuda.current_stream(cost_volume[0].device)
+            side.wait_stream(main)  # the cost volumes are written on the current stream
+            keep = list(cost_volume)
         for i in range(self.num_fusions):
             fusion = self.fusions[i]
-            cost_volume = fusion(cost_volume)
+            cost_volume = fusion(cost_volume, side, keep) if side is not None else fusion(cost_volume)
+        if side is not None:
+            main.wait_stream(side)
+            del keep
         out = []  # 1/3, 1/6, 1/12
-        fused = use_fused(self, cost_volume[0])
         for i in range(len(self.final_conv)):
             if fused:
                 out = out + [conv_bn_act(cost_volume[i], self.final_conv[i])]

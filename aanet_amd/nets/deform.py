@@ -119,14 +119,16 @@ class _BottleneckBase(FoldCacheMixin, nn.Module):
         out = self.relu(out)
         return out
 
-    def _forward_fused(self, x, deform, conv1_out=None, csa_up=None):
+    def _forward_fused(self, x, deform, conv1_out=None, csa_up=None, before_tail=None):
         """conv1+bn1+relu, then conv2+bn2+relu -> conv3+bn3 (+identity) + relu as ONE HIP kernel
         (the conv3 GEMM runs in conv2's epilogue).  When the tail kernel takes the block, conv1
         writes its output channels-last (NHWC) so that conv2 / offset_conv / the DCN read each
         32-channel chunk of a position as one 128-byte line.  conv1_out: precomputed conv1.
         csa_up: coarser CSA exchange terms of this resolution's output branch; the tail kernel
         then also writes that branch's cross-scale sum, and (out, csa_out) is returned
-        (csa_out None when the tail kernel does not take the block)."""
+        (csa_out None when the tail kernel does not take the block).  before_tail: called just
+        before the tail kernel is launched (the stream join of the concurrent-scale schedule,
+        AdaptiveAggregation: csa_up is produced on the side stream)."""
         w3, b3, p3 = folded(self.conv3, self.bn3)
         width = self.conv1.weight.shape[0]
         c2 = self.conv2
@@ -150,6 +152,8 @@ class _BottleneckBase(FoldCacheMixin, nn.Module):
             ps, psh = bn_affine(self.bn2)
             _, _, wp = folded(dc, None)
             if pw:
+                if before_tail is not None:
+                    before_tail()
                 return ops.mdcn_pw(out, offset_mask, dc.weight, wp, dc.bias, ps, psh, "relu", p3, b3,
                                    identity, "relu", dc.stride, dc.padding, dc.dilation,
                                    c2.deformable_groups, 2.0 if c2.double_mask else 1.0,
@@ -160,16 +164,19 @@ class _BottleneckBase(FoldCacheMixin, nn.Module):
         else:
             w2, b2, p2 = folded(self.conv2, self.bn2)
             if pw:
+                if before_tail is not None:
+                    before_tail()
                 return ops.conv2d_pw(out, w2, p2, b2, None, None, "relu", p3, b3, identity, "relu",
                                      c2.stride[0], c2.padding[0], c2.dilation[0], csa_up=csa_up)
             out = conv_bn_act(out, self.conv2, self.bn2, "relu")
         out = conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity)
         return out if csa_up is None else (out, None)
 
-    def forward_csa(self, x, csa_up):
+    def forward_csa(self, x, csa_up, before_tail=None):
         """Eval-only: (block output, its output branch's CSA sum or None); see _forward_fused."""
         deform = isinstance(self, DeformSimpleBottleneck) or isinstance(self, DeformBottleneck)
-        r = self._forward_fused(x, deform=deform, csa_up=None if csa_up is None else list(csa_up))
+        r = self._forward_fused(x, deform=deform, csa_up=None if csa_up is None else list(csa_up),
+                                before_tail=before_tail)
         return r if isinstance(r, tuple) else (r, None)
 
 

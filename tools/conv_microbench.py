@@ -72,6 +72,13 @@ cases = {
                       2 * B * (H // 2) * (W // 2) * C * C * 9),
     "conv3x3_s2_32": (lambda: ops.conv2d_fused(x, w3[:32].contiguous(), b[:32].contiguous(), 2, 1, 1, 1,
                                                packed_weight=p3h), 2 * B * (H // 2) * (W // 2) * 32 * C * 9),
+    "conv3x3_s2_64_nhwc": (lambda: ops.conv2d_fused(xn, w3, b, 2, 1, 1, 1, "leaky", packed_weight=p3,
+                                                    out_nhwc=True), 2 * B * (H // 2) * (W // 2) * C * C * 9),
+    "conv3x3_s2_32_nhwc": (lambda: ops.conv2d_fused(xn, w3[:32].contiguous(), b[:32].contiguous(), 2, 1, 1, 1,
+                                                    packed_weight=p3h, out_nhwc=True),
+                           2 * B * (H // 2) * (W // 2) * 32 * C * 9),
+    "conv1x1_in_nhwc": (lambda: ops.conv2d_fused(xn, w1, b, act="relu", packed_weight=p1, out_nhwc=True),
+                        2 * B * H * W * C * C),
     "corr": (lambda: ops.corr_volume(fl, fr, 64), 0),
     "regress": (lambda: ops.disp_regress(vol64), 0),
     # C5 (PSMNet 4-D volume, 384x1248 -> 1/4: [B,32,96,312], D=192/4=48), B=4
