@@ -15,6 +15,7 @@
 // and sampling indices equal the CPU oracle's bit for bit (tests/test_gpu_mdcn.py).
 #include "common.h"
 #include "dcn_tile.h"
+#include "pointwise.h"
 
 #include <stdlib.h>
 
@@ -2444,6 +2445,25 @@ extern "C" int aanet_conv2d_fused_f32(const float *x, const float *weight, const
   a.residual = residual;
   set_split(a, layout, weight_packed);
   a.layout = layout & ~(AANET_CONV_EXACT_F32 | AANET_CONV_WEIGHTS_SPLIT);
+  if (a.split && a.layout >= 0 && a.layout <= 3 && !check_shapes(a) &&
+      pw_conv_supported(c, co, kh, kw, stride, pad, groups, (long)n * h * w, a.layout >> 1)) {
+    PwArgs p;  // 1x1: the streaming kernel (pointwise.hip)
+    p.x = x;
+    p.wsplit = a.wsplit;
+    p.bias = bias;
+    p.post_scale = post_scale;
+    p.post_shift = post_shift;
+    p.residual = residual;
+    p.act = act;
+    p.out = out;
+    p.N = n;
+    p.C = c;
+    p.P = h * w;
+    p.Co = co;
+    p.in_nhwc = a.layout & 1;
+    p.out_nhwc = a.layout >> 1;
+    return pw_conv_launch(p, as_hip(stream));
+  }
   return launch_fwd<0>(a, weight_packed, as_hip(stream));
 }
 
