@@ -53,6 +53,7 @@ struct MdcnArgs {
   int split;   // conv engine: split-bf16 contraction (AANET_CONV_EXACT_F32 clear, weights carry pieces)
   int halo;    // conv engine: 3x3 stride-1 halo-tile form (conv_fwd_kernel HALO)
   const bf16x8_t *wsplit, *tail_wsplit;  // bf16 piece fragments of weight / tail_w (split_frag_offset)
+  int dbg_noatom;  // AANET_DCN_BWD_DBG=1: the backward data kernels skip the grad_x scatter (timing)
   // CSA epilogue (tail kernels): csa_out = csa_act(out + sum_j up_r[j](up[j])), r = 2 or 4
   float *csa_out;
   const float *up[3];
@@ -1521,7 +1522,7 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_nhwc_kernel(MdcnArgs a, cons
       }
       // grad_x: lanes 0-31 channel cl of pixel 16w + 2t, lanes 32-63 of pixel 16w + 2t + 1
       const int cl = lane & 31;
-      if (cl < rows) {
+      if (cl < rows && !a.dbg_noatom) {
         const long cbase = (long)n * HW * C + c0 + cl;
         auto nadd = [&](int i, float v) {
           if (DET)
@@ -1705,7 +1706,7 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_win_kernel(MdcnArgs a, const
       // grad_x: lanes 0-31 channel cl of pixel 16w + 2t, lanes 32-63 of pixel 16w + 2t + 1; the
       // window channel index is c0 + cl - g*cpg (< cpg <= 32: one chunk per group)
       const int cl = lane & 31;
-      if (cl < rows) {
+      if (cl < rows && a.dbg_noatom != 1) {
         const long cbase = (long)n * HW * C + c0 + cl;
         const int wc = c0 + cl - g * cpg;
         auto gadd = [&](int i, float v) {
@@ -1767,6 +1768,7 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_win_kernel(MdcnArgs a, const
     }
   }
   __syncthreads();  // the window is complete
+  if (a.dbg_noatom) return;
   // add the window to the global accumulator: consecutive threads take consecutive channels of a
   // position (one 128-byte line per 32 lanes); untouched (zero) elements are skipped
   for (int e = tid; e < nwin; e += NT) {
@@ -1900,7 +1902,108 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_weight_kernel(MdcnArgs a, const f
       }
     }
   }
-  for (long t0 = r0; t0 < r1 && !PLAIN; t0 += PT) {
+  if constexpr (NR && !PLAIN) {
+    // Three-stage pipeline over the 64-pixel sub-tiles: the offsets / mask of sub-tile t+2 and
+    // the corner quads + grad_out tile of t+1 are loaded while the MFMAs of t run from LDS
+    // (sampling positions depend on the offsets: two dependent load levels per sub-tile).
+    const int q = tid & 7;
+    const int K2 = 2 * K;
+    float oh[2][2], ow[2][2], om[2][2];  // [stage slot][it]
+    f32x4 rc[2][4];                       // corner quads of the next sub-tile, per it
+    float rwt[2][5];                      // w1..w4, mask
+    float rg[64 * PT / NT];
+    auto off_load = [&](long t0, int sl) {
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const long t = t0 + (tid >> 3) + 32 * it;
+        const bool tv = t < r1;
+        const int n = tv ? (int)(t / P) : 0;
+        const long p = tv ? t % P : 0;
+        const float *off = a.offset + (long)n * a.off_bs + (long)g * K2 * P;
+        oh[sl][it] = tv ? off[(long)(2 * k) * P + p] : 0.f;
+        ow[sl][it] = tv ? off[(long)(2 * k + 1) * P + p] : 0.f;
+        om[sl][it] = tv ? load_mask(a, n, g, k, K, P, p) : 0.f;
+      }
+    };
+    auto corner_load = [&](long t0, int sl) {
+#pragma clang fp contract(off)
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const long t = t0 + (tid >> 3) + 32 * it;
+        const bool tv = t < r1;
+        const int n = tv ? (int)(t / P) : 0;
+        const long p = tv ? t % P : 0;
+        const int ho = (int)(p / a.Wo), wo = (int)(p % a.Wo);
+        const float h = (float)(ho * a.stride - a.pad + (k / a.kw) * a.dil) + oh[sl][it];
+        const float w = (float)(wo * a.stride - a.pad + (k % a.kw) * a.dil) + ow[sl][it];
+        Samp sp;
+        make_samp(sp, h, w, a.H, a.W, om[sl][it]);
+        const bool ok = tv && 4 * q < rows;
+        const float *xq = xh + (long)n * HW * C + c0 + 4 * q;
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        rc[it][0] = ok ? *reinterpret_cast<const f32x4 *>(xq + (long)sp.i1 * C) : z;
+        rc[it][1] = ok ? *reinterpret_cast<const f32x4 *>(xq + (long)sp.i2 * C) : z;
+        rc[it][2] = ok ? *reinterpret_cast<const f32x4 *>(xq + (long)sp.i3 * C) : z;
+        rc[it][3] = ok ? *reinterpret_cast<const f32x4 *>(xq + (long)sp.i4 * C) : z;
+        rwt[it][0] = sp.w1;
+        rwt[it][1] = sp.w2;
+        rwt[it][2] = sp.w3;
+        rwt[it][3] = sp.w4;
+        rwt[it][4] = ok ? sp.m : 0.f;  // 0 * (finite corners) = 0: masked-out rows stage zeros
+      }
+      const long t = t0 + lane;
+      const int n = t < r1 ? (int)(t / P) : 0;
+      const long p = t < r1 ? t % P : 0;
+      const float *gp = gout + (long)n * Co * P + p;
+#pragma unroll
+      for (int i = 0; i < 64 * PT / NT; ++i) {
+        const int co = co0 + wave + 4 * i;
+        rg[i] = (t < r1 && co < coE) ? gp[(long)co * P] : 0.f;
+      }
+    };
+    auto store = [&]() {
+#pragma clang fp contract(off)
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int pl = (tid >> 3) + 32 * it;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)  // samp_val per channel (same products and order)
+          sC[(4 * q + u) * GP2 + pl] = (rwt[it][0] * rc[it][0][u] + rwt[it][1] * rc[it][1][u] +
+                                        rwt[it][2] * rc[it][2][u] + rwt[it][3] * rc[it][3][u]) * rwt[it][4];
+      }
+#pragma unroll
+      for (int i = 0; i < 64 * PT / NT; ++i) sG[(wave + 4 * i) * GP2 + lane] = rg[i];
+    };
+    off_load(r0, 0);
+    corner_load(r0, 0);
+    if (r0 + PT < r1) off_load(r0 + PT, 1);
+    store();
+    __syncthreads();
+    int sl = 1;  // offset slot of sub-tile t0 + PT
+    for (long t0 = r0; t0 < r1; t0 += PT) {
+      const bool more = t0 + PT < r1;
+      if (more) {
+        corner_load(t0 + PT, sl);
+        if (t0 + 2 * PT < r1) off_load(t0 + 2 * PT, sl ^ 1);
+      }
+#pragma unroll 4
+      for (int ks = 0; ks < PT / 4; ++ks) {
+        const float av = sG[(16 * wave + jj) * GP2 + 4 * ks + kr];
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const float bv = sC[(16 * cb + jj) * GP2 + 4 * ks + kr];
+          acc[cb] = mfma16x16x4(av, bv, acc[cb]);
+        }
+      }
+      __syncthreads();
+      if (more) {
+        store();
+        __syncthreads();
+      }
+      sl ^= 1;
+    }
+  }
+  for (long t0 = r0; t0 < r1 && !PLAIN && !NR; t0 += PT) {
     if constexpr (NR) {
       const int q = tid & 7;
 #pragma unroll
@@ -2085,6 +2188,7 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
   a.layout = 0;
   a.split = 0;
   a.halo = 0;
+  a.dbg_noatom = 0;
   a.csa_out = nullptr;
   a.num_up = 0;
   a.csa_act = 0;
@@ -2785,6 +2889,8 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
     // replace int64 global ones); with float atomics the global-atomic kernel is faster (agg_s0
     // 5.1 vs 7.9 ms: the 75 KB of LDS halve the waves that hide the per-tap gather latency).
     // AANET_DCN_BWD_WINDOW: 0 never, 1 deterministic only, 2 both.
+    const char *dbg_env = getenv("AANET_DCN_BWD_DBG");
+    a.dbg_noatom = dbg_env ? atoi(dbg_env) : 0;
     const char *bwd_env = getenv("AANET_DCN_BWD_WINDOW");  // read per call (tests switch it)
     const int bwd_win = bwd_env ? atoi(bwd_env) : 1;
     const int cpg = c / dg, R = 2;
