@@ -430,7 +430,11 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   // LDS slot to the threads that stage channels of that pixel and group (the VALU it saves is
   // matrix-pipe time).
   constexpr int PSLOT = GPC * PTT * 8;
-  __shared__ __attribute__((aligned(16))) float smem[2 * BUF + (MODE ? 2 * PSLOT : 0)];
+  // HALO 3 (3x3, stride 2, pad 1, NCHW input): a 4 x 16 output tile reads a 9 x 33 input halo,
+  // whose 32-channel piece planes (57 KB) exceed the two im2col buffers
+  constexpr int HALO3_FLOATS = HALO == 3 ? 9 * 33 * 32 * 3 / 2 : 0;
+  constexpr int SMEM = 2 * BUF > HALO3_FLOATS ? 2 * BUF : HALO3_FLOATS;
+  __shared__ __attribute__((aligned(16))) float smem[SMEM + (MODE ? 2 * PSLOT : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool pwave = __builtin_amdgcn_readfirstlane(wave) < GPC * PTT / 64;  // tid < GPC*PTT
@@ -438,15 +442,18 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   const int wc0 = __builtin_amdgcn_readfirstlane((wave / WP) * NCB);  // first co block of the wave
   const int wp0 = __builtin_amdgcn_readfirstlane((wave % WP) * NPB);  // first px block of the wave
   const long P = (long)a.Ho * a.Wo;
-  static_assert(!HALO || (MODE == 0 && PREC == 1 && PTT == 128 && (LAYOUT & 1)), "halo configuration");
+  static_assert(!HALO || (MODE == 0 && PREC == 1 &&
+                          (HALO == 3 ? PTT == 64 && !(LAYOUT & 1) : PTT == 128 && (LAYOUT & 1)) && !(HALO == 3 && TAIL)),
+                "halo configuration");
+  constexpr int TRH = HALO == 3 ? 4 : 8;  // output rows of a halo tile (16 columns)
   const int htx = HALO ? (a.Wo + 15) / 16 : 1;
-  const int ntiles = HALO ? htx * ((a.Ho + 7) / 8) : (int)((P + PTT - 1) / PTT);
+  const int ntiles = HALO ? htx * ((a.Ho + TRH - 1) / TRH) : (int)((P + PTT - 1) / PTT);
   // XCD-aware remap of the pixel-tile index (bijective for any grid size)
   const int nwg = gridDim.x, b0 = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b0 & 7;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b0 >> 3);
   const int n = bid / ntiles, tile = bid % ntiles;
-  const int hy0 = HALO ? (tile / htx) * 8 : 0, hx0 = HALO ? (tile % htx) * 16 : 0;  // HALO tile origin
+  const int hy0 = HALO ? (tile / htx) * TRH : 0, hx0 = HALO ? (tile % htx) * 16 : 0;  // HALO tile origin
   const int Cg = a.C / a.groups, Cog = a.Co / a.groups, K = a.kh * a.kw, cpg = a.C / a.dg;
   const int ncot = (Cog + CO_T - 1) / CO_T;
   const int gc = blockIdx.y / ncot, cot = blockIdx.y % ncot;
@@ -857,15 +864,38 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   }
 
   if constexpr (HALO) {
-    constexpr int d = HALO;  // the dilation (= padding): halo geometry is compile-time
-    constexpr int hw = 16 + 2 * d, npos = (8 + 2 * d) * hw;
-    const int hy = hy0 - d, hx = hx0 - d;
-    constexpr int HIT = (npos * 8 + FNT - 1) / FNT;  // halo quads per thread
-    f32x4 hv[HIT];
+    // HALO 1/2: stride 1, dilation = padding = d; HALO 3: stride 2, dilation 1, padding 1
+    constexpr bool S2 = HALO == 3;
+    constexpr int d = S2 ? 1 : HALO;  // tap spacing in the halo
+    constexpr int hw = S2 ? 33 : 16 + 2 * d, npos = (S2 ? 9 : 8 + 2 * d) * hw;
+    const int hy = S2 ? 2 * hy0 - 1 : hy0 - d, hx = S2 ? 2 * hx0 - 1 : hx0 - d;
+    constexpr int HIT = S2 ? 1 : (npos * 8 + FNT - 1) / FNT;  // halo quads per thread (NHWC)
+    // NCHW (HALO 3): unit = (halo row, column quad, channel quad): 9 rows x 9 quads (input columns
+    // 2*hx0-4 .. 2*hx0+31, the first three unused) x 8 channel quads = 648 units, 2 per thread;
+    // a unit is 4 channel rows x 4 columns, stored as 4 positions of 4 channels (put_split)
+    constexpr int NU = 9 * 9 * 8, UIT = S2 ? (NU + FNT - 1) / FNT : 1;
+    f32x4 hv[HIT], hu[UIT][4];
+    auto load_halo_nchw = [&](int c0) {
+#pragma unroll
+      for (int i = 0; i < UIT; ++i) {
+        const int u = tid + FNT * i, cq = u / 81, rq = u % 81, row = rq / 9, qd = rq % 9;
+        const int yy = hy + row, xx = 2 * hx0 - 4 + 4 * qd;
+        const bool ok = u < NU && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;  // W % 4 == 0
+#pragma unroll
+        for (int ch = 0; ch < 4; ++ch) {
+          const int off = ok ? (((c0 + 4 * cq + ch) * a.H + yy) * a.W + xx) * 4 : img_bytes;
+          hu[i][ch] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+        }
+      }
+    };
     // 64-channel tiles recompute the halo quad offsets per chunk (a few VALU) rather than hold
     // them across the chunk loop: held, they were spilled to scratch and re-read every chunk
     // (76 B/lane at the 128-VGPR cap).  32-channel tiles have the registers to hold them.
     auto load_halo = [&](int c0) {
+      if constexpr (S2) {
+        load_halo_nchw(c0);
+        return;
+      }
       const int soff = __builtin_amdgcn_readfirstlane(c0 * 4);
       int t = tid;
       if constexpr (CO_T >= 64) asm volatile("" : "+v"(t));  // keep the arithmetic in the loop
@@ -908,7 +938,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       asm volatile("" : "+v"(col));  // recomputed per tap (not hoisted as 18 live addresses)
 #pragma unroll
       for (int b = 0; b < NPB; ++b) {
-        const int pos = (wp0 + b + ti * d) * hw + col + tj * d;
+        const int pos = S2 ? (2 * (wp0 + b) + ti) * hw + 2 * col + tj : (wp0 + b + ti * d) * hw + col + tj * d;
         const __bf16 *sH = reinterpret_cast<const __bf16 *>(smem) + swz(pos, kr);
         bf16x8 fb[3];
 #pragma unroll
@@ -917,19 +947,39 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
         for (int m = 0; m < NCB; ++m) acc[m][b] = mfma_split6(cur[m], fb, acc[m][b]);
       }
     };
+    // HALO 3 with 64-channel tiles: the next chunk's halo is not held in registers across the nine
+    // taps (32 VGPRs: they spilled at the 128 cap); its loads are issued just before the barrier
+    // that ends the previous chunk, so they overlap the slowest waves' last taps only
+    constexpr bool LATE = S2 && CO_T >= 64;
     auto stage = [&](int c0) {
+      if constexpr (LATE) load_halo(c0);
       __syncthreads();  // every wave is done with the previous chunk's halo
+      if constexpr (S2) {
+#pragma unroll
+        for (int i = 0; i < UIT; ++i) {
+          const int u = tid + FNT * i, cq = u / 81, rq = u % 81, row = rq / 9, qd = rq % 9;
+          if (u >= NU) continue;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {  // column 2*hx0-4 + 4qd + e -> halo column 4qd + e - 3
+            const int col = 4 * qd + e - 3;
+            if (col < 0) continue;
+            put_split(reinterpret_cast<__bf16 *>(smem), npos * 32, row * hw + col, cq,
+                      f32x4{hu[i][0][e], hu[i][1][e], hu[i][2][e], hu[i][3][e]});
+          }
+        }
+      } else {
 #pragma unroll
       for (int i = 0; i < HIT; ++i) {
         const int pos = (tid + FNT * i) >> 3;
         if (pos < npos) put_split(reinterpret_cast<__bf16 *>(smem), npos * 32, pos, tid & 7, hv[i]);
       }
+      }
       __syncthreads();
       const bool more = c0 + 32 < cend;
-      if (more) load_halo(c0 + 32);
+      if (more && !LATE) load_halo(c0 + 32);
       return more;
     };
-    load_halo(cbeg);
+    if constexpr (!LATE) load_halo(cbeg);
     load_ha(ha0, cbeg, 0);
     // nine taps per chunk: the A buffers alternate, so consecutive chunks start on opposite ones
     for (int c0 = cbeg; c0 < cend; c0 += 64) {
@@ -2224,8 +2274,17 @@ void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
       }
       return;
     }
+    if constexpr (MODE == 0 && PTT == 64) {
+      if (a.split && packed && a.halo == 3) {  // 3x3 stride-2 halo-tile form (NCHW input)
+        if (a.layout == 2)
+          hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 64, 1, 0, 1, 1, 2, CFG, 1, 3>), grid, blk, 0, st, a);
+        else
+          hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 64, 1, 0, 1, 1, 0, CFG, 1, 3>), grid, blk, 0, st, a);
+        return;
+      }
+    }
     if constexpr (MODE == 0 && PTT == 128) {
-      if (a.split && packed && a.halo) {  // 3x3 stride-1 halo-tile form (NHWC input), HALO = dil
+      if (a.split && packed && a.halo == 1) {  // 3x3 stride-1 halo-tile form (NHWC input), HALO = dil
         if (a.dil == 1) {
           if (a.tail_w)
             hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 1, 1, 1, 1, CFG, 1, 1>), grid, blk, 0, st, a);
@@ -2348,7 +2407,19 @@ int launch_fwd(const MdcnArgs &a_in, int packed, hipStream_t st) {
   a.halo = !nohalo && MODE == 0 && a.split && packed && (a.layout & 1) && a.kh == 3 && a.kw == 3 &&
            a.stride == 1 && a.pad == a.dil && a.dil <= 2 && co_t >= 32 && full_cfg(a, 0, co_t) == 0;
   if (a.halo) ptt = 128;
-  dim3 grid((unsigned)(a.halo ? (long)a.N * host_div_up(a.Wo, 16) * host_div_up(a.Ho, 8)
+  // stride-2 halo form (the CSA down-sampling convs, aggregation.py:364-372): NCHW input.  Opt-in
+  // (AANET_HALO_S2=1): alone it is 9-16 % faster than the im2col form at the C2 scale-0 shapes,
+  // but in the two-stream eval schedule its 57 KB workgroups take LDS from the scale-0 chain's
+  // kernels and the step got 2 % slower
+  static const int halo2 = [] { const char *e = getenv("AANET_HALO_S2"); return e ? atoi(e) : 0; }();
+  if (!nohalo && halo2 && MODE == 0 && a.split && packed && !(a.layout & 1) && !a.tail_w &&
+      a.kh == 3 && a.kw == 3 && a.stride == 2 && a.pad == 1 && a.dil == 1 && co_t >= 32 &&
+      full_cfg(a, 0, co_t) == 0 && a.W % 4 == 0) {
+    a.halo = 3;
+    ptt = 64;
+  }
+  const int trh = a.halo == 3 ? 4 : 8;
+  dim3 grid((unsigned)(a.halo ? (long)a.N * host_div_up(a.Wo, 16) * host_div_up(a.Ho, trh)
                               : a.N * host_div_up(P, ptt)),
             (unsigned)(a.groups * ncot));
   if (ptt == 128) {

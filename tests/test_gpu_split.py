@@ -35,7 +35,9 @@ def _errs(got, ref64, scale64):
     (2, 64, 24, 52, 64, 3, 1, 1, 1, 1, False),    # same, NCHW staging
     (2, 64, 24, 52, 54, 3, 1, 2, 2, 2, True),     # offset_conv: grouped, dilated, Cog = 27
     (2, 64, 24, 52, 64, 1, 1, 0, 1, 1, False),    # conv1 / conv3
-    (2, 64, 24, 52, 32, 3, 2, 1, 1, 1, False),    # CSA strided 3x3
+    (2, 64, 24, 52, 32, 3, 2, 1, 1, 1, False),    # CSA strided 3x3 (HALO 3 under AANET_HALO_S2=1)
+    (2, 64, 25, 36, 64, 3, 2, 1, 1, 1, False),    # stride 2, 64-ch tile, ragged rows / columns
+    (1, 32, 16, 40, 32, 3, 2, 1, 1, 1, False),    # stride 2, one input chunk
     (1, 128, 12, 40, 96, 3, 1, 1, 1, 1, False),   # Co > 64: two output tiles
     # halo-tile form (NHWC 3x3 stride 1): odd chunk counts, ragged tiles, Wo % 4 != 0, dil 2
     (1, 96, 13, 30, 64, 3, 1, 1, 1, 1, True),     # 3 channel chunks, element epilogue
@@ -173,6 +175,59 @@ def test_halo_conv_nhwc_output_vs_torch():
     assert (got.cpu() - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item())
 
 
+def test_halo_stride2_nhwc_output_vs_torch():
+    """Stride-2 halo form (NCHW input, HALO 3) with a channels-last output, bias, BN affine and
+    LeakyReLU: the CSA down-sampling exchange conv of aggregation.py:364-372."""
+    gen = torch.Generator().manual_seed(10)
+    x = torch.randn(2, 64, 21, 44, generator=gen)
+    w = torch.randn(64, 64, 3, 3, generator=gen) / 24
+    b = torch.randn(64, generator=gen)
+    sc, sh = torch.rand(64, generator=gen) + 0.5, torch.randn(64, generator=gen)
+    y = (F.conv2d(x, w, b, 2, 1) * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1))
+    ref = torch.where(y > 0, y, 0.2 * y)
+    xd, wd = x.to(DEV), w.to(DEV)
+    got = ops.conv2d_fused(xd, wd, b.to(DEV), 2, 1, 1, 1, "leaky", post_scale=sc.to(DEV),
+                           post_shift=sh.to(DEV), packed_weight=ops.pack_weight_split(wd), out_nhwc=True)
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=torch.channels_last)
+    assert (got.cpu() - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item())
+
+
+_S2_SCRIPT = """
+import torch, torch.nn.functional as F
+from aanet_amd import ops
+g = torch.Generator().manual_seed(12)
+for (N, C, H, W, Co, onhwc) in [(2, 64, 24, 52, 32, False), (2, 64, 25, 36, 64, True),
+                                (1, 32, 16, 40, 32, False), (1, 64, 128, 416, 64, True)]:
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(Co, C, 3, 3, generator=g) / (3 * C ** 0.5)
+    b = torch.randn(Co, generator=g)
+    ref = F.leaky_relu(F.conv2d(x.double(), w.double(), b.double(), 2, 1), 0.2)
+    wd = w.cuda()
+    got = ops.conv2d_fused(x.cuda(), wd, b.cuda(), 2, 1, 1, 1, "leaky",
+                           packed_weight=ops.pack_weight_split(wd), out_nhwc=onhwc)
+    again = ops.conv2d_fused(x.cuda(), wd, b.cuda(), 2, 1, 1, 1, "leaky",
+                             packed_weight=ops.pack_weight_split(wd), out_nhwc=onhwc)
+    assert torch.equal(got, again)
+    err = (got.cpu().double() - ref).abs().max().item()
+    assert err <= 2e-5 * (1 + ref.abs().max().item()), (N, C, H, W, Co, err)
+print("s2 halo ok")
+"""
+
+
+def test_halo_stride2_form_opt_in():
+    """The opt-in stride-2 halo form (AANET_HALO_S2=1, read once per process: run in a child
+    process) against torch fp64 over ragged tiles, one and two input chunks, 32/64-channel tiles,
+    NCHW and channels-last outputs and the C2 scale-0 shape, and run to run."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, AANET_HALO_S2="1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _S2_SCRIPT], env=env, cwd=root, capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0 and "s2 halo ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 def test_fused_paths_bit_reproducible():
     """Identical launches give identical bits on every fused path the hot path uses, at the C2
     scale-0 shape (B=8, contention on every CU) with fractional DCN offsets."""
@@ -192,6 +247,8 @@ def test_fused_paths_bit_reproducible():
     cases = {
         "halo 3x3": lambda: ops.conv2d_fused(xn, w3, b, 1, 1, 1, 1, "relu", packed_weight=p3),
         "halo offset conv": lambda: ops.conv2d_fused(xn, wo, bo, 1, 2, 2, 2, packed_weight=po),
+        "halo stride 2": lambda: ops.conv2d_fused(x, w3, b, 2, 1, 1, 1, "leaky", packed_weight=p3,
+                                                  out_nhwc=True),
         "conv1 nhwc out": lambda: ops.conv2d_fused(x, w1, b, act="relu", packed_weight=p1, out_nhwc=True),
         "dcn nhwc": lambda: ops.mdcn_forward_fused(xn, om, w3, None, b, b, "relu", 1, 2, 2, 2, 2.0,
                                                    packed_weight=p3),
