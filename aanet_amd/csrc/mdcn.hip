@@ -1873,7 +1873,8 @@ __global__ __launch_bounds__(256) void weight_kcco_kernel(const float *__restric
 // DET: each pixel-range split writes its partial sums to part[split][co][c][k] (no atomics);
 // det_weight_reduce_kernel adds them to grad_weight in split order.
 // NR: the col chunk is sampled from the channels-last copy xh [N][H*W][C] (C, C/dg % 4 == 0):
-// thread = (pixel, channel quad), one 16-byte load per corner (8 lanes = one 128-B line).
+// thread = (pixel, channel quad), one 16-byte load per corner (8 lanes = one 128-B line); the
+// sub-tile loop is software-pipelined (see the NR branch).
 // PLAIN: the weight gradient of an ordinary (grouped) convolution (aanet_conv2d_wgrad_f32): the
 // col chunk is the tap's shifted window of x (zero outside), a.dg carries the conv's groups,
 // grad_weight is [Co][C/groups][K] and output-channel tiles stay inside the chunk's group.
@@ -2053,34 +2054,8 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_weight_kernel(MdcnArgs a, const f
       sl ^= 1;
     }
   }
+  // NCHW x (neither PLAIN nor NR): the sampled col chunk and the grad_out tile per sub-tile
   for (long t0 = r0; t0 < r1 && !PLAIN && !NR; t0 += PT) {
-    if constexpr (NR) {
-      const int q = tid & 7;
-#pragma unroll
-      for (int it = 0; it < 2; ++it) {
-        const int pl = (tid >> 3) + 32 * it;
-        const long t = t0 + pl;
-        const bool tv = t < r1;
-        const int n = tv ? (int)(t / P) : 0;
-        const long p = tv ? t % P : 0;
-        Samp s;
-        pixel_samp(s, a, n, g, k, p, (int)(p / a.Wo), (int)(p % a.Wo));
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (tv && 4 * q < rows) {
-#pragma clang fp contract(off)
-          const float *xq = xh + (long)n * HW * C + c0 + 4 * q;
-          const f32x4 v1 = *reinterpret_cast<const f32x4 *>(xq + (long)s.i1 * C);
-          const f32x4 v2 = *reinterpret_cast<const f32x4 *>(xq + (long)s.i2 * C);
-          const f32x4 v3 = *reinterpret_cast<const f32x4 *>(xq + (long)s.i3 * C);
-          const f32x4 v4 = *reinterpret_cast<const f32x4 *>(xq + (long)s.i4 * C);
-#pragma unroll
-          for (int u = 0; u < 4; ++u)  // samp_val per channel (same products and order)
-            v[u] = (s.w1 * v1[u] + s.w2 * v2[u] + s.w3 * v3[u] + s.w4 * v4[u]) * s.m;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) sC[(4 * q + u) * GP2 + pl] = v[u];
-      }
-    } else {
     const long t = t0 + lane;
     const bool tv = t < r1;
     const int n = tv ? (int)(t / P) : 0;
@@ -2094,7 +2069,6 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_weight_kernel(MdcnArgs a, const f
       float v = 0.f;
       if (cl < rows && tv) v = samp_val(xn + (long)(c0 + cl) * HW, s);
       sC[cl * GP2 + lane] = v;
-    }
     }
     for (int e = tid; e < 64 * PT; e += NT) {
       const int col = e / PT, pl = e % PT;
