@@ -169,11 +169,12 @@ class Trainer:
     """One optimizer step per `accumulation_steps` micro-batches (model.py:64-153)."""
 
     def __init__(self, model, lr=1e-3, weight_decay=1e-4, accumulation_steps=1,
-                 highest_loss_only=False, max_disp=192, engine_convs=None):
+                 highest_loss_only=False, max_disp=192, engine_convs=None, capturable=False):
         """max_disp: the image-resolution disparity range of the valid mask (train.py --max_disp,
         default 192), NOT the cost-volume D.  engine_convs: run the plain convs on the HIP engine
         (use_engine_convs); default: when torch.use_deterministic_algorithms(True) is on, where
-        MIOpen has only its naive deterministic kernels."""
+        MIOpen has only its naive deterministic kernels.  capturable: Adam keeps its step count on
+        the device, so that the step can be captured into a HIP graph (graph_step)."""
         if engine_convs is None:
             engine_convs = torch.are_deterministic_algorithms_enabled()
         if engine_convs:
@@ -182,8 +183,61 @@ class Trainer:
         self.accumulation_steps = accumulation_steps
         self.highest_loss_only = highest_loss_only
         self.max_disp = max_disp
-        self.optimizer = torch.optim.Adam(param_groups(model, lr), weight_decay=weight_decay)
+        self.optimizer = torch.optim.Adam(param_groups(model, lr), weight_decay=weight_decay,
+                                          capturable=capturable)
         self.micro = 0
+        self._graph = None
+
+    def graph_step(self, left_feature, right_feature, gt_disp, mask, warmup=3):
+        """The whole step (forward, loss, backward, Adam) as ONE HIP graph replay, for a single
+        process with static inputs (the tensors passed on the first call are captured by address
+        and must be refilled in place for new data) and one micro-batch per optimizer step.  The
+        eager step issues ~2.9k kernel launches; replayed, the host cost is one launch.  The first
+        call runs `warmup` eager steps on a side stream (allocator and MIOpen algorithm state),
+        then captures; it needs Trainer(capturable=True).  Returns the loss tensor (overwritten by
+        every replay).  The empty-mask skip of step() is a host synchronisation and is not taken
+        here: the caller guarantees valid pixels."""
+        if self._graph is None:
+            if self.accumulation_steps != 1 or isinstance(self.model, nn.parallel.DistributedDataParallel):
+                raise RuntimeError("graph_step: one process, no gradient accumulation")
+            if not self.optimizer.param_groups[0].get("capturable", False):
+                raise RuntimeError("graph_step needs Trainer(capturable=True)")
+            self.model.train()
+
+            def body():
+                pyramid = self.model(left_feature, right_feature)
+                if self.highest_loss_only:
+                    pyramid = [pyramid[-1]]
+                total, _ = disparity_loss(pyramid, gt_disp, mask,
+                                          pyramid_weights(len(pyramid), self.highest_loss_only))
+                total.backward()
+                self.optimizer.step()
+                return total.detach()
+            # the warm-up steps must not count: parameters, BN buffers and the optimizer state are
+            # restored in place afterwards (the graph holds their addresses)
+            snap = [(t, t.detach().clone()) for t in
+                    list(self.model.parameters()) + list(self.model.buffers())]
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(warmup):
+                    self.optimizer.zero_grad(set_to_none=True)
+                    body()
+            torch.cuda.current_stream().wait_stream(side)
+            self.optimizer.zero_grad(set_to_none=True)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                self._graph_loss = body()
+            self._graph = graph
+            with torch.no_grad():
+                for t, v in snap:
+                    t.copy_(v)
+                for st in self.optimizer.state.values():  # Adam: step, exp_avg, exp_avg_sq start at 0
+                    for v in st.values():
+                        if torch.is_tensor(v):
+                            v.zero_()
+        self._graph.replay()
+        return self._graph_loss
 
     def valid_mask(self, disp):
         """model.py:71,75: 0 < d < max_disp."""

@@ -641,21 +641,32 @@ def train_main(args, device, rank, world):
         torch.utils.deterministic.fill_uninitialized_memory = False
     model = build_model(device, intermediate_supervision=True).train()
     model = atrain.wrap_data_parallel(model, device)
-    trainer = atrain.Trainer(model, lr=1e-3, engine_convs={"auto": None, "on": True,
-                                                           "off": False}[args.engine_convs])
+    use_graph = world == 1 and not args.no_graph
+    engine = {"auto": None, "on": True, "off": False}[args.engine_convs]
+    trainer = atrain.Trainer(model, lr=1e-3, engine_convs=engine, capturable=use_graph)
     left, right = make_features(args.train_batch, rank, device, args.features, TRAIN_IMG)
     gen = torch.Generator(device=device).manual_seed(99 + rank)
     gt = torch.rand((args.train_batch,) + TRAIN_IMG, device=device, generator=gen) * (MAXD_IMG - 1)
     mask = (gt > 0) & (gt < MAXD_IMG)
+    step = lambda: trainer.step(left, right, gt, mask)  # noqa: E731
+    if use_graph:  # one HIP graph per step (the eager step is launch-bound: ~2.9k launches)
+        try:
+            trainer.graph_step(left, right, gt, mask)
+            step = lambda: trainer.graph_step(left, right, gt, mask)  # noqa: E731
+        except Exception as e:  # noqa: BLE001
+            print(f"training graph capture failed ({e}); timing eager steps", file=sys.stderr)
+            use_graph = False
+            trainer = atrain.Trainer(model, lr=1e-3, engine_convs=engine)
+            step = lambda: trainer.step(left, right, gt, mask)  # noqa: E731
     for _ in range(args.warmup):
-        loss = trainer.step(left, right, gt, mask)
+        loss = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = trainer.step(left, right, gt, mask)
+        loss = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -679,6 +690,7 @@ def train_main(args, device, rank, world):
                        "global_batch": args.train_batch * world,
                        "parallelism": f"dp{world} (SyncBN + DDP all-reduce)" if world > 1
                        else "dp1", "deterministic": bool(args.deterministic),
+                       "hip_graph": use_graph,
                        "engine_convs": args.engine_convs},
             "final_loss": float(loss)}), flush=True)
     if world > 1:

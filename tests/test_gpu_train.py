@@ -134,3 +134,31 @@ def test_ddp_syncbn_two_ranks_match_full_batch():
         assert p.exitcode == 0
     assert sums[0] == sums[1]                 # all-reduced gradients identical on both ranks
     assert cos > 0.9999 and rel < 1e-2, (cos, rel)
+
+
+@pytest.mark.parametrize("det", [False, True])
+def test_graph_step_matches_eager_steps(det):
+    """Trainer.graph_step (the whole step as one HIP graph replay, warm-up steps undone) gives the
+    parameters of the same number of eager steps (same capturable Adam), and the loss falls."""
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(det, warn_only=True)
+    try:
+        l, r, gt = _inputs(2, 7)
+        mask = (gt > 0) & (gt < 192)
+        runs = []
+        for graph in (False, True):
+            m = _model(13).train()
+            t = train.Trainer(m, lr=1e-3, capturable=True)
+            losses = []
+            for _ in range(3):
+                loss = t.graph_step(l, r, gt, mask) if graph else t.step(l, r, gt, mask)
+                losses.append(float(loss))
+            runs.append(([p.detach().clone() for p in m.parameters()], losses))
+    finally:
+        torch.use_deterministic_algorithms(prev)
+    (pe, le), (pg, lg) = runs
+    assert abs(le[0] - lg[0]) <= 1e-5 * abs(le[0]), (le, lg)
+    assert lg[-1] < lg[0]
+    num = sum(float((a - b).double().norm() ** 2) for a, b in zip(pe, pg)) ** 0.5
+    den = sum(float(a.double().norm() ** 2) for a in pe) ** 0.5
+    assert num <= 1e-5 * den, (num, den)
