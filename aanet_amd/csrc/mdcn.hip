@@ -2595,7 +2595,7 @@ extern "C" int aanet_conv2d_fused_f32(const float *x, const float *weight, const
   set_split(a, layout, weight_packed);
   a.layout = layout & ~(AANET_CONV_EXACT_F32 | AANET_CONV_WEIGHTS_SPLIT);
   if (a.split && a.layout >= 0 && a.layout <= 3 && !check_shapes(a) &&
-      pw_conv_supported(c, co, kh, kw, stride, pad, groups, (long)n * h * w, a.layout >> 1)) {
+      pw_conv_supported(c, co, kh, kw, stride, pad, groups, (long)n * h * w, a.layout >> 1, h * w)) {
     PwArgs p;  // 1x1: the streaming kernel (pointwise.hip)
     p.x = x;
     p.wsplit = a.wsplit;

@@ -31,12 +31,13 @@ __device__ __forceinline__ float pw_act(float v, int act) {
 
 // Epilogue of one 16-pixel column block: lane holds channels c0..c0+3 (c0 = 16 blk + 4kr) of
 // flattened pixel t.
+// (n, p): image and pixel of t for the NCHW output (callers derive them without a division).
 template <int NB, int ONH>
 __device__ __forceinline__ void pw_store(const PwArgs &a, const f32x4 (&acc)[NB],
-                                         const float (&eb)[NB][4], int t, int half, int kr) {
+                                         const float (&eb)[NB][4], int t, int half, int kr, int n,
+                                         int p) {
   const int T = a.N * a.P, P = a.P, Co = a.Co;
   if (t >= T) return;
-  const int n = ONH ? 0 : t / P, p = ONH ? 0 : t - n * P;
 #pragma unroll
   for (int m = 0; m < NB; ++m) {
     const int c0 = 16 * (NB * half + m) + 4 * kr;
@@ -130,7 +131,8 @@ __global__ __launch_bounds__(256) void pw_conv_kernel(PwArgs a) {
 #pragma unroll
       for (int m = 0; m < NB; ++m) acc[m] = mfma_split6(A[cc][m], B, acc[m]);
     }
-    pw_store<NB, ONH>(a, acc, eb, b * 16 + jj, half, kr);
+    const int t = b * 16 + jj, n = ONH ? 0 : t / a.P;
+    pw_store<NB, ONH>(a, acc, eb, t, half, kr, n, t - n * a.P);
   };
 
   float va[NCC][8], vb[NCC][8];
@@ -156,7 +158,9 @@ __global__ __launch_bounds__(256) void pw_conv_nchw_kernel(PwArgs a) {
   constexpr int SUB = 4 / CB;               // pixel sub-blocks per workgroup block
   constexpr int SW = CB == 4 ? 64 : 32;     // pixels per sub-block (16-pixel MFMA column groups)
   constexpr int BP = SW * SUB;              // pixels per block
-  constexpr int PXP = BP + 4;               // LDS row pitch (floats): 16-byte aligned rows
+  // LDS row pitch (floats): 8 * PXP = 16 (mod 32), so the two lane groups kr, kr+1 of a 32-lane
+  // half read banks 16 apart (conflict-free fragment reads); rows are 8-byte aligned
+  constexpr int PXP = BP + 2;
   constexpr int QPR = BP / 4;               // 16-byte pieces per channel row
   constexpr int LV = CI * QPR / 256;        // pieces per thread per block
   static_assert(LV >= 1 && 256 % QPR == 0, "block shape");
@@ -204,9 +208,13 @@ __global__ __launch_bounds__(256) void pw_conv_nchw_kernel(PwArgs a) {
     }
   };
   auto stage = [&](int buf) {
+    typedef float f32x2_t __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int i = 0; i < LV; ++i)
-      *reinterpret_cast<f32x4 *>(&sX[buf][(RSTEP * i + lrow) * PXP + 4 * lq]) = rv[i];
+    for (int i = 0; i < LV; ++i) {
+      float *d = &sX[buf][(RSTEP * i + lrow) * PXP + 4 * lq];
+      *reinterpret_cast<f32x2_t *>(d) = f32x2_t{rv[i][0], rv[i][1]};
+      *reinterpret_cast<f32x2_t *>(d + 2) = f32x2_t{rv[i][2], rv[i][3]};
+    }
   };
 
   load(b0);
@@ -216,6 +224,7 @@ __global__ __launch_bounds__(256) void pw_conv_nchw_kernel(PwArgs a) {
     const int buf = (b - b0) & 1;
     if (b + 1 < b1) load(b + 1);
     const float *xs = sX[buf];
+    const int n0b = __builtin_amdgcn_readfirstlane((b * BP) / P), p0b = b * BP - n0b * P;
 #pragma unroll
     for (int g = 0; g < SW / 16; ++g) {
       f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -228,7 +237,15 @@ __global__ __launch_bounds__(256) void pw_conv_nchw_kernel(PwArgs a) {
         split8(v, B);
         acc[0] = mfma_split6(A[cc], B, acc[0]);
       }
-      pw_store<1, ONH>(a, acc, eb, b * BP + SW * sub + 16 * g + jj, cb, kr);
+      // the block's first pixel is (n0, p0) (one scalar division per block); a block spans at
+      // most 1 + BP / P images, so the carry below runs at most once when P >= BP
+      const int off = SW * sub + 16 * g + jj;
+      int nn = n0b, pp = p0b + off;
+      while (pp >= P) {
+        pp -= P;
+        ++nn;
+      }
+      pw_store<1, ONH>(a, acc, eb, b * BP + off, cb, kr, nn, pp);
     }
     if (b + 1 < b1) {
       stage(buf ^ 1);
@@ -279,15 +296,15 @@ void launch_ci(const PwArgs &a, hipStream_t st) {
 }  // namespace
 
 int pw_conv_supported(int c, int co, int kh, int kw, int stride, int pad, int groups, long np,
-                      int out_nhwc) {
+                      int out_nhwc, int p) {
   static const int on = [] { const char *e = getenv("AANET_PW"); return e ? atoi(e) : 1; }();
   return on && kh == 1 && kw == 1 && stride == 1 && pad == 0 && groups == 1 && (c == 32 || c == 64) &&
-         co >= 1 && co <= 64 && np + 16 < 0x7fffffffL && (!out_nhwc || co % 4 == 0);
+         co >= 1 && co <= 64 && np + 16 < 0x7fffffffL && (!out_nhwc || co % 4 == 0) && p >= 1;
 }
 
 int pw_conv_launch(const PwArgs &a, hipStream_t st) {
   if (!a.x || !a.wsplit || !a.out || (a.post_scale && !a.post_shift)) return AANET_EINVAL;
-  if (!pw_conv_supported(a.C, a.Co, 1, 1, 1, 0, 1, (long)a.N * a.P, a.out_nhwc))
+  if (!pw_conv_supported(a.C, a.Co, 1, 1, 1, 0, 1, (long)a.N * a.P, a.out_nhwc, a.P))
     return AANET_EUNSUPPORTED;
   if (a.C == 32)
     launch_ci<32>(a, st);

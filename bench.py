@@ -165,6 +165,16 @@ def kernel_rooflines(model, left, right, batch, iters):
     ms = time_events(lambda: ops.disp_regress(vol), iters, stream)
     res["disp_regress_s0"] = dict(bound="hbm", ms=ms, algo=reg_bytes, unit="GB/s",
                                   achieved=reg_bytes / ms / 1e6, peak=HBM_PEAK_GBS)
+    # the bottleneck conv1 (1x1 + BN + ReLU, NCHW in -> channels-last out; pointwise.hip), scale 0:
+    # algorithmic bytes = read the 64-channel input once + write the 64-channel output once
+    blk1 = model.aggregation.fusions[5].branches[0][0]
+    with torch.no_grad():
+        w1, b1, p1 = folded(blk1.conv1, blk1.bn1)
+        ms = time_events(lambda: ops.conv2d_fused(vol, w1, b1, act="relu", packed_weight=p1,
+                                                  out_nhwc=True), iters, stream)
+    pw_bytes = 4 * B * H * W * (w1.shape[1] + w1.shape[0])
+    res["conv1x1_s0"] = dict(bound="hbm", ms=ms, algo=pw_bytes, unit="GB/s",
+                             achieved=pw_bytes / ms / 1e6, peak=HBM_PEAK_GBS)
     # modulated DCN as the hot path runs it (DeformSimpleBottleneck of the last fusion, scale 0):
     # NHWC conv1 output in, DCN + BN2 + ReLU -> conv3 + BN3 + identity + ReLU -> block output and
     # the scale-0 cross-scale sum, in one kernel

@@ -18,6 +18,8 @@ os.makedirs(dst, exist_ok=True)
 # bench.py kernel_rooflines keys -> kernel names
 KMAP = {"corr_volume_s0": r"corr_volume_kernel<5, 1>", "disp_regress_s0": r"disp_regress_fixed_kernel<64>",
         "corr_pyramid": r"corr_pyramid_kernel",
+        # the streaming 1x1 conv (pointwise.hip), NCHW input, 4 output-channel blocks, NHWC out
+        "conv1x1_s0": r"pw_conv_nchw_kernel<64, 4, 1>",
         # the LDS-window deformable tail (dcn_tile.hip; the generic engine's split form was
         # conv_fwd_kernel<1, 64, 128, 1, 1, 1, 1, 1, 0, 1, 0>)
         "mdcn_pw_s0": r"dcn_tile_kernel<2>",
