@@ -1152,6 +1152,12 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   // expose the HBM / L2 latency once per item.
   constexpr int EB = EPT >= 2 ? 2 : 1;
   const bool csa = TAIL && a.csa_out;
+  // the resize ratios of the CSA terms (area_pixel_compute_scale), once per thread: an IEEE
+  // division is a ~10-instruction sequence, and the item loop would repeat it per item and term
+  float rsc[2] = {0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    if (csa && j < a.num_up) rsc[j] = (float)a.up_h[j] / (float)a.Ho;
 #pragma unroll
   for (int i0 = 0; i0 < EPT; i0 += EB) {
     f32x4 ev[EB], er[EB], eu[EB][2][2];
@@ -1173,7 +1179,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
         for (int j = 0; j < 2; ++j) {
           if (j >= a.num_up) break;
           const int ih = a.up_h[j], iw = a.up_w[j], r = a.up_r[j];
-          float hr = ((float)ih / (float)a.Ho) * ((float)y + 0.5f) - 0.5f;
+          float hr = rsc[j] * ((float)y + 0.5f) - 0.5f;
           hr = hr < 0.f ? 0.f : hr;
           const int h1 = (int)hr, h1p = h1 < ih - 1 ? 1 : 0;
           const float *im = a.up[j] + plane * ih * iw;
@@ -1209,8 +1215,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           if (j >= a.num_up) break;
-          const int ih = a.up_h[j];
-          float hr = ((float)ih / (float)a.Ho) * ((float)y + 0.5f) - 0.5f;
+          float hr = rsc[j] * ((float)y + 0.5f) - 0.5f;
           hr = hr < 0.f ? 0.f : hr;
           const float h1l = hr - (float)(int)hr, h0l = 1.f - h1l;
           v += h0l * hlerp(eu[b][j][0], a.up_r[j]) + h1l * hlerp(eu[b][j][1], a.up_r[j]);
