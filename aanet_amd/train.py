@@ -145,8 +145,8 @@ def _engine_conv_ok(m):
 
 
 def _engine_conv_forward(m, x):
-    if x.dtype != torch.float32 or not x.is_cuda:
-        raise RuntimeError("engine convs take fp32 CUDA tensors")
+    if x.dtype != torch.float32 or not x.is_cuda:  # the HIP engine takes fp32 device tensors
+        return nn.Conv2d.forward(m, x)
     return EngineConv2dFunction.apply(x, m.weight, m.bias, m.stride[0], m.padding[0],
                                       m.dilation[0], m.groups)
 

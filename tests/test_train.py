@@ -14,7 +14,7 @@ import torch.multiprocessing as mp
 import torch.nn as nn
 import torch.nn.functional as F
 
-from aanet_amd import train
+from aanet_amd import nets, train
 
 
 class TinyPath(nn.Module):
@@ -205,3 +205,21 @@ def test_all_invalid_batch_is_skipped_like_the_reference():
     assert loss is not None and torch.isfinite(loss)
     assert not all(torch.equal(a, b) for a, b in zip(before, m.parameters()))
     assert all(torch.isfinite(p).all() for p in m.parameters())
+
+
+def test_use_engine_convs_marks_convs_and_keeps_cpu_path():
+    """use_engine_convs patches every engine-eligible nn.Conv2d (the grouped dilated offset conv
+    too) without changing the module tree; CPU tensors still take the reference convolution."""
+    torch.manual_seed(0)
+    m = nets.AANetHotPath(16, no_intermediate_supervision=False, num_deform_blocks=3)
+    keys = set(m.state_dict())
+    n = train.use_engine_convs(m)
+    convs = [c for c in m.modules() if isinstance(c, torch.nn.Conv2d)]
+    assert n == len(convs) > 20 and all(getattr(c, "_aanet_engine", False) for c in convs)
+    assert set(m.state_dict()) == keys
+    assert train.use_engine_convs(m) == 0  # idempotent
+    conv = convs[0]
+    x = torch.randn(1, conv.in_channels, 9, 11)
+    ref = torch.nn.functional.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding,
+                                     conv.dilation, conv.groups)
+    assert torch.equal(conv(x), ref)
