@@ -165,3 +165,31 @@ def test_grouped_deform_conv_fused_matches_autograd_path():
         fused = dc(x)
     ref = dc(x.clone().requires_grad_()).detach()   # autograd path (ModulatedDeformConvFunction)
     assert (fused - ref).abs().max().item() <= 2e-4 * (1 + ref.abs().max().item())
+
+
+def test_two_stream_schedule_graph_replay_and_single_stream_match():
+    """The eval aggregation's two-stream schedule (coarse scales on a side stream, joined before
+    the scale-0 tail kernel) captured in a HIP graph, as bench.py runs it: replays give the eager
+    result bit for bit, at every pyramid level, and so does the one-stream schedule
+    (AANET_CONCURRENT_SCALES=0: the kernels and their inputs are the same, only their issue
+    order differs)."""
+    import os
+    from aanet_amd.nets import aggregation
+    g, sd, m, left, right = _model("hotpath_d64")
+    with torch.no_grad():
+        eager = [t.clone() for t in m(left, right)]
+        os.environ["AANET_CONCURRENT_SCALES"] = "0"
+        try:
+            assert not aggregation.concurrent_scales()
+            single = [t.clone() for t in m(left, right)]
+        finally:
+            del os.environ["AANET_CONCURRENT_SCALES"]
+        assert aggregation.concurrent_scales()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            static = m(left, right)
+        for _ in range(3):
+            graph.replay()
+            torch.cuda.synchronize()
+            for a, b, c in zip(eager, static, single):
+                assert torch.equal(a, b) and torch.equal(a, c)
