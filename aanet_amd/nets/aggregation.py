@@ -23,18 +23,30 @@ from .deform import DeformSimpleBottleneck, SimpleBottleneck
 _SIDE_STREAMS = {}
 
 
-def side_stream(device):
-    """The second HIP stream of the concurrent-scale schedule (one per device, created outside
-    any graph capture: the first eval forward is a warm-up)."""
-    s = _SIDE_STREAMS.get(device)
-    if s is None:
-        s = _SIDE_STREAMS[device] = torch.cuda.Stream(device=device)
-    return s
+def side_streams(device, n):
+    """The side HIP streams of the concurrent-scale schedule: one per coarse scale (created once
+    per device, outside any graph capture: the first eval forward is a warm-up)."""
+    ss = _SIDE_STREAMS.setdefault(device, [])
+    while len(ss) < n:
+        ss.append(torch.cuda.Stream(device=device))
+    return ss[:n]
 
 
 def concurrent_scales():
-    """AANET_CONCURRENT_SCALES=0 runs the whole eval aggregation on one stream (A/B switch)."""
+    """AANET_CONCURRENT_SCALES=0 runs the whole eval aggregation on one stream (A/B switch);
+    AANET_SIDE_STREAMS=1 puts every coarse scale on one shared side stream (round-2 schedule)."""
     return os.environ.get("AANET_CONCURRENT_SCALES", "1") != "0"
+
+
+def num_side_streams(num_scales):
+    n = int(os.environ.get("AANET_SIDE_STREAMS", "0") or 0)
+    return max(1, min(n, num_scales - 1)) if n > 0 else num_scales - 1
+
+
+def _record(stream):
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    return ev
 
 
 def csa_epilogue_ok(x0, up):
@@ -110,44 +122,99 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
         layer = self.fuse_layers[i][j]
         return conv_bn_act(x[j], layer[0], layer[1], None)
 
-    def _forward_eval(self, x, side=None, keep=None):
+    def _down(self, x, i, j):
+        """Exchange term fuse_layers[i][j] for i > j: the chain of 3x3 stride-2 convs (+BN,
+        LeakyReLU between them) from scale j down to scale i."""
+        y = x[j]
+        layer = self.fuse_layers[i][j]
+        for k, seq in enumerate(layer):
+            y = conv_bn_act(y, seq[0], seq[1], None if k == len(layer) - 1 else "leaky")
+        return y
+
+    def _forward_eval(self, x, streams=None, keep=None):
         """Eval ISA + CSA.  The coarser scales run first, so that their exchange terms for output
         branch 0 exist when the scale-0 bottleneck runs: its tail kernel then writes both the
         block output and the cross-scale sum of branch 0 (aanet_csa_epilogue_t), which removes
         the scale-0 resize-sum kernel.  The in-place list mutation of aggregation.py:382 and the
         term order of aggregation.py:388-400 are unchanged (the branches are independent).
 
-        side (a second HIP stream, AdaptiveAggregation): the coarse-scale work -- the scale 1..S-1
-        blocks, the exchange terms of branch 0, and after the scale-0 block the CSA of branches
-        1..S-1 -- is issued on `side`, concurrently with the scale-0 chain on the current stream
-        (conv1 -> offset conv -> tail kernel, which joins `side` just before it launches).  The
-        scale-0 kernels are latency-bound, so the coarse scales fill the CUs they leave idle.
-        Tensors read across the two streams are appended to `keep` (alive until the caller joins
-        the streams, so the caching allocator cannot hand their memory to the other stream)."""
+        streams (AdaptiveAggregation's concurrent-scale schedule): [current stream, side stream
+        of scale 1, ..., of scale S-1] (side streams may repeat).  Every piece of work runs on
+        the stream of the scale it produces, as soon as its inputs exist (HIP events):
+          scale j >= 1: block j -> the up terms (i < j, 1x1 at scale j) -> [every coarse
+                        block done] the down terms from the coarse scales j' < j (stride-2
+                        chains) -> [block 0 done] the down term from scale 0 -> branch j's sum;
+          scale 0:      conv1 -> offset conv -> [coarse up terms done] the tail kernel (block
+                        output + branch 0's CSA sum).
+        After the scale-0 tail, the down chains of the coarse branches run concurrently on their
+        own streams, and with them the next module's coarse blocks and exchange terms: that is
+        the dependency chain between two scale-0 tail kernels.  Tensors read
+        across streams are appended to `keep` (alive until the caller joins the streams, so the
+        caching allocator cannot hand their memory to another stream)."""
         S = len(self.branches)
-        main = torch.cuda.current_stream(x[0].device) if side is not None else None
-        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+        nout = len(self.fuse_layers)
+        if streams is None:
             for i in range(1, S):
                 for j in range(self.num_blocks):
                     x[i] = self.branches[i][j](x[i])
             up0 = [self._exchange_up(x, 0, j) for j in range(1, S)]
-        terms = {(0, j): t for j, t in zip(range(1, S), up0)}
-        for j in range(self.num_blocks - 1):
-            x[0] = self.branches[0][j](x[0])
-        last = self.branches[0][self.num_blocks - 1]
-        join = (lambda: main.wait_stream(side)) if side is not None else None
-        x[0], csa0 = last.forward_csa(x[0], up0 if csa_epilogue_ok(x[0], up0) else None,
-                                      before_tail=join)
-        if side is None:
+            terms = {(0, j): t for j, t in zip(range(1, S), up0)}
+            for j in range(self.num_blocks - 1):
+                x[0] = self.branches[0][j](x[0])
+            x[0], csa0 = self.branches[0][self.num_blocks - 1].forward_csa(
+                x[0], up0 if csa_epilogue_ok(x[0], up0) else None)
             return self._fuse_eval(x, {0: csa0} if csa0 is not None else {}, terms)
-        keep.extend(up0)
+
+        main = streams[0]
+        terms, up_ev = {}, {}
+        # coarse blocks and their up terms (i < j: 1x1 at scale j), each on its scale's stream
+        for j in range(1, S):
+            with torch.cuda.stream(streams[j]):
+                for b in range(self.num_blocks):
+                    x[j] = self.branches[j][b](x[j])
+                for i in range(min(j, nout)):
+                    terms[(i, j)] = self._exchange_up(x, i, j)
+                up_ev[j] = _record(streams[j])
+        keep.extend(x[1:])
+        keep.extend(terms.values())
+        # scale 0: joins the coarse streams just before its tail kernel.  Every cross-stream edge
+        # goes through the current stream: HIP graph capture crashes (host segfault in
+        # hipStreamEndCapture) when two side streams wait on each other's events.
+        up0 = [terms[(0, j)] for j in range(1, S)]
+        mark = {}
+
+        def join():
+            for j in range(1, S):
+                main.wait_event(up_ev[j])
+            mark["coarse"] = _record(main)  # every coarse block and up term is done
+
+        for b in range(self.num_blocks - 1):
+            x[0] = self.branches[0][b](x[0])
+        x[0], csa0 = self.branches[0][self.num_blocks - 1].forward_csa(
+            x[0], up0 if csa_epilogue_ok(x[0], up0) else None, before_tail=join)
         keep.append(x[0])
-        if csa0 is None:  # no tail epilogue: the whole CSA on the current stream, after a join
-            main.wait_stream(side)
-            return self._fuse_eval(x, {}, terms)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            return self._fuse_eval(x, {0: csa0}, terms)
+        if "coarse" not in mark:  # the tail kernel did not take the block
+            join()
+        b0_ev = _record(main)
+        out = [None] * nout
+        if csa0 is None:  # no tail epilogue: branch 0's sum on the current stream
+            out[0] = ops.csa_sum([x[0]] + [t.contiguous() for t in up0], act="leaky")
+        else:
+            out[0] = csa0
+        # coarse branches: the down terms from the coarse scales (concurrent with the scale-0
+        # tail), then the one from scale 0, then the sum, on the branch's stream
+        for i in range(1, nout):
+            st = streams[i]
+            with torch.cuda.stream(st):
+                st.wait_event(mark["coarse"])
+                for j in range(1, i):
+                    terms[(i, j)] = self._down(x, i, j)
+                st.wait_event(b0_ev)
+                terms[(i, 0)] = self._down(x, i, 0)
+                out[i] = ops.csa_sum([(x[i] if i == j else terms[(i, j)]).contiguous()
+                                      for j in range(S)], act="leaky")
+            keep.append(out[i])
+        return out
 
     def _fuse_eval(self, x, done=None, terms_cache=None):
         """Eval CSA: each exchange conv (+BN folded, +LeakyReLU inside strided chains) is one HIP
@@ -179,14 +246,15 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
             x_fused.append(ops.csa_sum([t.contiguous() for t in terms], act="leaky"))
         return x_fused
 
-    def forward(self, x, side=None, keep=None):
-        """aggregation.py:375-402.  side / keep: the concurrent-scale schedule of
+    def forward(self, x, streams=None, keep=None):
+        """aggregation.py:375-402.  streams / keep: the concurrent-scale schedule of
         AdaptiveAggregation (eval only, see _forward_eval)."""
         assert len(self.branches) == len(x)
         if self.num_scales > 1 and use_fused(self, x[0]) and getattr(self, "aanet_fuse_csa", True):
-            return self._forward_eval(x, side, keep)
-        if side is not None:  # reference op sequence: one stream
-            torch.cuda.current_stream(x[0].device).wait_stream(side)
+            return self._forward_eval(x, streams, keep)
+        if streams is not None:  # reference op sequence: one stream
+            for st in streams[1:]:
+                streams[0].wait_stream(st)
         for i in range(len(self.branches)):
             branch = self.branches[i]
             for j in range(self.num_blocks):
@@ -253,17 +321,22 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
         """aggregation.py:452-464 (final 1x1 conv with bias on the HIP conv engine in eval)."""
         assert isinstance(cost_volume, list)
         fused = use_fused(self, cost_volume[0])
-        side = None
+        streams = None
         if fused and cost_volume[0].is_cuda and self.num_scales > 1 and concurrent_scales():
-            side = side_stream(cost_volume[0].device)
-            main = torch.cuda.current_stream(cost_volume[0].device)
-            side.wait_stream(main)  # the cost volumes are written on the current stream
+            dev = cost_volume[0].device
+            main = torch.cuda.current_stream(dev)
+            ss = side_streams(dev, num_side_streams(self.num_scales))
+            # scale i >= 1 on side stream (i - 1) mod n
+            streams = [main] + [ss[(i - 1) % len(ss)] for i in range(1, self.num_scales)]
+            for st in ss:
+                st.wait_stream(main)  # the cost volumes are written on the current stream
             keep = list(cost_volume)
         for i in range(self.num_fusions):
             fusion = self.fusions[i]
-            cost_volume = fusion(cost_volume, side, keep) if side is not None else fusion(cost_volume)
-        if side is not None:
-            main.wait_stream(side)
+            cost_volume = fusion(cost_volume, streams, keep) if streams is not None else fusion(cost_volume)
+        if streams is not None:
+            for st in ss:
+                main.wait_stream(st)
             del keep
         out = []  # 1/3, 1/6, 1/12
         for i in range(len(self.final_conv)):

@@ -168,11 +168,11 @@ def test_grouped_deform_conv_fused_matches_autograd_path():
 
 
 def test_two_stream_schedule_graph_replay_and_single_stream_match():
-    """The eval aggregation's two-stream schedule (coarse scales on a side stream, joined before
-    the scale-0 tail kernel) captured in a HIP graph, as bench.py runs it: replays give the eager
-    result bit for bit, at every pyramid level, and so does the one-stream schedule
-    (AANET_CONCURRENT_SCALES=0: the kernels and their inputs are the same, only their issue
-    order differs)."""
+    """The eval aggregation's concurrent-scale schedule (each coarse scale on its own side stream,
+    every cross-stream edge through the capturing stream) captured in a HIP graph, as bench.py
+    runs it: replays give the eager result bit for bit, at every pyramid level, and so does the
+    one-stream schedule (AANET_CONCURRENT_SCALES=0: the kernels and their inputs are the same,
+    only their issue order differs)."""
     import os
     from aanet_amd.nets import aggregation
     g, sd, m, left, right = _model("hotpath_d64")

@@ -6,10 +6,12 @@ from collections import defaultdict
 path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof_step/run_kernel_trace.csv"
 rows = list(csv.DictReader(open(path)))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
-# a step starts with the scale-0 correlation launch followed by the scale-1 one
-idx = [i for i, r in enumerate(rows[:-1]) if 'corr_volume_kernel<5' in r['Kernel_Name']
-       and 'corr_volume_kernel<3' in rows[i + 1]['Kernel_Name']]
-a, b = idx[-2], idx[-1]
+# a step starts with the one-launch correlation pyramid
+idx = [i for i, r in enumerate(rows) if 'corr_pyramid_kernel' in r['Kernel_Name']]
+# the bench's roofline loops repeat single kernels after the timed steps: take the last pair of
+# pyramid launches with a whole step between them
+pairs = [(i, j) for i, j in zip(idx[:-1], idx[1:]) if j - i > 50]
+a, b = pairs[-1]
 seg = rows[a:b]
 t0 = int(seg[0]['Start_Timestamp'])
 t1 = int(rows[b]['Start_Timestamp'])
@@ -22,6 +24,8 @@ for r in seg:
     agg[key][0] += 1
     agg[key][1] += d
     if '-v' in sys.argv:
-        print(f"  {d:8.1f} us  {key}  vgpr {r['VGPR_Count']} lds {r['LDS_Block_Size']}")
+        q = r.get('Stream_Id', r.get('Queue_Id', '?'))
+        st = (int(r['Start_Timestamp']) - t0) / 1e3
+        print(f"  {st:8.1f} {d:8.1f} us  q{q}  {key}  vgpr {r['VGPR_Count']} lds {r['LDS_Block_Size']}")
 for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
     print(f"{t / 1e3:8.3f} ms {c:4d}  {k}")
