@@ -44,6 +44,8 @@ _SIGNATURES = {
     "aanet_mdcn_pw_f32": [_P, _P, _L, _P, _L, _I, _F, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _P]
     + [_I] * 11 + [_P, _I, _P],
     "aanet_csa_sum_f32": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P],
+    "aanet_conv3x3s2_pack_f32": [_P, _I, _I, _P, _P],
+    "aanet_conv3x3s2_f32": [_P, _P, _P] + [_I] * 6 + [_P, _I, _P, _I, _P],
     "aanet_mdcn_im2col_f32": [_P, _P, _P, _P] + [_I] * 9 + [_P],
     "aanet_mdcn_sample_index": [_P, _P, _P, _P] + [_I] * 9 + [_P],
 }
@@ -79,6 +81,8 @@ def lib():
         L.aanet_version.restype = _I
         L.aanet_conv_weight_pack_split_bytes.argtypes = [_I] * 5
         L.aanet_conv_weight_pack_split_bytes.restype = _L
+        L.aanet_conv3x3s2_pack_bytes.argtypes = [_I, _I]
+        L.aanet_conv3x3s2_pack_bytes.restype = ctypes.c_size_t
         _lib = L
     return _lib
 
@@ -86,7 +90,7 @@ def lib():
 def exported_symbols():
     return (["aanet_version", "aanet_status_string", "aanet_mdcn_bwd_det_workspace_size",
              "aanet_mdcn_bwd_ws_workspace_size", "aanet_conv2d_wgrad_workspace_size",
-             "aanet_conv_weight_pack_split_bytes"] + list(_SIGNATURES))
+             "aanet_conv_weight_pack_split_bytes", "aanet_conv3x3s2_pack_bytes"] + list(_SIGNATURES))
 
 
 def call(name, *args):

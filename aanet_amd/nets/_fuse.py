@@ -4,6 +4,8 @@ into its weights/bias (cached per parameter version), the activation and the bot
 residual add in its epilogue.  Training mode never uses these: modules then run the reference
 op sequence with autograd.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -35,7 +37,7 @@ def clear_fold_caches(module):
     """Drop every folded-weight / BN-affine cache in `module`'s subtree (called on each
     train()/eval() switch of the drop-in modules, see FoldCacheMixin)."""
     for m in module.modules():
-        for attr in ("_aanet_fold", "_aanet_affine"):
+        for attr in ("_aanet_fold", "_aanet_affine", "_aanet_s2pack"):
             if attr in m.__dict__:
                 del m.__dict__[attr]
 
@@ -75,6 +77,34 @@ def folded(conv, bn):
             wp = ops.pack_weight(w)
     conv._aanet_fold = (key, w, b, wp)
     return w, b, wp
+
+
+def s2_pack(owner, pairs):
+    """(pre-split fragments, bias) of the 3x3 stride-2 convs `pairs` = [(conv, bn), ...] (BN
+    folded) concatenated along the output channels, for ops.conv3x3_s2; cached on `owner`, keyed
+    by the folded weights' cache keys.  None when the shape is outside the kernel."""
+    fs = [folded(c, b) for c, b in pairs]
+    key = tuple(c._aanet_fold[0] for c, _ in pairs)
+    cache = owner.__dict__.get("_aanet_s2pack")
+    if cache is not None and cache[0] == key:
+        return cache[1]
+    with torch.no_grad():
+        w = torch.cat([f[0] for f in fs])
+        b = torch.cat([f[1] if f[1] is not None else torch.zeros(f[0].shape[0], device=w.device)
+                       for f in fs]).contiguous()
+        wsplit = ops.pack_conv3x3s2(w)
+    val = None if wsplit is None else (wsplit, b)
+    owner.__dict__["_aanet_s2pack"] = (key, val)
+    return val
+
+
+def s2_conv_ok(conv):
+    """A conv of the CSA down chains that ops.conv3x3_s2 takes (3x3, stride 2, pad 1, plain);
+    AANET_S2_KERNEL=0 keeps them on the conv engine (A/B switch)."""
+    return os.environ.get("AANET_S2_KERNEL", "1") != "0" and type(conv) is nn.Conv2d and engine_conv(conv) and _int(conv.kernel_size) == 3 and \
+        _int(conv.stride) == 2 and _int(conv.padding) == 1 and _int(conv.dilation) == 1 and \
+        conv.groups == 1 and conv.in_channels % 32 == 0 and conv.out_channels % 16 == 0 and \
+        conv.out_channels <= 96
 
 
 def bn_affine(bn):

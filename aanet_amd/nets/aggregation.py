@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from ._fuse import FoldCacheMixin, conv_bn_act, use_fused
+from ._fuse import FoldCacheMixin, conv_bn_act, s2_conv_ok, s2_pack, use_fused
 from .deform import DeformSimpleBottleneck, SimpleBottleneck
 
 
@@ -122,14 +122,49 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
         layer = self.fuse_layers[i][j]
         return conv_bn_act(x[j], layer[0], layer[1], None)
 
-    def _down(self, x, i, j):
-        """Exchange term fuse_layers[i][j] for i > j: the chain of 3x3 stride-2 convs (+BN,
-        LeakyReLU between them) from scale j down to scale i."""
-        y = x[j]
+    def _down(self, y, i, j, start=0):
+        """Exchange term fuse_layers[i][j] for i > j from y = x[j] (or, start > 0, from the output
+        of its first `start` convs): the chain of 3x3 stride-2 convs (+BN, LeakyReLU between
+        them), each on the stride-2 kernel (ops.conv3x3_s2) where it takes the shape."""
         layer = self.fuse_layers[i][j]
-        for k, seq in enumerate(layer):
-            y = conv_bn_act(y, seq[0], seq[1], None if k == len(layer) - 1 else "leaky")
+        for k in range(start, len(layer)):
+            conv, bn = layer[k][0], layer[k][1]
+            act = None if k == len(layer) - 1 else "leaky"
+            pk = s2_pack(conv, [(conv, bn)]) if s2_conv_ok(conv) else None
+            if pk is None:
+                y = conv_bn_act(y, conv, bn, act)
+            else:
+                y = ops.conv3x3_s2(y.contiguous(), pk[0], pk[1], conv.out_channels,
+                                   conv.out_channels, act)[0]
         return y
+
+    def _down0_heads(self, x0):
+        """The first convs of the down chains that start at scale 0 (branches 1 and 2 at S = 3),
+        as ONE stride-2 launch that reads x0 once: {branch i: that conv's output}, or {} when
+        the convs do not fit the kernel (then every chain runs conv by conv, _down)."""
+        nout = len(self.fuse_layers)
+        heads = list(range(1, nout))
+        if not heads or len(heads) > 2:
+            return {}
+        pairs = [(self.fuse_layers[i][0][0][0], self.fuse_layers[i][0][0][1]) for i in heads]
+        if not all(s2_conv_ok(c) for c, _ in pairs) or \
+                sum(c.out_channels for c, _ in pairs) > 96:
+            return {}
+        pk = s2_pack(self.fuse_layers[heads[0]][0], pairs)
+        if pk is None:
+            return {}
+        acts = [None if len(self.fuse_layers[i][0]) == 1 else "leaky" for i in heads]
+        co_a = pairs[0][0].out_channels
+        co = co_a + (pairs[1][0].out_channels if len(pairs) > 1 else 0)
+        ya, yb = ops.conv3x3_s2(x0.contiguous(), pk[0], pk[1], co, co_a, acts[0],
+                                acts[1] if len(acts) > 1 else None)
+        return {heads[0]: ya, **({heads[1]: yb} if len(heads) > 1 else {})}
+
+    def _term_down0(self, x, i, heads):
+        """Exchange term (i, 0) given the head outputs of _down0_heads."""
+        if i in heads:
+            return self._down(heads[i], i, 0, start=1)
+        return self._down(x[0], i, 0)
 
     def _forward_eval(self, x, streams=None, keep=None):
         """Eval ISA + CSA.  The coarser scales run first, so that their exchange terms for output
@@ -195,6 +230,8 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
         keep.append(x[0])
         if "coarse" not in mark:  # the tail kernel did not take the block
             join()
+        heads = self._down0_heads(x[0])  # on the current stream: both branches need them
+        keep.extend(heads.values())
         b0_ev = _record(main)
         out = [None] * nout
         if csa0 is None:  # no tail epilogue: branch 0's sum on the current stream
@@ -208,9 +245,9 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
             with torch.cuda.stream(st):
                 st.wait_event(mark["coarse"])
                 for j in range(1, i):
-                    terms[(i, j)] = self._down(x, i, j)
+                    terms[(i, j)] = self._down(x[j], i, j)
                 st.wait_event(b0_ev)
-                terms[(i, 0)] = self._down(x, i, 0)
+                terms[(i, 0)] = self._term_down0(x, i, heads)
                 out[i] = ops.csa_sum([(x[i] if i == j else terms[(i, j)]).contiguous()
                                       for j in range(S)], act="leaky")
             keep.append(out[i])
@@ -218,12 +255,14 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
 
     def _fuse_eval(self, x, done=None, terms_cache=None):
         """Eval CSA: each exchange conv (+BN folded, +LeakyReLU inside strided chains) is one HIP
-        conv kernel at its own resolution; the resize + sum + LeakyReLU of every output branch is
+        conv kernel at its own resolution (the first convs of the down chains from scale 0 as one
+        stride-2 launch, _down0_heads); the resize + sum + LeakyReLU of every output branch is
         one aanet_csa_sum_f32 kernel (same term order as aggregation.py:388-400).  done: output
         branches already summed (by a tail-kernel epilogue); terms_cache: exchange terms already
         computed, keyed (i, j)."""
         done = done or {}
         terms_cache = terms_cache or {}
+        heads = self._down0_heads(x[0]) if any(i not in done for i in range(1, len(self.fuse_layers))) else {}
         x_fused = []
         for i in range(len(self.fuse_layers)):
             if i in done:
@@ -238,11 +277,10 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
                     terms.append(terms_cache[(i, j)])
                 elif i < j:
                     terms.append(conv_bn_act(x[j], layer[0], layer[1], None))
+                elif j == 0:
+                    terms.append(self._term_down0(x, i, heads))
                 else:
-                    y = x[j]
-                    for k, seq in enumerate(layer):
-                        y = conv_bn_act(y, seq[0], seq[1], None if k == len(layer) - 1 else "leaky")
-                    terms.append(y)
+                    terms.append(self._down(x[j], i, j))
             x_fused.append(ops.csa_sum([t.contiguous() for t in terms], act="leaky"))
         return x_fused
 

@@ -387,6 +387,34 @@ def mdcn_pw(x, offset_mask, weight, packed_weight, bias, post_scale, post_shift,
     return out if desc is None else (out, csa_out)
 
 
+def pack_conv3x3s2(weight):
+    """Pre-split A fragments of a [co][c][3][3] weight for conv3x3_s2 (aanet_conv3x3s2_pack_f32;
+    co % 16 == 0, co <= 96, c % 32 == 0), or None when the shape is outside the kernel."""
+    co, c, kh, kw = weight.shape
+    if (kh, kw) != (3, 3) or co % 16 or co > 96 or c % 32 or not weight.is_cuda:
+        return None
+    nbytes = _lib.lib().aanet_conv3x3s2_pack_bytes(co, c)
+    out = torch.empty(nbytes // 2, device=weight.device, dtype=torch.int16)
+    w = weight.contiguous().float()
+    call("aanet_conv3x3s2_pack_f32", ptr(w), co, c, ptr(out), stream_of(w))
+    return out
+
+
+def conv3x3_s2(x, wsplit, bias, co, co_a, act_a=None, act_b=None):
+    """3x3 stride-2 pad-1 conv (BN folded) with its output channels split over two outputs:
+    [0, co_a) -> out_a (act_a), [co_a, co) -> out_b (act_b); returns (out_a, out_b), either None
+    when empty.  The CSA down exchange convs that share an input run as one launch
+    (aanet_conv3x3s2_f32, nets/aggregation.py:362-371)."""
+    require_gpu(x, bias)
+    N, C, H, W = x.shape
+    Ho, Wo = (H + 1) // 2, (W + 1) // 2
+    out_a = torch.empty((N, co_a, Ho, Wo), device=x.device, dtype=x.dtype) if co_a > 0 else None
+    out_b = torch.empty((N, co - co_a, Ho, Wo), device=x.device, dtype=x.dtype) if co_a < co else None
+    call("aanet_conv3x3s2_f32", ptr(x), ptr(wsplit), ptr(bias), N, C, H, W, co, co_a, ptr(out_a),
+         ACT[act_a], ptr(out_b), ACT[act_b], stream_of(x))
+    return out_a, out_b
+
+
 def csa_sum(inputs, act="leaky"):
     """act(inputs[0] + resize(inputs[1]) + ...) at inputs[0]'s size (aggregation.py:387-400)."""
     require_gpu(*inputs)

@@ -218,6 +218,22 @@ int aanet_csa_sum_f32(float *out, int n, int c, int h, int w, int num_inputs,
                       const float *const *inputs, const int *in_h, const int *in_w, int act,
                       aanet_stream_t stream);
 
+/* The CSA down exchange convs (nets/aggregation.py:362-371 in eval: 3x3, stride 2, pad 1, BN
+ * folded into weight/bias), several of which may share one input: the output channels
+ * [0, co_a) go to out_a ([n][co_a][ho][wo], activation act_a) and [co_a, co) to out_b
+ * ([n][co - co_a][ho][wo], act_b), ho = (h + 1) / 2, wo = (w + 1) / 2.  At C2 scale 0 the
+ * branch-1 conv (64 -> 32) and the first conv of the branch-2 chain (64 -> 64, LeakyReLU) run
+ * as one co = 96 launch that reads the scale-0 block output once.  x is NCHW, c % 32 == 0,
+ * co % 16 == 0, co <= 96 (AANET_EUNSUPPORTED otherwise); wsplit: aanet_conv3x3s2_pack_f32 of the
+ * [co][c][3][3] weight into aanet_conv3x3s2_pack_bytes(co, c) device bytes.  Split-bf16
+ * contraction (fp32-accurate, see AANET_EXACT_F32 above for the arithmetic).  act: 0 none,
+ * 1 ReLU, 2 LeakyReLU(0.2). */
+size_t aanet_conv3x3s2_pack_bytes(int co, int c);
+int aanet_conv3x3s2_pack_f32(const float *w, int co, int c, void *wsplit, aanet_stream_t stream);
+int aanet_conv3x3s2_f32(const float *x, const void *wsplit, const float *bias, int n, int c, int h,
+                        int w, int co, int co_a, float *out_a, int act_a, float *out_b, int act_b,
+                        aanet_stream_t stream);
+
 /* Backward of F.interpolate(x, size=(out_h, out_w), mode='bilinear', align_corners=False)
  * (aggregation.py:395-396 in training; the loss's upsampling, model.py:115-117):
  * grad_in [planes, in_h, in_w] is OVERWRITTEN with the gather-form sum over grad_out

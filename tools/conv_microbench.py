@@ -33,7 +33,24 @@ fr = torch.randn(B, 128, H, W, device=dev, generator=g)
 vol64 = torch.randn(B, 64, H, W, device=dev, generator=g)
 f5l = torch.randn(4, 32, 96, 312, device=dev, generator=g)
 f5r = torch.randn(4, 32, 96, 312, device=dev, generator=g)
+x1 = torch.randn(B, 64, H // 2, W // 2, device=dev, generator=g)    # scale 1, 64 ch (branch-2 chain)
+x1b = torch.randn(B, 32, H // 2, W // 2, device=dev, generator=g)   # scale 1, 32 ch (block output)
+w96 = torch.randn(96, C, 3, 3, device=dev, generator=g) * 0.04
+b96 = torch.randn(96, device=dev, generator=g)
+w16, w16b = w3[:16].contiguous(), w3[:16, :32].contiguous()
+ws96, ws16, ws16b = ops.pack_conv3x3s2(w96), ops.pack_conv3x3s2(w16), ops.pack_conv3x3s2(w16b)
+p16, p16b = ops.pack_weight_split(w16), ops.pack_weight_split(w16b)
+b16 = b[:16].contiguous()
 cases = {
+    # CSA down convs: the merged scale-0 heads (64 -> 32 + 64) and the narrow 64/32 -> 16 convs
+    "s2_heads96": (lambda: ops.conv3x3_s2(x, ws96, b96, 96, 32, None, "leaky"),
+                   2 * B * (H // 2) * (W // 2) * 96 * C * 9),
+    "s2_64to16": (lambda: ops.conv3x3_s2(x1, ws16, b16, 16, 16), 2 * B * (H // 4) * (W // 4) * 16 * 64 * 9),
+    "s2_64to16_engine": (lambda: ops.conv2d_fused(x1, w16, b16, 2, 1, 1, 1, packed_weight=p16),
+                         2 * B * (H // 4) * (W // 4) * 16 * 64 * 9),
+    "s2_32to16": (lambda: ops.conv3x3_s2(x1b, ws16b, b16, 16, 16), 2 * B * (H // 4) * (W // 4) * 16 * 32 * 9),
+    "s2_32to16_engine": (lambda: ops.conv2d_fused(x1b, w16b, b16, 2, 1, 1, 1, packed_weight=p16b),
+                         2 * B * (H // 4) * (W // 4) * 16 * 32 * 9),
     "conv1x1": (lambda: ops.conv2d_fused(x, w1, b, act="relu", packed_weight=p1), 2 * B * H * W * C * C),
     "conv1x1_res": (lambda: ops.conv2d_fused(x, w1, b, act="relu", residual=res, packed_weight=p1),
                     2 * B * H * W * C * C),
