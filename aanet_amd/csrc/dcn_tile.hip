@@ -290,18 +290,25 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   // ---- main loop: 2 deformable groups x 9 taps = 18 chunks, one barrier per chunk --------------
   // L2 warm-up loads (one dword per 128-B line, results unused): the next group's window lines
   // during group 0, the epilogue's identity rows during group 1, so those loads hit L2.
+  // Order inside a chunk: the ds_bpermute hand-off of the sampling state comes BEFORE any vector
+  // memory op of the chunk.  The compiler cannot tell a ds_bpermute from an LDS access that may
+  // alias the outstanding LDS-DMA of the next tap's weights, so it puts s_waitcnt vmcnt(0) in
+  // front of it; issued after the DMA, that wait exposed the DMA's whole L2 latency every chunk.
   float pf_win = 0.f, pf_res = 0.f;
   auto step = [&](int c, const char *cur, char *nxt) {
     const int g = c >= K ? 1 : 0, k = c - K * g, t0 = k & ~3;
+    TapState s;
     if (k == 0) {  // group start: its window (loaded in the chunk before) and pass-0 states
       if (g == 1) asm volatile("" ::"v"(pf_win));
       store_window();
       compute_pass(0);
-      load_pass(g, 4);
+      s = get_state(k, t0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of A(c) landed
       __syncthreads();
-    } else if (k == 4 || k == 8) {
-      compute_pass(k);
+      load_pass(g, 4);
+    } else {
+      if (k == 4 || k == 8) compute_pass(k);
+      s = get_state(k, t0);
       if (k == 4) load_pass(g, 8);
     }
     if (c + 1 < 2 * K) issue_a(c + 1, nxt);
@@ -315,7 +322,6 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       const int yy = min(y0 + (tid & 7), H - 1), co2 = min(tid >> 3, a.Co2 - 1);
       pf_res = a.residual[((long)(n * a.Co2 + co2) * H + yy) * W + x0];
     }
-    const TapState s = get_state(k, t0);
     tap(g, k, cur, s);
     if (c == K - 1) {  // the next group's window and first offsets, behind the MFMAs
       __builtin_amdgcn_sched_barrier(0);

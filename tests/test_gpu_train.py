@@ -161,4 +161,7 @@ def test_graph_step_matches_eager_steps(det):
     assert lg[-1] < lg[0]
     num = sum(float((a - b).double().norm() ** 2) for a, b in zip(pe, pg)) ** 0.5
     den = sum(float(a.double().norm() ** 2) for a in pe) ** 0.5
-    assert num <= 1e-5 * den, (num, den)
+    # Non-deterministic mode sums gradients with float atomics, so two eager runs already differ in
+    # the last bits; Adam's m / sqrt(v) turns that into lr-sized moves of near-zero-gradient
+    # elements (measured 1.5e-5 relative after 3 steps).  Deterministic mode must agree tightly.
+    assert num <= (1e-5 if det else 1e-4) * den, (num, den)
