@@ -39,7 +39,6 @@ constexpr int NT = 512;          // 8 waves, one tile row each
 constexpr int TR = 8, TC = 16;   // tile: 8 rows x 16 columns of output pixels
 constexpr int RW = 2;            // window margin beyond the taps: offsets in [-RW, RW) stay inside
 constexpr int K = 9;             // 3x3 taps
-constexpr int ABUF = 12 * 1024;  // one tap's A fragments: 4 co blocks x 3 pieces x 64 lanes x 16 B
 constexpr int OP = TR * TC + 4;  // epilogue tile pitch (floats)
 
 // ---- split-bf16 contraction (same scheme as mdcn.hip split3 / mfma_split6) -------------------
@@ -117,14 +116,23 @@ __device__ __forceinline__ TapState tap_state(float oh, float ow, float ml, int 
   return s;
 }
 
-template <int DIL>
+// CG = channels per deformable group (two groups): 32 (scale 0: C = 64) or 16 (scale 1: C = 32).
+// A chunk is one tap of a 32-channel K slice ("phase"): with CG = 32 a phase is one group, with
+// CG = 16 it holds both groups (lane groups kr = 0, 1 carry group 0's channels, kr = 2, 3 group 1's).
+template <int DIL, int CG>
 __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
+  constexpr int CT = 2 * CG;             // channels = Co = Co2
+  constexpr int NPH = CT / 32;           // phases
+  constexpr int NCH = NPH * K;           // chunks
+  constexpr int NCO = CT / 16;           // 16-row co blocks
+  constexpr int ABUF = NCO * 3 * 1024;   // one chunk's A fragments: NCO blocks x 3 pieces x 64 lanes x 16 B
+  constexpr int TPP = CG == 32 ? 4 : 2;  // taps per sampling pass (x groups per pass = 4 lane groups)
   constexpr int MG = DIL + RW;                     // window margin around the tile
   constexpr int WR = TR + 2 * MG, WC = TC + 2 * MG;
   constexpr int NPOS = (WR * WC + 63) / 64 * 64;   // positions per quad plane (multiple of 64)
   constexpr int NWI = NPOS / 64;                   // window quads staged per thread (8*NPOS/512)
   constexpr int WIN = 8 * NPOS * 16;               // window bytes: [8 channel quads][NPOS][16 B]
-  static_assert(WIN >= 64 * OP * 4, "epilogue tile must fit the window");
+  static_assert(WIN >= CT * OP * 4, "epilogue tile must fit the window");
   // Three LDS objects: the compiler orders a ds_read after an outstanding LDS-DMA only when they
   // may alias, so the DMA of tap c+1's weights into one A slot never holds reads of the window or
   // of the other slot.
@@ -183,26 +191,29 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
     if (a.dbg & 64) return;
     const int g = c / K, k = c - K * (c / K);
     const char *src = wsp + (long)((k * ncc + g) * 12) * 1024 + lane * 16;
-    for (int pc = wave; pc < 12; pc += 8)
+    for (int pc = wave; pc < 3 * NCO; pc += 8)
       __builtin_amdgcn_global_load_lds((const void *)(src + pc * 1024), (lds_void *)(dst + pc * 1024), 16, 0, 0);
   };
 
-  // ---- sampling state: lane group kr computes tap t0 + kr of this lane's pixel -----------------
+  // ---- sampling state: lane group kr computes (tap, group) pt(kr) of this lane's pixel: tap
+  // t0 + kr of the phase's group (CG = 32), or tap t0 + (kr & 1) of group kr >> 1 (CG = 16)
+  const int pt = CG == 32 ? kr : (kr & 1);
+  const int lgrp = CG == 32 ? 0 : (kr >> 1);  // this lane's group within the phase
   float poh = 0.f, pow_ = 0.f, pml = 0.f;  // prefetched offsets / mask of the next pass
   auto load_pass = [&](int g, int t0) {
-    const int t = min(t0 + kr, K - 1);
-    const int oplane = (g * 2 * K + 2 * t) * P * 4, mplane = (g * K + t) * P * 4;
+    const int t = min(t0 + pt, K - 1), gr = CG == 32 ? g : (kr >> 1);
+    const int oplane = (gr * 2 * K + 2 * t) * P * 4, mplane = (gr * K + t) * P * 4;
     poh = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, p4 + oplane, 0, 0));
     pow_ = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, p4 + oplane + P * 4, 0, 0));
     pml = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mskr, p4 + mplane, 0, 0));
   };
   TapState ps;  // this lane's state for tap t0 + kr
   auto compute_pass = [&](int t0) {
-    ps = tap_state<DIL, WR, WC>(poh, pow_, pml, py, px, pv, min(t0 + kr, K - 1), H, W, wy0, wx0,
+    ps = tap_state<DIL, WR, WC>(poh, pow_, pml, py, px, pv, min(t0 + pt, K - 1), H, W, wy0, wx0,
                                 a.mask_logits, a.mask_scale);
   };
   auto get_state = [&](int k, int t0) -> TapState {
-    const int src = ((((k - t0) << 4) | jj)) << 2;
+    const int src = (((k - t0 + 2 * lgrp) << 4) | jj) << 2;
     TapState s;
     s.pos = __builtin_amdgcn_ds_bpermute(src, ps.pos);
     s.w0 = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, ps.w0)));
@@ -212,9 +223,9 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
     return s;
   };
 
-  f32x4 acc[4];
+  f32x4 acc[NCO];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int m = 0; m < NCO; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // one tap of one group: corners -> blend -> split -> 24 MFMAs
   auto tap = [&](int g, int k, const char *sAc, const TapState &s) {
@@ -243,7 +254,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       if (s.pos < 0) {
         // global gather of this lane's corners (blended here, so no load is pending at the join)
 #pragma clang fp contract(off)
-        const int oplane = (g * 2 * K + 2 * k) * P * 4;
+        const int oplane = ((CG == 32 ? g : lgrp) * 2 * K + 2 * k) * P * 4;
         const float oh = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, p4 + oplane, 0, 0));
         const float ow = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, p4 + oplane + P * 4, 0, 0));
         const int i = k / 3, j = k - 3 * (k / 3);
@@ -279,7 +290,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
     split8(v, B);
     const char *ab = sAc + lane * 16;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+    for (int m = 0; m < NCO; ++m) {
       bf16x8 A[3];
 #pragma unroll
       for (int pc = 0; pc < 3; ++pc) A[pc] = *reinterpret_cast<const bf16x8 *>(ab + (m * 3 + pc) * 1024);
@@ -287,7 +298,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
     }
   };
 
-  // ---- main loop: 2 deformable groups x 9 taps = 18 chunks, one barrier per chunk --------------
+  // ---- main loop: NPH phases x 9 taps (18 or 9 chunks), one barrier per chunk ----------------
   // L2 warm-up loads (one dword per 128-B line, results unused): the next group's window lines
   // during group 0, the epilogue's identity rows during group 1, so those loads hit L2.
   // Order inside a chunk: the ds_bpermute hand-off of the sampling state comes BEFORE any vector
@@ -296,7 +307,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   // front of it; issued after the DMA, that wait exposed the DMA's whole L2 latency every chunk.
   float pf_win = 0.f, pf_res = 0.f;
   auto step = [&](int c, const char *cur, char *nxt) {
-    const int g = c >= K ? 1 : 0, k = c - K * g, t0 = k & ~3;
+    const int g = c >= K ? 1 : 0, k = c - K * g, t0 = k - k % TPP;
     TapState s;
     if (k == 0) {  // group start: its window (loaded in the chunk before) and pass-0 states
       if (g == 1) asm volatile("" ::"v"(pf_win));
@@ -305,25 +316,25 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       s = get_state(k, t0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of A(c) landed
       __syncthreads();
-      load_pass(g, 4);
+      load_pass(g, TPP);
     } else {
-      if (k == 4 || k == 8) compute_pass(k);
+      if (k == t0) compute_pass(k);
       s = get_state(k, t0);
-      if (k == 4) load_pass(g, 8);
+      if (k == t0 && k + TPP < K) load_pass(g, k + TPP);
     }
-    if (c + 1 < 2 * K) issue_a(c + 1, nxt);
-    if (c == 3 && tid < WR * WC) {
+    if (c + 1 < NCH) issue_a(c + 1, nxt);
+    if (NPH == 2 && c == 3 && tid < WR * WC) {
       const int wy = wy0 + tid / WC, wx = wx0 + tid % WC;
       const bool ok = wy >= 0 && wy < H && wx >= 0 && wx < W;
       pf_win = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
           xr, ok ? (wy * W + wx) * C * 4 : img_bytes, 128, 0));
     }
-    if (c == 12 && a.residual) {
+    if (c == NCH - 6 && a.residual) {
       const int yy = min(y0 + (tid & 7), H - 1), co2 = min(tid >> 3, a.Co2 - 1);
       pf_res = a.residual[((long)(n * a.Co2 + co2) * H + yy) * W + x0];
     }
     tap(g, k, cur, s);
-    if (c == K - 1) {  // the next group's window and first offsets, behind the MFMAs
+    if (NPH == 2 && c == K - 1) {  // the next phase's window and first offsets, behind the MFMAs
       __builtin_amdgcn_sched_barrier(0);
       load_window(1);
       load_pass(1, 0);
@@ -335,10 +346,11 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   issue_a(0, sA0);
   load_pass(0, 0);
 #pragma unroll 1
-  for (int c = 0; c < 2 * K; c += 2) {
+  for (int c = 0; c < NCH - 1; c += 2) {
     step(c, sA0, sA1);
     step(c + 1, sA1, sA0);
   }
+  if constexpr (NCH % 2) step(NCH - 1, sA0, sA1);
   asm volatile("" ::"v"(pf_res));
 
   // ---- tail: BN2 + act -> conv3 (pointwise, split-bf16) ----------------------------------------
@@ -348,17 +360,18 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
     const char *src = reinterpret_cast<const char *>(a.tail_wsplit) + lane * 16;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-      const int pc = wave + 8 * r;
-      char *dst = pc < 12 ? sA0 + pc * 1024 : sA1 + (pc - 12) * 1024;
+      const int pc = wave + 8 * r;  // NPH K chunks x NCO blocks x 3 pieces
+      if (pc >= 3 * NCO * NPH) break;
+      char *dst = pc < 3 * NCO ? sA0 + pc * 1024 : sA1 + (pc - 3 * NCO) * 1024;
       __builtin_amdgcn_global_load_lds((const void *)(src + pc * 1024), (lds_void *)dst, 16, 0, 0);
     }
   }
   // The accumulator of co block m holds channels 16m + 4kr + r of pixel jj: for the conv3 K chunk
   // h2 (channels 32h2..32h2+31) lane group kr supplies {32h2 + 4kr + r, 32h2 + 16 + 4kr + r}, a
   // permutation of the chunk's K index that the A fragments below are read in.
-  bf16x8 B2[2][3];
+  bf16x8 B2[NPH][3];
 #pragma unroll
-  for (int h2 = 0; h2 < 2; ++h2) {
+  for (int h2 = 0; h2 < NPH; ++h2) {
     float v[8];
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -371,9 +384,9 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
     }
     split8(v, B2[h2]);
   }
-  f32x4 acc2[4];
+  f32x4 acc2[NCO];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) acc2[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int m = 0; m < NCO; ++m) acc2[m] = f32x4{0.f, 0.f, 0.f, 0.f};
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed ...
   __syncthreads();                                   // ... and every other wave's
   {
@@ -382,9 +395,9 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
     // 8 (kr & 1); channels 32h2 + 16 + 4kr + 0..3 the same 32 lanes further.
     const int tl = (((kr >> 1) << 4) | jj) * 16 + 8 * (kr & 1);
 #pragma unroll
-    for (int m2 = 0; m2 < 4; ++m2)
+    for (int m2 = 0; m2 < NCO; ++m2)
 #pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
+      for (int h2 = 0; h2 < NPH; ++h2) {
         bf16x8 A[3];
 #pragma unroll
         for (int pc = 0; pc < 3; ++pc) {
@@ -399,11 +412,11 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   // ---- epilogue: tile -> LDS [co2][px] -> 16-byte row quads (+ bias, identity, act, CSA) ------
   float *sO = reinterpret_cast<float *>(sWin);
 #pragma unroll
-  for (int m2 = 0; m2 < 4; ++m2)
+  for (int m2 = 0; m2 < NCO; ++m2)
 #pragma unroll
     for (int r = 0; r < 4; ++r) sO[(16 * m2 + 4 * kr + r) * OP + wave * 16 + jj] = acc2[m2][r];
   __syncthreads();
-  constexpr int EPT = 64 * TR * (TC / 4) / NT;  // items (4 pixels x 1 channel) per thread
+  constexpr int EPT = CT * TR * (TC / 4) / NT;  // items (4 pixels x 1 channel) per thread
   const int Co2 = a.Co2;
   // every global load of the thread's items (identity, bias, the CSA terms' source segments) is
   // issued before the first use: the item loop would otherwise pay one L2/HBM round trip per
@@ -483,7 +496,7 @@ int window_enabled() {
 
 int dcn_tile_supported(int c, int co, int co2, int kh, int kw, int stride, int pad, int dil,
                        int dg, int groups, int w) {
-  return window_enabled() && c == 64 && co == 64 && co2 == 64 && kh == 3 && kw == 3 &&
+  return window_enabled() && (c == 64 || c == 32) && co == c && co2 == c && kh == 3 && kw == 3 &&
          stride == 1 && pad == dil && dil == 2 && dg == 2 && groups == 1 && w % 4 == 0;
 }
 
@@ -508,6 +521,9 @@ int dcn_tile_launch(const DcnTileArgs &a, hipStream_t stream) {
   static const int dbg = [] { const char *e = getenv("AANET_DCN_DBG"); return e ? atoi(e) : 0; }();
   DcnTileArgs b = a;
   b.dbg = dbg;
-  hipLaunchKernelGGL(dcn_tile_kernel<2>, dim3((unsigned)(a.N * tiles)), dim3(NT), 0, stream, b);
+  if (a.C == 64)
+    hipLaunchKernelGGL((dcn_tile_kernel<2, 32>), dim3((unsigned)(a.N * tiles)), dim3(NT), 0, stream, b);
+  else
+    hipLaunchKernelGGL((dcn_tile_kernel<2, 16>), dim3((unsigned)(a.N * tiles)), dim3(NT), 0, stream, b);
   return aanet_launch_status();
 }

@@ -1,6 +1,7 @@
 """The LDS-window deformable bottleneck tail (aanet_amd/csrc/dcn_tile.hip), which aanet_mdcn_pw_f32
 takes for the aggregation's scale-0 DeformSimpleBottleneck (64 channels, two 32-channel
-deformable groups, 3x3, dilation 2, NHWC conv1 output, split weights).  Checked against the CPU
+deformable groups) and scale-1 one (32 channels, two 16-channel groups), 3x3, dilation 2, NHWC
+conv1 output, split weights.  Checked against the CPU
 oracle (restated kernel.cu:467-767 + torch-CPU conv3) and against the generic engine it replaces
 (AANET_CONV_GENERIC_DCN), including samples that leave the window (global-gather fallback),
 ragged tiles and the CSA epilogue."""
@@ -15,9 +16,9 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _case(N, H, W, off_scale, seed, bias=False):
+def _case(N, H, W, off_scale, seed, bias=False, C=64):
     rng = np.random.default_rng(seed)
-    C, dg = 64, 2
+    dg = 2
     x = np.maximum(rng.standard_normal((N, C, H, W)), 0).astype(np.float32)
     om = rng.standard_normal((N, dg * 27, H, W)).astype(np.float32)
     om[:, :dg * 18] *= off_scale
@@ -51,14 +52,15 @@ def _run(x, om, w2, b2, sc, sh, w3, b3, ident, generic=False, csa_up=None):
                        1, 2, 2, 2, 2.0, csa_up=csa_up, generic_dcn=generic)
 
 
+@pytest.mark.parametrize("C", [64, 32])
 @pytest.mark.parametrize("N,H,W,off_scale,bias", [
     (2, 16, 48, 1.0, False),   # whole tiles, offsets mostly inside the window
     (2, 16, 48, 4.0, False),   # most samples leave the window: global-gather fallback
     (1, 13, 36, 1.5, True),    # ragged tiles (13 % 8, 36 % 16), DCN bias
     (1, 8, 4, 0.7, False),     # one tile narrower than the window's column margin
 ])
-def test_dcn_tile_vs_oracle(N, H, W, off_scale, bias):
-    args = _case(N, H, W, off_scale, seed=H * 100 + W, bias=bias)
+def test_dcn_tile_vs_oracle(N, H, W, off_scale, bias, C):
+    args = _case(N, H, W, off_scale, seed=H * 100 + W + C, bias=bias, C=C)
     ref = _oracle(*args)
     got = _run(*args).cpu().numpy()
     err = np.abs(got - ref).max()
@@ -78,18 +80,29 @@ def test_dcn_tile_matches_generic_engine_with_csa(off_scale):
         assert (a - b).abs().max().item() <= 2e-5 * (1 + b.abs().max().item())
 
 
-def test_dcn_tile_c2_reproducible():
-    """B=8 C2 scale 0, every CU busy: identical bits over repeated launches."""
-    args = _case(8, 128, 416, 1.0, seed=4)
+@pytest.mark.parametrize("off_scale", [0.5, 3.0])
+def test_dcn_tile_c32_matches_generic_engine(off_scale):
+    """Scale-1 shape (32 channels, two 16-channel groups, C2 64 x 208, B=2): the window kernel
+    vs the generic engine on the same split weights, fp32-rounding agreement."""
+    args = _case(2, 64, 208, off_scale, seed=3, C=32)
+    o_w, o_g = _run(*args), _run(*args, generic=True)
+    assert (o_w - o_g).abs().max().item() <= 2e-5 * (1 + o_g.abs().max().item())
+
+
+@pytest.mark.parametrize("C,H,W", [(64, 128, 416), (32, 64, 208)])
+def test_dcn_tile_c2_reproducible(C, H, W):
+    """B=8 C2 scale 0 / scale 1, every CU busy: identical bits over repeated launches."""
+    args = _case(8, H, W, 1.0, seed=4, C=C)
     ref = _run(*args).clone()
     for _ in range(4):
         assert torch.equal(_run(*args), ref)
 
 
-def test_dcn_tile_sampling_edges():
+@pytest.mark.parametrize("C", [64, 32])
+def test_dcn_tile_sampling_edges(C):
     """Offsets placing samples exactly on integer grid points, at -1 / H boundaries and far
     outside the image (zero contribution) in both deformable groups."""
-    x, om, w2, b2, sc, sh, w3, b3, ident = _case(1, 16, 32, 0.0, seed=9)
+    x, om, w2, b2, sc, sh, w3, b3, ident = _case(1, 16, 32, 0.0, seed=9, C=C)
     rng = np.random.default_rng(10)
     vals = np.array([0.0, 1.0, -1.0, 2.0, -2.0, 0.5, -0.5, 1.999, -2.001, 17.0, -40.0, 3.25],
                     dtype=np.float32)

@@ -22,7 +22,7 @@ KMAP = {"corr_volume_s0": r"corr_volume_kernel<5, 1>", "disp_regress_s0": r"disp
         "conv1x1_s0": r"pw_conv_nchw_kernel<64, 4, 1>",
         # the LDS-window deformable tail (dcn_tile.hip; the generic engine's split form was
         # conv_fwd_kernel<1, 64, 128, 1, 1, 1, 1, 1, 0, 1, 0>)
-        "mdcn_pw_s0": r"dcn_tile_kernel<2>",
+        "mdcn_pw_s0": r"dcn_tile_kernel<2, 32>",
         # MODE, CO_T, PTT, PACKED, TAIL, SCHED, FULL, LAYOUT, CFG, PREC (1: split-bf16), HALO (= dil)
         "conv3x3_pw_s0": r"conv_fwd_kernel<0, 64, 128, 1, 1, 1, 1, 1, 0, 1, 1>"}
 
