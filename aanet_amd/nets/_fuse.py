@@ -37,7 +37,7 @@ def clear_fold_caches(module):
     """Drop every folded-weight / BN-affine cache in `module`'s subtree (called on each
     train()/eval() switch of the drop-in modules, see FoldCacheMixin)."""
     for m in module.modules():
-        for attr in ("_aanet_fold", "_aanet_affine", "_aanet_s2pack"):
+        for attr in ("_aanet_fold", "_aanet_fold_dense", "_aanet_affine", "_aanet_s2pack"):
             if attr in m.__dict__:
                 del m.__dict__[attr]
 
@@ -77,6 +77,37 @@ def folded(conv, bn):
             wp = ops.pack_weight(w)
     conv._aanet_fold = (key, w, b, wp)
     return w, b, wp
+
+
+def dense_grouped_ok(conv, x):
+    """A 2-group conv whose groups are narrower than the split-bf16 engine's 32-channel K chunk
+    (the scale-1 offset_conv: 32 -> 54, two 16-channel groups) but whose full input is a multiple
+    of 32 channels: run as ONE ungrouped conv with a block-diagonal weight.  Twice the MACs, but
+    on the split-bf16 contraction instead of the exact-f32 16-channel form (C2 scale 1, B=8:
+    37 -> 29 us, tools/dense_grouped_bench.py); the
+    zero blocks add exact zeros, so only the fp32 summation order differs.  AANET_DENSE_GROUPED=0 keeps the grouped engine (A/B switch)."""
+    return conv.groups == 2 and (conv.in_channels // 2) % 32 != 0 and conv.in_channels % 32 == 0 \
+        and x.is_cuda and os.environ.get("AANET_DENSE_GROUPED", "1") != "0"
+
+
+def folded_dense(conv, bn):
+    """folded() of a grouped conv as its block-diagonal ungrouped equivalent, cached on the conv
+    under the same parameter-version key."""
+    w, b, _ = folded(conv, bn)
+    key = conv._aanet_fold[0]
+    cache = conv.__dict__.get("_aanet_fold_dense")
+    if cache is not None and cache[0] == key:
+        return cache[1], cache[2], cache[3]
+    with torch.no_grad():
+        g, co, cg = conv.groups, w.shape[0], w.shape[1]
+        wd = torch.zeros((co, cg * g) + tuple(w.shape[2:]), device=w.device, dtype=w.dtype)
+        cog = co // g
+        for i in range(g):
+            wd[i * cog:(i + 1) * cog, i * cg:(i + 1) * cg] = w[i * cog:(i + 1) * cog]
+        wd = wd.contiguous()
+        wp = ops.pack_weight_split(wd, 1)
+    conv.__dict__["_aanet_fold_dense"] = (key, wd, b, wp)
+    return wd, b, wp
 
 
 def s2_pack(owner, pairs):
@@ -127,13 +158,18 @@ def _int(v):
 def conv_bn_act(x, conv, bn=None, act=None, residual=None, out_nhwc=False):
     """act(BN(conv(x)) [+ residual]) as ONE HIP kernel (BN folded into the conv).  A channels_last
     x is read as NHWC in place; out_nhwc=True returns a channels_last (NHWC) tensor."""
-    w, b, wp = folded(conv, bn)
+    groups = conv.groups
+    if dense_grouped_ok(conv, x):
+        w, b, wp = folded_dense(conv, bn)
+        groups = 1
+    else:
+        w, b, wp = folded(conv, bn)
     for v in (conv.stride, conv.padding, conv.dilation):
         if isinstance(v, (tuple, list)) and v[0] != v[1]:
             raise NotImplementedError("asymmetric conv parameters")
     xin = x if is_nhwc(x) else x.contiguous()
     return ops.conv2d_fused(xin, w, b, _int(conv.stride), _int(conv.padding),
-                            _int(conv.dilation), conv.groups, act, residual, packed_weight=wp,
+                            _int(conv.dilation), groups, act, residual, packed_weight=wp,
                             out_nhwc=out_nhwc)
 
 
