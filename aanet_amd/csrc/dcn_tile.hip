@@ -228,7 +228,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   for (int m = 0; m < NCO; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // one tap of one group: corners -> blend -> split -> 24 MFMAs
-  auto tap = [&](int g, int k, const char *sAc, const TapState &s) {
+  auto tap = [&](int g, int k, const char *sAc, const TapState &s, bool reload) {
     f32x4 cq[4][2];  // corners TL, TR, BL, BR x channel quads 2kr, 2kr+1
     const int lpos = (s.pos < 0 || (a.dbg & 2)) ? 0 : s.pos;
     const char *base = sWin + (lpos + kr * 2 * NPOS) * 16;
@@ -288,6 +288,14 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
     }
     bf16x8 B[3];
     split8(v, B);
+    if (reload) {
+      // the next phase's window and first offsets: issued once this chunk's corners are blended
+      // (their registers free) and before its MFMAs, so the load latency overlaps the MFMA run
+      __builtin_amdgcn_sched_barrier(0);
+      load_window(1);
+      load_pass(1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     const char *ab = sAc + lane * 16;
 #pragma unroll
     for (int m = 0; m < NCO; ++m) {
@@ -333,12 +341,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       const int yy = min(y0 + (tid & 7), H - 1), co2 = min(tid >> 3, a.Co2 - 1);
       pf_res = a.residual[((long)(n * a.Co2 + co2) * H + yy) * W + x0];
     }
-    tap(g, k, cur, s);
-    if (NPH == 2 && c == K - 1) {  // the next phase's window and first offsets, behind the MFMAs
-      __builtin_amdgcn_sched_barrier(0);
-      load_window(1);
-      load_pass(1, 0);
-    }
+    tap(g, k, cur, s, NPH == 2 && c == K - 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of A(c+1) landed ...
     if (!(a.dbg & 8)) __syncthreads();                 // ... and every other wave's
   };
@@ -352,6 +355,25 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   }
   if constexpr (NCH % 2) step(NCH - 1, sA0, sA1);
   asm volatile("" ::"v"(pf_res));
+
+  // ---- epilogue items (4 pixels x 1 channel): addresses, bias and identity loads, issued before
+  // the conv3 tail so their latency overlaps its weight DMA and MFMAs
+  constexpr int EPT = CT * TR * (TC / 4) / NT;  // items per thread
+  const int Co2 = a.Co2;
+  f32x4 er[EPT];
+  float eb[EPT];
+  long eo[EPT];
+  bool eok[EPT];
+  const bool res = a.residual && !(a.dbg & 16), csa = a.csa_out && !(a.dbg & 16);
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int e = tid + NT * i, co2 = e >> 5, qi = e & 31, yy = y0 + (qi >> 2), xx = x0 + 4 * (qi & 3);
+    eok[i] = co2 < Co2 && yy < H && xx < W;
+    eo[i] = ((long)(n * Co2 + co2) * H + yy) * W + xx;
+    if (!eok[i]) continue;
+    eb[i] = a.tail_b ? a.tail_b[co2] : 0.f;
+    if (res) er[i] = *reinterpret_cast<const f32x4 *>(a.residual + eo[i]);
+  }
 
   // ---- tail: BN2 + act -> conv3 (pointwise, split-bf16) ----------------------------------------
   // conv3's A fragments (24 KB, standard fragment order) by LDS-DMA into the two A slots: K chunk
@@ -416,25 +438,15 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) sO[(16 * m2 + 4 * kr + r) * OP + wave * 16 + jj] = acc2[m2][r];
   __syncthreads();
-  constexpr int EPT = CT * TR * (TC / 4) / NT;  // items (4 pixels x 1 channel) per thread
-  const int Co2 = a.Co2;
-  // every global load of the thread's items (identity, bias, the CSA terms' source segments) is
-  // issued before the first use: the item loop would otherwise pay one L2/HBM round trip per
-  // item and term (the stores may alias the sources, so the compiler cannot hoist them)
-  f32x4 ev[EPT], er[EPT], eu[EPT][2][2];
-  float eb[EPT];
-  long eo[EPT];
-  bool eok[EPT];
-  const bool res = a.residual && !(a.dbg & 16), csa = a.csa_out && !(a.dbg & 16);
+  // every global load of the thread's items (the CSA terms' source segments; identity and bias
+  // above) is issued before the first use: the item loop would otherwise pay one L2/HBM round
+  // trip per item and term (the stores may alias the sources, so the compiler cannot hoist them)
+  f32x4 ev[EPT], eu[EPT][2][2];
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
     const int e = tid + NT * i, co2 = e >> 5, qi = e & 31, yy = y0 + (qi >> 2), xx = x0 + 4 * (qi & 3);
-    eok[i] = co2 < Co2 && yy < H && xx < W;
-    eo[i] = ((long)(n * Co2 + co2) * H + yy) * W + xx;
     ev[i] = *reinterpret_cast<const f32x4 *>(sO + co2 * OP + (qi >> 2) * 16 + 4 * (qi & 3));
     if (!eok[i]) continue;
-    eb[i] = a.tail_b ? a.tail_b[co2] : 0.f;
-    if (res) er[i] = *reinterpret_cast<const f32x4 *>(a.residual + eo[i]);
     if (csa) {
       const long plane = (long)n * Co2 + co2;
 #pragma unroll
