@@ -234,24 +234,31 @@ __global__ __launch_bounds__(NTHREADS) void corr_volume_kernel(
 }
 
 // The whole pyramid (nets/cost.py:58-76) in ONE launch: a scale-major work list (scale 0's
-// tiles first), XCD-contiguous as in the single-volume kernel; a workgroup runs the tile code
-// instantiated for its scale's band width, so the coarse scales fill the chip while scale 0's
-// last tiles drain instead of running as separate, under-filled launches.
+// tiles first); a workgroup runs the tile code instantiated for its scale's band width, so the
+// coarse scales fill the chip while scale 0's last tiles drain instead of running as separate,
+// under-filled launches.  XCD placement is balanced PER SCALE: each scale's items are padded to a
+// multiple of 8 and block b (dealt to XCD b % 8) takes item (b % 8) * per + j of its scale, so
+// every XCD owns a contiguous eighth of every scale (neighbouring x tiles share the R window in
+// that XCD's L2).  A remap contiguous over the whole list gave the last XCDs only the cheap
+// coarse tiles and the first ones only scale-0 tiles: the launch ran at the pace of the busiest.
 constexpr int MAXS = 4;
 struct CorrPyramid {
   const float *L[MAXS], *R[MAXS];
   float *out[MAXS];
   int C[MAXS], H[MAXS], W[MAXS], D[MAXS], dchunk[MAXS], ntx[MAXS], nchunks[MAXS], nj[MAXS];
-  int start[MAXS + 1];
+  int cnt[MAXS];         // work items of scale s
+  int per[MAXS];         // items of scale s per XCD: ceil(cnt / 8)
+  int mstart[MAXS + 1];  // prefix sums of per[]: grid = 8 * mstart[ns]
   int ns;
 };
 
 __global__ __launch_bounds__(NTHREADS) void corr_pyramid_kernel(CorrPyramid p) {
   __shared__ __attribute__((aligned(16))) float smem[CorrSmem<5>::BYTES / 4];
-  const int id = xcd_remap(gridDim.x, blockIdx.x);
+  const int xcd = blockIdx.x & 7, i = blockIdx.x >> 3;
   int s = 0;
-  while (s + 1 < p.ns && id >= p.start[s + 1]) ++s;
-  const int local = id - p.start[s];
+  while (s + 1 < p.ns && i >= p.mstart[s + 1]) ++s;
+  const int local = xcd * p.per[s] + (i - p.mstart[s]);
+  if (local >= p.cnt[s]) return;  // padding of scale s to a multiple of 8 (whole workgroup)
 #define AANET_CORR_CASE(J) \
   case J: corr_tile<J, 1>(p.L[s], p.R[s], p.out[s], p.C[s], p.H[s], p.W[s], p.D[s], p.dchunk[s], \
                           p.ntx[s], p.nchunks[s], local, smem); break;
@@ -528,12 +535,19 @@ extern "C" int aanet_corr_pyramid_f32(int num_scales, const float *const *left,
     p.dchunk[s] = corr_dchunk(p.nj[s]);
     p.nchunks[s] = host_div_up(d, p.dchunk[s]);
     p.ntx[s] = host_div_up(w[s], TX);
-    p.start[s] = (int)total;
-    total += (long)p.ntx[s] * p.nchunks[s] * h[s] * n;
+    const long cnt = (long)p.ntx[s] * p.nchunks[s] * h[s] * n;
+    if (cnt > 0x7fffffffL - 8) {
+      one = false;
+      break;
+    }
+    p.cnt[s] = (int)cnt;
+    p.per[s] = (int)((cnt + 7) / 8);
+    p.mstart[s] = (int)(total / 8);
+    total += 8L * p.per[s];
     if (total > 0x7fffffffL) one = false;
   }
   if (one) {
-    p.start[num_scales] = (int)total;
+    p.mstart[num_scales] = (int)(total / 8);
     hipLaunchKernelGGL(corr_pyramid_kernel, dim3((unsigned)total), dim3(NTHREADS), 0,
                        as_hip(stream), p);
     return aanet_launch_status();
