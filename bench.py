@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=8, help="stereo pairs per GPU")
     ap.add_argument("--no-graph", action="store_true", help="time eager launches, not a HIP graph")
+    ap.add_argument("--graph", action="store_true",
+                    help="time the HIP-graph replay even when eager launches probe faster")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=20)
     ap.add_argument("--features", default="randn", choices=sorted(FEATURE_KINDS),
@@ -305,9 +307,24 @@ def cpu_baseline(model, left, right):
                        "regression) + torch-CPU convs", seconds=dt)
 
 
+def _time_calls(fn, n):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n
+
+
 def timed_run(step, args, world):
     """W warmup steps, optional HIP-graph capture of one step, then exactly K timed steps between
-    barrier + synchronize pairs.  -> (last output, elapsed seconds, graph or None)."""
+    barrier + synchronize pairs.  -> (last output, elapsed seconds, graph or None).
+
+    The graph replay is not always the faster schedule: ROCm's graph executor maps the captured
+    multi-stream DAG onto its own queues, and on the eval aggregation it lost most of the
+    concurrent-scale overlap (3.91-3.93 ms vs 3.76 ms eager on the same box,
+    tools/ab_schedules.sh).  So after capture a few untimed replays and eager steps are probed
+    and the faster one is timed (--graph / --no-graph force one); args.schedule records it."""
     for _ in range(args.warmup):
         out = step()
     torch.cuda.synchronize()
@@ -329,12 +346,26 @@ def timed_run(step, args, world):
             graph = None
             torch.cuda.synchronize()
     run = graph.replay if graph is not None else step
+    args.schedule = {"timed": "hip_graph" if graph is not None else "eager"}
+    if graph is not None and not getattr(args, "graph", False):
+        # alternating rounds, best of each: one short probe per schedule is noisier than the
+        # few-percent difference it decides
+        tg = te = float("inf")
+        for _ in range(3):
+            tg = min(tg, _time_calls(graph.replay, 5))
+            te = min(te, _time_calls(step, 5))
+        args.schedule = {"graph_probe_ms": round(tg * 1e3, 4), "eager_probe_ms": round(te * 1e3, 4)}
+        if te < tg:
+            run, graph = step, None
+        args.schedule["timed"] = "hip_graph" if graph is not None else "eager"
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        run()
+        r = run()
+        if r is not None:  # eager step output (a graph replay returns None: out is its buffer)
+            out = r
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -459,7 +490,7 @@ def main():
                 "batch_per_gpu": args.batch,
                 "global_batch": args.batch * world,
                 "parallelism": f"dp{world} (pairs sharded, no data-path collective)",
-                "hip_graph": graph is not None,
+                "hip_graph": graph is not None, "schedule": getattr(args, "schedule", None),
             },
             "roofline": {"kernel": dom_name, "bound": dom["bound"], "achieved": dom["achieved"],
                          "peak": dom["peak"], "unit": dom["unit"], "frac": dom["frac"],
@@ -626,7 +657,7 @@ def model_main(args, device, rank, world):
             "config": {"workload": f"{args.model}: {FULL_MODELS[args.model]}, max_disp 192",
                        "batch_per_gpu": args.batch, "global_batch": args.batch * world,
                        "parallelism": f"dp{world} (pairs sharded, no data-path collective)",
-                       "hip_graph": graph is not None},
+                       "hip_graph": graph is not None, "schedule": getattr(args, "schedule", None)},
             "disp_range": [summary["disp_min"], summary["disp_max"]]}), flush=True)
     if world > 1:
         dist.barrier()
