@@ -442,6 +442,11 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   // above) is issued before the first use: the item loop would otherwise pay one L2/HBM round
   // trip per item and term (the stores may alias the sources, so the compiler cannot hoist them)
   f32x4 ev[EPT], eu[EPT][2][2];
+  // the CSA terms' resize ratios ih / H (PyTorch's area_pixel_compute_scale), divided once
+  float rsc[2] = {1.f, 1.f};
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    if (csa && j < a.num_up) rsc[j] = (float)a.up_h[j] / (float)H;
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
     const int e = tid + NT * i, co2 = e >> 5, qi = e & 31, yy = y0 + (qi >> 2), xx = x0 + 4 * (qi & 3);
@@ -453,7 +458,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       for (int j = 0; j < 2; ++j) {
         if (j >= a.num_up) break;
         const int ih = a.up_h[j], iw = a.up_w[j], r = a.up_r[j];
-        float hr = ((float)ih / (float)H) * ((float)yy + 0.5f) - 0.5f;
+        float hr = rsc[j] * ((float)yy + 0.5f) - 0.5f;
         hr = hr < 0.f ? 0.f : hr;
         const int h1 = (int)hr, h1p = h1 < ih - 1 ? 1 : 0;
         const float *im = a.up[j] + plane * ih * iw;
@@ -483,8 +488,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         if (j >= a.num_up) break;
-        const int ih = a.up_h[j];
-        float hr = ((float)ih / (float)H) * ((float)yy + 0.5f) - 0.5f;
+        float hr = rsc[j] * ((float)yy + 0.5f) - 0.5f;
         hr = hr < 0.f ? 0.f : hr;
         const float h1l = hr - (float)(int)hr, h0l = 1.f - h1l;
         v += h0l * hlerp(eu[i][j][0], a.up_r[j]) + h1l * hlerp(eu[i][j][1], a.up_r[j]);
