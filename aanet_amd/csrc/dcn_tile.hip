@@ -11,7 +11,11 @@
 // copy), so L2 sees each input line about three times per launch instead of ~36.  Samples outside
 // the window (large offsets) read their corners from global memory, so any offset is handled.
 //
-// Work split.  Wave w owns tile row w (16 output pixels) and all 64 output channels: lane
+// The kernel is templated on the deformable group width: 32 channels (the scale-0 block, C = 64,
+// the window of one group per phase) or 16 (the scale-1 block, C = 32: both groups share one
+// 32-channel K slice and each lane blends with its own group's sampling state).
+//
+// Work split.  Wave w owns tile row w (16 output pixels) and all output channels: lane
 // (kr = lane / 16, jj = lane % 16) blends pixel jj's channels 8kr..8kr+7 -- exactly the B fragment
 // of v_mfma_f32_16x16x32_bf16 -- so the deformable im2col never goes through LDS and needs no
 // per-chunk hand-off between waves.  The A fragments (pre-split weights of one tap) are staged
@@ -207,7 +211,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
     pow_ = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, p4 + oplane + P * 4, 0, 0));
     pml = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mskr, p4 + mplane, 0, 0));
   };
-  TapState ps;  // this lane's state for tap t0 + kr
+  TapState ps;  // this lane's state for (tap, group) pt(kr) of the current pass
   auto compute_pass = [&](int t0) {
     ps = tap_state<DIL, WR, WC>(poh, pow_, pml, py, px, pv, min(t0 + pt, K - 1), H, W, wy0, wx0,
                                 a.mask_logits, a.mask_scale);
@@ -227,7 +231,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
 #pragma unroll
   for (int m = 0; m < NCO; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // one tap of one group: corners -> blend -> split -> 24 MFMAs
+  // one chunk (tap of a 32-channel K slice): corners -> blend -> split -> 6 NCO MFMAs
   auto tap = [&](int g, int k, const char *sAc, const TapState &s, bool reload) {
     f32x4 cq[4][2];  // corners TL, TR, BL, BR x channel quads 2kr, 2kr+1
     const int lpos = (s.pos < 0 || (a.dbg & 2)) ? 0 : s.pos;
