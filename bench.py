@@ -323,7 +323,8 @@ def timed_run(step, args, world):
     The graph replay is not always the faster schedule: ROCm's graph executor maps the captured
     multi-stream DAG onto its own queues, and on the eval aggregation it lost most of the
     concurrent-scale overlap (3.91-3.93 ms vs 3.76 ms eager on the same box,
-    tools/ab_schedules.sh).  So after capture a few untimed replays and eager steps are probed
+    tools/ab_schedules.sh).  So after capture untimed replays and eager steps are probed (5 alternating
+    rounds of 5, best of each)
     and the faster one is timed (--graph / --no-graph force one); args.schedule records it."""
     for _ in range(args.warmup):
         out = step()
@@ -351,7 +352,7 @@ def timed_run(step, args, world):
         # alternating rounds, best of each: one short probe per schedule is noisier than the
         # few-percent difference it decides
         tg = te = float("inf")
-        for _ in range(3):
+        for _ in range(5):
             tg = min(tg, _time_calls(graph.replay, 5))
             te = min(te, _time_calls(step, 5))
         args.schedule = {"graph_probe_ms": round(tg * 1e3, 4), "eager_probe_ms": round(te * 1e3, 4)}
