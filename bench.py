@@ -62,6 +62,8 @@ def parse():
                     help="--train: plain convs on the HIP engine (auto: with --deterministic)")
     ap.add_argument("--deterministic", action="store_true",
                     help="--train with torch.use_deterministic_algorithms (det DCN backward)")
+    ap.add_argument("--img", default=None,
+                    help="--model: image HxW (default 384x1248, KITTI; BASELINE C3 is 576x960)")
     ap.add_argument("--model", default=None, choices=sorted(FULL_MODELS),
                     help="time the full model (features + hot path + refinement) instead")
     ap.add_argument("--exact-f32", action="store_true",
@@ -635,8 +637,9 @@ def model_main(args, device, rank, world):
                 mod.bias.normal_(0.0, 0.5, generator=g)
     model = model.to(device).eval()
     gen = torch.Generator(device=device).manual_seed(4321 + rank)
-    left = torch.randn((args.batch, 3, H_IMG, W_IMG), device=device, generator=gen)
-    right = torch.randn((args.batch, 3, H_IMG, W_IMG), device=device, generator=gen)
+    ih, iw = (int(v) for v in args.img.lower().split("x")) if args.img else (H_IMG, W_IMG)
+    left = torch.randn((args.batch, 3, ih, iw), device=device, generator=gen)
+    right = torch.randn((args.batch, 3, ih, iw), device=device, generator=gen)
 
     def step():
         with torch.no_grad():
@@ -649,7 +652,7 @@ def model_main(args, device, rank, world):
     summary = adist.summarize(adist.gather_records(rec))
     if rank == 0:
         print(json.dumps({
-            "metric": f"full-model stereo-pairs/s @384x1248 ({args.model}, KITTI config) fp32",
+            "metric": f"full-model stereo-pairs/s @{ih}x{iw} ({args.model}, KITTI config) fp32",
             "value": summary["pairs"] / summary["elapsed_max_s"], "unit": "stereo-pairs/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": 1000.0 * summary["elapsed_max_s"] / args.steps,
