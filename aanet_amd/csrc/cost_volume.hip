@@ -4,7 +4,8 @@
 //   P[x][x'] = sum_c L[c][x] * R[c][x'],  out[d][x] = P[x][x-d] / C  for 0 <= d < D.
 // One workgroup owns a 64-wide x tile of one (b, y) row and a chunk of <=64 disparities.
 // Channels stream through LDS in 16-channel stages (double-buffered LDS, two stages of loads in
-// flight in a register ring).  Each of the 4 waves owns 16 x
+// flight in a register ring; for C in {32, 64, 128} the branch-free, fully unrolled ring tile
+// corr_reg_tile, otherwise the general corr_tile).  Each of the 4 waves owns 16 x
 // and computes the 16 x (16*NJ) band of P with v_mfma_f32_16x16x4_f32 (exact fp32), so
 // every L / R element is read from HBM once and the FMAs run on the matrix pipe.  The band
 // is transposed through LDS to [d][x] and stored as full 256-B rows.  x' < 0 reads are
@@ -273,6 +274,193 @@ __global__ __launch_bounds__(NTHREADS) void corr_pyramid_kernel(CorrPyramid p) {
 #undef AANET_CORR_CASE
 }
 
+// ------------------------------------------ register-ring correlation tile (round 3) ------
+// (An LDS-DMA form of this tile -- buffer_load ... lds into a ring of three stage buffers, no VGPR
+// staging -- was bit-identical but 15 % slower: the LDS ring caps the bytes in flight per CU at
+// about a third of what five register-staged workgroups keep in flight)
+// The round-2 tile's register ring, rebuilt so that nothing serialises it: in the round-2 form
+// the staging stores sat behind per-lane guards (exec-masked branches), and on the path around
+// a guard the compiler's wait tracking kept the ring registers "pending", so before issuing the
+// next stage it waited for nearly all of the previous one (vmcnt(1)) -- one stage in flight.
+//   * Every load and every staging store is unconditional: the R window is always 128 wide (its
+//     first 16 (5 - NJ) columns read zero through the range check), so each thread owns exactly
+//     one L and two R float4 per stage.
+//   * The channel offset lives in the buffer resource (base advanced c0 planes, num_records =
+//     (C - c0) planes): a lane's byte offsets are fixed for the whole tile, zero VALU per stage.
+//   * The stage loop is fully unrolled (NS = C / 16 compile-time): ring slots and LDS buffers are
+//     constants and the compiler's vmcnt waits are exact; RING stages are in flight during each
+//     stage's MFMAs (RING = 3: 36 KB per workgroup, in VGPRs).
+constexpr unsigned OOB = 0x80000000u;  // byte offset past any range: the buffer load returns 0
+
+template <int NJ, int NS, int RING>
+__device__ __forceinline__ void corr_reg_tile(const float *__restrict__ L, const float *__restrict__ R,
+                                              float *__restrict__ out, int C, int H, int W, int D,
+                                              int dchunk, int ntx, int nchunks, int id, float *smem) {
+  constexpr int RW = 128, LP = TX + 16, RP = RW + 16;  // pitches = 16 mod 32: conflict-free
+  constexpr int STAGE = CC * LP + CC * RP;
+  constexpr int OUTP = TX + 3, OROWS = 16 * NJ + 15;
+  static_assert(2 * STAGE >= OROWS * OUTP, "band tile fits the stage buffers");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tx = id % ntx;
+  id /= ntx;
+  const int chunk = id % nchunks;
+  id /= nchunks;
+  const int y = id % H, b = id / H;
+  const int x0 = tx * TX, d0 = chunk * dchunk;
+  const int xr0 = x0 - d0 - 64;  // the 128-wide window's first x' (NJ = 5 band reach)
+  const int HW = H * W;          // C*H*W*4 < 2^31 (launcher)
+  // thread -> (row, quad) of the L tile (one float4) and of the R window (two float4)
+  const int lrow = tid >> 4, lq = tid & 15;
+  unsigned lofs, rofs[2];
+  {
+    const int x = x0 + 4 * lq;
+    lofs = x < W ? (unsigned)((lrow * HW + y * W + x) * 4) : OOB;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 256 * i, row = e >> 5, q = e & 31;
+      const int xr = xr0 + 4 * q;
+      // columns left of the NJ band's reach are never read: keep them zero, no traffic
+      const bool need = q >= 4 * (5 - NJ);
+      rofs[i] = (need && xr >= 0 && xr < W) ? (unsigned)((row * HW + y * W + xr) * 4) : OOB;
+    }
+  }
+  const float *Lb = L + (long)b * C * HW, *Rb = R + (long)b * C * HW;
+  f32x4 lv[RING], rv[RING][2];
+  auto load = [&](int slot, int s) {
+    const int c0 = s * CC, nrec = (C - c0) * HW * 4;
+    const auto rl = __builtin_amdgcn_make_buffer_rsrc((void *)(Lb + (long)c0 * HW), (short)0, nrec,
+                                                      0x00020000);
+    const auto rr = __builtin_amdgcn_make_buffer_rsrc((void *)(Rb + (long)c0 * HW), (short)0, nrec,
+                                                      0x00020000);
+    lv[slot] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rl, lofs, 0, 2));
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      rv[slot][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, rofs[i], 0, 0));
+  };
+  auto store = [&](int slot, int buf) {
+    float *sL = smem + buf * STAGE, *sR = sL + CC * LP;
+    *reinterpret_cast<f32x4 *>(sL + lrow * LP + 4 * lq) = lv[slot];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 256 * i;
+      *reinterpret_cast<f32x4 *>(sR + (e >> 5) * RP + 4 * (e & 31)) = rv[slot][i];
+    }
+  };
+  f32x4 acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kr = lane >> 4, jj = lane & 15;
+  const bool active = x0 + 16 * wave < W;  // wave-uniform (scalar) branch around the MFMAs only
+  auto compute = [&](int buf) {
+    const float *sL = smem + buf * STAGE, *sR = sL + CC * LP;
+    float a[CC / 4], bv[CC / 4][NJ];
+#pragma unroll
+    for (int ks = 0; ks < CC / 4; ++ks) {
+      const int row = 4 * ks + kr;
+      a[ks] = sL[row * LP + 16 * wave + jj];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bv[ks][j] = sR[row * RP + 16 * wave + jj + 16 * (4 - j)];
+    }
+#pragma unroll
+    for (int ks = 0; ks < CC / 4; ++ks)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[j] = mfma16x16x4(a[ks], bv[ks][j], acc[j]);
+  };
+#pragma unroll
+  for (int k = 0; k < RING; ++k)
+    if (k < NS) load(k, k);
+  store(0, 0);
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (s + RING < NS) load(s % RING, s + RING);  // slot of stage s: stored last iteration
+    if (active) compute(s & 1);
+    if (s + 1 < NS) store((s + 1) % RING, (s + 1) & 1);
+    __syncthreads();
+  }
+
+  // band -> [d][x] tile in LDS (rows outside [0, dchunk) are scratch), then 256-B row stores
+  float *sO = smem + 15 * OUTP;
+  const float invC = 1.f / (float)C;
+  const int dmax = min(dchunk, D - d0);
+  float *sOl = sO + (4 * kr - jj) * OUTP + 16 * wave + 4 * kr;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sOl[(16 * j + r) * OUTP + r] = acc[j][r] * invC;
+  __syncthreads();
+  for (int e = tid; e < dmax * (TX / 4); e += NTHREADS) {
+    const int dl = e / (TX / 4), xq = e % (TX / 4);
+    if (x0 + 4 * xq < W) {
+      const float *src = sO + dl * OUTP + 4 * xq;
+      __builtin_nontemporal_store(
+          f32x4{src[0], src[1], src[2], src[3]},
+          reinterpret_cast<f32x4 *>(out + (((long)b * D + d0 + dl) * H + y) * W + x0 + 4 * xq));
+    }
+  }
+}
+
+constexpr int REG_SMEM = 2 * (CC * (TX + 16) + CC * (128 + 16));
+
+template <int NJ, int NS, int RG>
+__global__ __launch_bounds__(NTHREADS) void corr_reg_kernel(const float *__restrict__ L,
+                                                            const float *__restrict__ R,
+                                                            float *__restrict__ out, int C, int H,
+                                                            int W, int D, int dchunk, int ntx,
+                                                            int nchunks) {
+  __shared__ __attribute__((aligned(16))) float smem[REG_SMEM];
+  corr_reg_tile<NJ, NS, RG>(L, R, out, C, H, W, D, dchunk, ntx, nchunks,
+                            xcd_remap(gridDim.x, blockIdx.x), smem);
+}
+
+// The whole pyramid in one launch on the ring tile (the work list of corr_pyramid_kernel); every
+// scale has C in {32, 64, 128} (NS = C / 16 in {2, 4, 8}).  The body is compiled in the device
+// pass only: the host pass rejects the tile's instantiations in this switch with a bare
+// "substitution failure" (clang, ROCm 7.2), and the host never runs a kernel body.
+template <int RING>
+__global__ __launch_bounds__(NTHREADS) void corr_pyramid_reg_kernel(CorrPyramid p) {
+  __shared__ __attribute__((aligned(16))) float smem[REG_SMEM];
+#if __HIP_DEVICE_COMPILE__
+  const int xcd = blockIdx.x & 7, i = blockIdx.x >> 3;
+  int s = 0;
+  while (s + 1 < p.ns && i >= p.mstart[s + 1]) ++s;
+  const int local = xcd * p.per[s] + (i - p.mstart[s]);
+  if (local >= p.cnt[s]) return;
+  const int ns = p.C[s] >> 4;
+#define AANET_CORR_REG(J, NSV)                                                                    \
+  corr_reg_tile<J, NSV, RING>(p.L[s], p.R[s], p.out[s], p.C[s], p.H[s], p.W[s], p.D[s],          \
+                              p.dchunk[s], p.ntx[s], p.nchunks[s], local, smem)
+#define AANET_CORR_REG_NS(J)                 \
+  case J:                                    \
+    if (ns == 8) AANET_CORR_REG(J, 8);       \
+    else if (ns == 4) AANET_CORR_REG(J, 4);  \
+    else AANET_CORR_REG(J, 2);               \
+    break;
+  switch (p.nj[s]) {
+    AANET_CORR_REG_NS(1)
+    AANET_CORR_REG_NS(2)
+    AANET_CORR_REG_NS(3)
+    AANET_CORR_REG_NS(4)
+    default:
+      if (ns == 8) AANET_CORR_REG(5, 8);
+      else if (ns == 4) AANET_CORR_REG(5, 4);
+      else AANET_CORR_REG(5, 2);
+  }
+#undef AANET_CORR_REG_NS
+#undef AANET_CORR_REG
+#else
+  (void)smem;
+  (void)p;
+#endif
+}
+
+constexpr int RING = 2;  // register-ring depth on the product path (3 measured equal)
+
+bool corr_ring_ok(int c, int h, int w) {
+  return (c == 32 || c == 64 || c == 128) && w % 4 == 0 && (long)c * h * w * 4 < 0x7fffffffL;
+}
+
 int corr_nj(int max_disp) {
   const int dneed = max_disp < 64 ? max_disp : 64;
   return dneed <= 1 ? 1 : 1 + (dneed - 1 + 15) / 16;
@@ -292,7 +480,24 @@ template <int NJ>
 int launch_corr(const float *L, const float *R, float *out, int n, int c, int h, int w, int D,
                 hipStream_t st) {
   const int dchunk = CorrSmem<NJ>::DC;
-  const int nchunks = host_div_up(D, dchunk), ntx = host_div_up(w, TX);
+  const int nchunks = host_div_up(D, dchunk);
+  if (corr_ring_ok(c, h, w)) {
+    const int ntx = host_div_up(w, TX);
+    const long nb = (long)ntx * nchunks * h * n;
+    if (nb > 0x7fffffffL) return AANET_EUNSUPPORTED;
+    const dim3 grid((unsigned)nb), blk(NTHREADS);
+    if (c == 128)
+      hipLaunchKernelGGL((corr_reg_kernel<NJ, 8, RING>), grid, blk, 0, st, L, R, out, c, h, w, D,
+                         dchunk, ntx, nchunks);
+    else if (c == 64)
+      hipLaunchKernelGGL((corr_reg_kernel<NJ, 4, RING>), grid, blk, 0, st, L, R, out, c, h, w, D,
+                         dchunk, ntx, nchunks);
+    else
+      hipLaunchKernelGGL((corr_reg_kernel<NJ, 2, RING>), grid, blk, 0, st, L, R, out, c, h, w, D,
+                         dchunk, ntx, nchunks);
+    return aanet_launch_status();
+  }
+  const int ntx = host_div_up(w, TX);
   const long nblk = (long)ntx * nchunks * h * n;
   if (nblk > 0x7fffffffL) return AANET_EUNSUPPORTED;
   const bool vec = (w % 4) == 0 && (long)c * h * w * 4 < 0x7fffffffL;
@@ -514,6 +719,9 @@ extern "C" int aanet_corr_pyramid_f32(int num_scales, const float *const *left,
   AANET_HOST_CHECK(num_scales > 0 && left && right && out && c && h && w && n > 0);
   // one launch when every scale takes the vector tile path (w % 4 == 0, 32-bit offsets)
   bool one = num_scales <= MAXS;
+  bool ring = one;  // every scale on the register-ring tile
+  for (int s = 0; ring && s < num_scales; ++s)
+    ring = c[s] > 0 && h[s] > 0 && corr_ring_ok(c[s], h[s], w[s]);
   CorrPyramid p;
   p.ns = num_scales;
   long total = 0;
@@ -548,8 +756,12 @@ extern "C" int aanet_corr_pyramid_f32(int num_scales, const float *const *left,
   }
   if (one) {
     p.mstart[num_scales] = (int)(total / 8);
-    hipLaunchKernelGGL(corr_pyramid_kernel, dim3((unsigned)total), dim3(NTHREADS), 0,
-                       as_hip(stream), p);
+    if (ring)
+      hipLaunchKernelGGL(corr_pyramid_reg_kernel<RING>, dim3((unsigned)total), dim3(NTHREADS), 0,
+                         as_hip(stream), p);
+    else
+      hipLaunchKernelGGL(corr_pyramid_kernel, dim3((unsigned)total), dim3(NTHREADS), 0,
+                         as_hip(stream), p);
     return aanet_launch_status();
   }
   for (int s = 0; s < num_scales; ++s) {

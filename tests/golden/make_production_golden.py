@@ -12,6 +12,9 @@ NCHW engine only.  These fixtures pin the configurations the bench and the users
                NHWC bottleneck tails and the CSA epilogue (exact 2x/4x terms, W % 4 == 0)
   hotpath_c1   max_disp=24 (BASELINE configs[0]: 288x576, --max_disp 72 // 3), features
                [1,128,96,192] pyramid -> widths 24/12/6
+  hotpath_c3   max_disp=64, AANet+ feature widths (BASELINE configs[2]: GANetFeature +
+               FeaturePyrmaid, nets/feature.py:150,379-419): [1,32,48,80] / [1,64,24,40] /
+               [1,128,12,20] -- the C3 pyramid's channel counts at a reduced H x W
 
 The reference graph is nets/cost.py CostVolumePyramid -> nets/aggregation.py
 AdaptiveAggregation(num_deform_blocks=3, intermediate_supervision=False) ->
@@ -37,9 +40,10 @@ from make_golden import load_reference, save  # noqa: E402
 from tests.golden_io import fill_synthetic, synthetic_pyramid  # noqa: E402
 
 CASES = {
-    # tag: (max_disp, B, C, H, W, seed)
+    # tag: (max_disp, B, C, H, W, seed[, per-scale channels])
     "hotpath_d64": (64, 2, 128, 32, 96, 64),
     "hotpath_c1": (24, 1, 128, 96, 192, 24),
+    "hotpath_c3": (64, 1, 32, 48, 80, 3, (32, 64, 128)),
 }
 
 
@@ -52,7 +56,9 @@ def run(cost, est, agg, max_disp, left, right, model):
 
 def main():
     cost, est, agg = load_reference()
-    for tag, (max_disp, B, C, H, W, seed) in CASES.items():
+    for tag, case in CASES.items():
+        max_disp, B, C, H, W, seed = case[:6]
+        channels = case[6] if len(case) > 6 else None
         torch.manual_seed(seed)
         model = agg.AdaptiveAggregation(max_disp=max_disp, num_scales=3, num_fusions=6,
                                         num_stage_blocks=1, num_deform_blocks=3,
@@ -60,7 +66,7 @@ def main():
                                         mdconv_dilation=2)
         names = fill_synthetic(model, seed)
         model.eval()
-        left, right = synthetic_pyramid(B, C, H, W, seed)
+        left, right = synthetic_pyramid(B, C, H, W, seed, channels=channels)
         with torch.no_grad():
             disp, agg0 = run(cost, est, agg, max_disp, left, right, model)
             disp64, _ = run(cost, est, agg, max_disp, [t.double() for t in left],
@@ -77,6 +83,7 @@ def main():
              agg0_sum=np.float64(a0.astype(np.float64).sum()),
              agg0_abs_sum=np.float64(np.abs(a0.astype(np.float64)).sum()),
              **{f"disp{i}": d for i, d in enumerate(disp)},
+             **({"channels": np.array(channels)} if channels is not None else {}),
              **{f"disp64_{i}": d for i, d in enumerate(disp64)})
         d, d64 = disp[0].double().numpy(), disp64[0].numpy()
         print(f"  {tag}: disp {tuple(disp[0].shape)} mean {d.mean():.3f} std {d.std():.3f}; "

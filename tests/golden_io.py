@@ -70,14 +70,16 @@ def synthetic_pair(B, H, W, seed):
     return left, right
 
 
-def synthetic_pyramid(B, C, H, W, seed, num_scales=3):
+def synthetic_pyramid(B, C, H, W, seed, num_scales=3, channels=None):
     """Seeded N(0,1) feature pyramids (left, right) at H>>s x W>>s, s < num_scales (torch CPU
     generator), for the production-configuration fixtures: the test rebuilds them from the seed,
-    so the fixture carries outputs only."""
+    so the fixture carries outputs only.  `channels` gives per-scale widths (AANet+'s
+    FeaturePyrmaid: 32/64/128, nets/feature.py:379-419); otherwise every scale has C."""
     import torch
     g = torch.Generator().manual_seed(5000 + seed)
-    left = [torch.randn(B, C, H >> s, W >> s, generator=g) for s in range(num_scales)]
-    right = [torch.randn(B, C, H >> s, W >> s, generator=g) for s in range(num_scales)]
+    cs = list(channels) if channels is not None else [C] * num_scales
+    left = [torch.randn(B, cs[s], H >> s, W >> s, generator=g) for s in range(num_scales)]
+    right = [torch.randn(B, cs[s], H >> s, W >> s, generator=g) for s in range(num_scales)]
     return left, right
 
 
@@ -97,7 +99,8 @@ def production_case(tag):
     sd = {k: v.numpy() for k, v in m.aggregation.state_dict().items()}
     checksum = sum(float(torch.from_numpy(v).double().abs().sum()) for v in sd.values())
     assert abs(checksum - float(g["checksum"])) <= 1e-9 * abs(checksum), "weight fill differs"
-    left, right = synthetic_pyramid(B, C, H, W, seed)
+    channels = [int(c) for c in g["channels"]] if "channels" in g else None
+    left, right = synthetic_pyramid(B, C, H, W, seed, channels=channels)
     feat = sum(float(t.double().abs().sum()) for t in left + right)
     assert abs(feat - float(g["feat_checksum"])) <= 1e-9 * abs(feat), "feature fill differs"
     return g, sd, m, left, right

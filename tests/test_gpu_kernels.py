@@ -57,7 +57,11 @@ def test_corr_volume_vs_reference_golden(name):
                                        (2, 128, 3, 104, 16), (1, 32, 3, 130, 192), (1, 7, 2, 65, 24),
                                        (1, 3, 2, 5, 1), (1, 64, 2, 70, 100),
                                        # odd stage counts (3, 5 stages) on both load paths
-                                       (1, 48, 2, 96, 40), (1, 40, 2, 66, 30), (2, 80, 2, 136, 64)])
+                                       (1, 48, 2, 96, 40), (1, 40, 2, 66, 30), (2, 80, 2, 136, 64),
+                                       # the register-ring tile (C = 32 / 64 / 128): C3 (AANet+)
+                                       # scale widths 320 / 160 / 80, ragged x tiles, W < D
+                                       (2, 32, 3, 320, 64), (1, 64, 3, 160, 32), (2, 128, 2, 80, 16),
+                                       (1, 32, 2, 100, 64), (1, 64, 2, 28, 48), (1, 128, 3, 20, 24)])
 def test_corr_volume_vs_oracle(B, C, H, W, D):
     rng = np.random.default_rng(B * 1000 + C + D)
     L = rng.standard_normal((B, C, H, W)).astype(np.float32)

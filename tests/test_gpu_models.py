@@ -109,6 +109,30 @@ def test_full_model_vs_reference_golden(tag, fuse):
           for i, a, b, c in report])
 
 
+def test_aanetplus_c3_full_size_properties():
+    """BASELINE configs[2] at its own image size: AANet+ (GANetFeature + FeaturePyrmaid +
+    hourglass refinement, max_disp 192; scripts/aanet+_train.sh:12-15) on one 576x960 pair.
+    The 32/64/128-channel feature pyramid at 192x320 / 96x160 / 48x80 feeds the hot path; the
+    outputs must have the reference's shapes, be finite, the regressed level must lie in
+    [0, D-1] = [0, 63] and the refined levels (ReLU'd, nets/refinement.py) be >= 0."""
+    g = golden("model_aanetplus")
+    m = nets.AANet(192, 1, **json.loads(str(g["config"])))
+    fill_synthetic(m, int(g["seed"]))
+    m = m.to(DEV).eval()
+    left, right = synthetic_pair(1, 576, 960, int(g["seed"]))
+    with torch.no_grad():
+        feats = m.feature_extraction(left.to(DEV))
+        assert [tuple(f.shape) for f in feats] == [(1, 32, 192, 320), (1, 64, 96, 160),
+                                                   (1, 128, 48, 80)]
+        pyr = m(left.to(DEV), right.to(DEV))
+    assert [tuple(d.shape) for d in pyr] == [(1, 192, 320), (1, 288, 480), (1, 576, 960)]
+    for d in pyr:
+        assert torch.isfinite(d).all()
+        assert float(d.min()) >= 0.0
+    assert float(pyr[0].max()) <= 63.0
+    print("AANet+ 576x960: disparity ranges", [(float(d.min()), float(d.max())) for d in pyr])
+
+
 def test_full_model_training_step():
     """AANet with intermediate supervision in train mode: the 5-level pyramid, the reference
     loss weights, backward through every HIP kernel (DCN in the feature extractor and the

@@ -9,6 +9,9 @@ channels wide, so they exercise the exact-f32 NCHW engine only.  Here:
 * hotpath_c1 -- BASELINE configs[0] (288x576, D=24): features [1,128,96,192];
 * C2 pair 0 at full size ([1,128,128,416] pyramid, D=64) against the CPU oracle (which the
   d64 fixture pins to the reference at the same widths);
+* hotpath_c3 -- BASELINE configs[2] (AANet+: GANetFeature + FeaturePyrmaid) feature widths
+  32/64/128 at a reduced size, the reference graph's own output; and C3 pair 0 at its full
+  size ([1,32,192,320] / [1,64,96,160] / [1,128,48,80], D=64) against the CPU oracle;
 * the eval-cache, CSA-epilogue-precondition and grouped-DCN regressions of ADVICE round 1.
 
 Tolerances: disparity 2e-4 px max abs (north-star bar 1e-3); aggregated cost 1e-4 x its scale.
@@ -97,6 +100,41 @@ def test_c2_pair0_full_size_vs_oracle():
     err = np.abs(d.astype(np.float64) - ref)
     print(f"C2 pair 0 vs oracle: max|dd| {err.max():.3g} px, mean {err.mean():.3g}")
     assert d.shape == (1, 128, 416)
+    assert err.max() <= DISP_TOL, f"max |dd| {err.max():.3g} px"
+
+
+def test_hotpath_c3_vs_reference():
+    """BASELINE configs[2] (AANet+): per-scale feature widths 32/64/128 (nets/feature.py:379-419)
+    -> the register-ring correlation tile at C = 32 and 64, then the D=64 aggregation."""
+    g, _, m, left, right = _model("hotpath_c3")
+    assert [t.shape[1] for t in left] == [32, 64, 128]
+    with torch.no_grad():
+        disps = m(left, right)
+    d = disps[0].cpu().numpy()
+    assert d.shape == g["disp0"].shape == (1, 48, 80)
+    err = np.abs(d - g["disp0"])
+    print(f"hotpath_c3: max|dd| {err.max():.3g} px, mean {err.mean():.3g}, reference fp32 vs "
+          f"fp64 max {np.abs(g['disp0'] - g['disp64_0']).max():.3g}")
+    assert err.max() <= DISP_TOL, f"max |dd| {err.max():.3g} px"
+
+
+def test_c3_pair0_full_size_vs_oracle():
+    """C3 at its own shapes: one 576x960 AANet+ pair -- features [1,32,192,320] /
+    [1,64,96,160] / [1,128,48,80] (scripts/aanet+_train.sh:12-15, max_disp 192 -> D=64) --
+    through the bench kernels, against the CPU oracle on the same input."""
+    torch.manual_seed(0)
+    m = nets.AANetHotPath(64, no_intermediate_supervision=True, num_deform_blocks=3)
+    fill_synthetic(m.aggregation, 5)
+    sd = {k: v.numpy().copy() for k, v in m.aggregation.state_dict().items()}
+    m = m.to(DEV).eval()
+    left, right = synthetic_pyramid(1, 32, 192, 320, 5, channels=(32, 64, 128))
+    with torch.no_grad():
+        d = m([t.to(DEV) for t in left], [t.to(DEV) for t in right])[0].cpu().numpy()
+    ref = oagg.hot_path([t.numpy() for t in left], [t.numpy() for t in right], sd, 64,
+                        intermediate_supervision=False)[0]
+    err = np.abs(d.astype(np.float64) - ref)
+    print(f"C3 pair 0 vs oracle: max|dd| {err.max():.3g} px, mean {err.mean():.3g}")
+    assert d.shape == (1, 192, 320)
     assert err.max() <= DISP_TOL, f"max |dd| {err.max():.3g} px"
 
 
