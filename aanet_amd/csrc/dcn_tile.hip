@@ -29,6 +29,8 @@
 // split-bf16 one (three exact bf16 pieces, six products, fp32 accumulation; mdcn.hip split3).
 #include "dcn_tile.h"
 
+#include <cstdio>
+
 #include <stdlib.h>
 
 namespace {
@@ -538,7 +540,18 @@ int dcn_tile_launch(const DcnTileArgs &a, hipStream_t stream) {
   if ((long)a.C * P * 4 >= (1L << 31) || (long)(2 * a.dg * 27) * P * 4 >= (1L << 31))
     return AANET_EUNSUPPORTED;
   const long tiles = (long)host_div_up(a.W, TC) * host_div_up(a.H, TR);
-  static const int dbg = [] { const char *e = getenv("AANET_DCN_DBG"); return e ? atoi(e) : 0; }();
+  // timing-attribution switches (skip MFMAs / barriers / loads / the epilogue: WRONG results) are
+  // read only in a debug build (make AANET_DEBUG=1); the product library always runs the kernel
+#ifdef AANET_DEBUG_SWITCHES
+  static const int dbg = [] {
+    const char *e = getenv("AANET_DCN_DBG");
+    const int v = e ? atoi(e) : 0;
+    if (v) fprintf(stderr, "aanet: AANET_DCN_DBG=%d -- timing build, outputs are INVALID\n", v);
+    return v;
+  }();
+#else
+  constexpr int dbg = 0;
+#endif
   DcnTileArgs b = a;
   b.dbg = dbg;
   if (a.C == 64)

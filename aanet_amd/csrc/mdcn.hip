@@ -17,6 +17,7 @@
 #include "dcn_tile.h"
 #include "pointwise.h"
 
+#include <cstdio>
 #include <stdlib.h>
 
 namespace {
@@ -2939,8 +2940,13 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
     // replace int64 global ones); with float atomics the global-atomic kernel is faster (agg_s0
     // 5.1 vs 7.9 ms: the 75 KB of LDS halve the waves that hide the per-tap gather latency).
     // AANET_DCN_BWD_WINDOW: 0 never, 1 deterministic only, 2 both.
+#ifdef AANET_DEBUG_SWITCHES  // timing build only (skips the grad_x scatter: WRONG gradients)
     const char *dbg_env = getenv("AANET_DCN_BWD_DBG");
     a.dbg_noatom = dbg_env ? atoi(dbg_env) : 0;
+    if (a.dbg_noatom) fprintf(stderr, "aanet: AANET_DCN_BWD_DBG -- timing build, gradients INVALID\n");
+#else
+    a.dbg_noatom = 0;
+#endif
     const char *bwd_env = getenv("AANET_DCN_BWD_WINDOW");  // read per call (tests switch it)
     const int bwd_win = bwd_env ? atoi(bwd_env) : 1;
     const int cpg = c / dg, R = 2;

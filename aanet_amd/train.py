@@ -30,6 +30,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
+from .nets._fuse import clear_fold_caches
 
 # model.py:98-107: pyramid weights by pyramid length
 PYRAMID_WEIGHTS = {5: [1 / 3, 2 / 3, 1.0, 1.0, 1.0],  # AANet and AANet+
@@ -144,22 +145,28 @@ def _engine_conv_ok(m):
             and p[0] <= d[0] * (k[0] - 1))
 
 
-def _engine_conv_forward(m, x):
-    if x.dtype != torch.float32 or not x.is_cuda:  # the HIP engine takes fp32 device tensors
-        return nn.Conv2d.forward(m, x)
-    return EngineConv2dFunction.apply(x, m.weight, m.bias, m.stride[0], m.padding[0],
-                                      m.dilation[0], m.groups)
+class EngineConv2d(nn.Conv2d):
+    """nn.Conv2d whose training forward runs EngineConv2dFunction (use_engine_convs swaps a
+    module's class to this one in place).  Same parameters, buffers and state-dict keys; being a
+    module-level subclass, a whole-model torch.save / torch.load round-trips (a bound method
+    stored in the instance __dict__ did not unpickle)."""
+
+    def forward(self, x):
+        if x.dtype != torch.float32 or not x.is_cuda:  # the HIP engine takes fp32 device tensors
+            return nn.Conv2d.forward(self, x)
+        return EngineConv2dFunction.apply(x, self.weight, self.bias, self.stride[0],
+                                          self.padding[0], self.dilation[0], self.groups)
 
 
 def use_engine_convs(model):
     """Route every nn.Conv2d of `model` that the engine takes (square kernel, symmetric
     stride/padding/dilation, zero padding) through EngineConv2dFunction; returns how many.
-    The module type and parameters are unchanged (state_dict, DDP and the eval-mode folding of
-    nets/_fuse.py see the same module)."""
+    Only the class changes (nn.Conv2d -> EngineConv2d, a subclass): parameters, state_dict,
+    DDP and the eval-mode folding of nets/_fuse.py see the same module."""
     n = 0
     for m in model.modules():
-        if _engine_conv_ok(m) and "forward" not in m.__dict__:
-            m.forward = _engine_conv_forward.__get__(m)
+        if type(m) is nn.Conv2d and _engine_conv_ok(m):
+            m.__class__ = EngineConv2d
             m._aanet_engine = True
             n += 1
     return n
@@ -214,9 +221,13 @@ class Trainer:
                 self.optimizer.step()
                 return total.detach()
             # the warm-up steps must not count: parameters, BN buffers and the optimizer state are
-            # restored in place afterwards (the graph holds their addresses)
+            # restored in place afterwards (the graph holds their addresses).  Optimizer state
+            # that exists already (eager step() calls before the first graph_step) is restored to
+            # its values; state the warm-up creates is zeroed (Adam's initial state).
             snap = [(t, t.detach().clone()) for t in
                     list(self.model.parameters()) + list(self.model.buffers())]
+            opt_snap = {id(v): (v, v.detach().clone()) for st in self.optimizer.state.values()
+                        for v in st.values() if torch.is_tensor(v)}
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
@@ -232,10 +243,20 @@ class Trainer:
             with torch.no_grad():
                 for t, v in snap:
                     t.copy_(v)
-                for st in self.optimizer.state.values():  # Adam: step, exp_avg, exp_avg_sq start at 0
+                for st in self.optimizer.state.values():
                     for v in st.values():
-                        if torch.is_tensor(v):
+                        if not torch.is_tensor(v):
+                            continue
+                        prev = opt_snap.get(id(v))
+                        if prev is not None and prev[0] is v:
+                            v.copy_(prev[1])
+                        else:  # created by the warm-up: Adam's step, exp_avg, exp_avg_sq start at 0
                             v.zero_()
+        # a replay updates parameters and BN running statistics in place without bumping their
+        # _version, which the eval path's folded-weight caches key on: drop the caches (and put
+        # the model in train mode, as step() does) so a later eval forward refolds
+        self.model.train()
+        clear_fold_caches(self.model)
         self._graph.replay()
         return self._graph_loss
 

@@ -21,6 +21,11 @@ SHAPES = [
     (1, 16, 25, 39, 32, 3, 2, 1, 1, 1, False),   # stride 2, odd sizes (dropped row/column)
     (3, 48, 12, 20, 1, 1, 1, 0, 1, 1, True),     # final_conv-like, Co = 1
     (2, 70, 9, 13, 40, 3, 1, 1, 1, 1, True),     # ragged channel counts
+    # feature-extractor shapes that Trainer(engine_convs) also routes here:
+    (1, 3, 48, 96, 32, 7, 3, 3, 1, 1, False),    # AANetFeature conv1: 7x7 stride 3, Cin 3
+    (1, 3, 50, 97, 32, 7, 3, 3, 1, 1, False),    # ... stride-3 dgrad zero insertion, ragged
+    (2, 64, 24, 40, 128, 1, 2, 0, 1, 1, False),  # ResNet downsample 1x1 stride 2
+    (1, 32, 25, 39, 64, 1, 2, 0, 1, 1, False),   # ... odd sizes
 ]
 
 

@@ -165,3 +165,55 @@ def test_graph_step_matches_eager_steps(det):
     # the last bits; Adam's m / sqrt(v) turns that into lr-sized moves of near-zero-gradient
     # elements (measured 1.5e-5 relative after 3 steps).  Deterministic mode must agree tightly.
     assert num <= (1e-5 if det else 1e-4) * den, (num, den)
+
+
+def test_graph_step_keeps_prior_eager_optimizer_state():
+    """eager step()s before the first graph_step -- the capture's warm-up is undone
+    back to THAT state (Adam moments and step count kept), so 2 eager + 2 graph steps give the
+    parameters of 4 eager steps."""
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        l, r, gt = _inputs(2, 9)
+        mask = (gt > 0) & (gt < 192)
+        runs = []
+        for graph in (False, True):
+            m = _model(17).train()
+            t = train.Trainer(m, lr=1e-3, capturable=True)
+            for i in range(4):
+                if graph and i >= 2:
+                    t.graph_step(l, r, gt, mask)
+                else:
+                    t.step(l, r, gt, mask)
+            torch.cuda.synchronize()
+            runs.append([p.detach().clone() for p in m.parameters()])
+    finally:
+        torch.use_deterministic_algorithms(prev)
+    num = sum(float((a - b).double().norm() ** 2) for a, b in zip(*runs)) ** 0.5
+    den = sum(float(a.double().norm() ** 2) for a in runs[0]) ** 0.5
+    assert num <= 1e-5 * den, (num, den)
+
+
+def test_graph_step_then_eval_refolds():
+    """ADVICE r2: graph replays update parameters and BN statistics without bumping _version;
+    graph_step, eval forward, graph_step, eval forward must match a freshly folded model."""
+    l, r, gt = _inputs(2, 11)
+    mask = (gt > 0) & (gt < 192)
+    m = _model(19).train()
+    t = train.Trainer(m, lr=1e-2, capturable=True)
+    t.graph_step(l, r, gt, mask)
+    m.eval()
+    with torch.no_grad():
+        first = m(l, r)[0].clone()
+    t.graph_step(l, r, gt, mask)
+    for mod in m.modules():  # eval mode WITHOUT Module.eval(), whose override clears the caches:
+        mod.training = False  # only graph_step's own clearing can make the forward refold
+    with torch.no_grad():
+        second = m(l, r)[0].clone()
+    fresh = _model(19)
+    fresh.load_state_dict(m.state_dict())
+    fresh.eval()
+    with torch.no_grad():
+        ref = fresh(l, r)[0]
+    assert not torch.equal(first, second)  # the second replay moved the weights
+    assert (second - ref).abs().max().item() <= 1e-4, (second - ref).abs().max().item()

@@ -223,3 +223,22 @@ def test_use_engine_convs_marks_convs_and_keeps_cpu_path():
     ref = torch.nn.functional.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding,
                                      conv.dilation, conv.groups)
     assert torch.equal(conv(x), ref)
+
+
+def test_engine_convs_model_pickles(tmp_path):
+    """a whole-model torch.save of a model with engine convs loads back (the engine
+    conv is a module-level nn.Conv2d subclass, not a bound method in the instance dict)."""
+    torch.manual_seed(0)
+    m = nets.AANetHotPath(16, no_intermediate_supervision=False, num_deform_blocks=3)
+    assert train.use_engine_convs(m) > 20
+    path = tmp_path / "whole.pt"
+    torch.save(m, path)
+    m2 = torch.load(path, weights_only=False)  # a file this test wrote itself
+    convs = [c for c in m2.modules() if isinstance(c, torch.nn.Conv2d)]
+    assert all(isinstance(c, train.EngineConv2d) for c in convs)
+    for (k, a), (k2, b) in zip(m.state_dict().items(), m2.state_dict().items()):
+        assert k == k2 and torch.equal(a, b)
+    x = torch.randn(1, convs[0].in_channels, 9, 11)
+    assert torch.equal(convs[0](x), torch.nn.functional.conv2d(
+        x, convs[0].weight, convs[0].bias, convs[0].stride, convs[0].padding, convs[0].dilation,
+        convs[0].groups))

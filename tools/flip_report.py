@@ -6,7 +6,11 @@ and the count of "flipped" pixels (|error| > 0.05 px) for each.  Run it once as 
 MIOPEN_DEBUG_CONV_WINOGRAD=0 (read by MIOpen at start-up) to see whether MIOpen's fp32 Winograd
 convolutions are what moves the reference-order path.
 
-    python tools/flip_report.py [tag ...]
+    python tools/flip_report.py [--tf32 0|1] [--cudnn 0|1] [tag ...]
+
+--tf32 sets torch.backends.cudnn.allow_tf32 inside the run (torch's cudnn.flags() context
+defaults it to True); --cudnn 0 sends the reference-order convs to PyTorch's native kernels
+instead of MIOpen.
 """
 import json
 import os
@@ -29,8 +33,14 @@ def stats(e):
 
 
 def main():
-    tags = sys.argv[1:] or golden_names("model_")
-    env = os.environ.get("MIOPEN_DEBUG_CONV_WINOGRAD", "default")
+    args = sys.argv[1:]
+    opts = {"--tf32": 1, "--cudnn": 1}
+    while args and args[0] in opts:
+        opts[args[0]] = int(args[1])
+        args = args[2:]
+    tags = args or golden_names("model_")
+    env = (f"wino={os.environ.get('MIOPEN_DEBUG_CONV_WINOGRAD', 'default')} "
+           f"tf32={opts['--tf32']} cudnn={opts['--cudnn']}")
     for tag in tags:
         g = golden(tag)
         for fuse in (True, False):
@@ -41,13 +51,14 @@ def main():
                 mod.aanet_fuse = fuse
             B, H, W = (int(v) for v in g["shape"])
             left, right = synthetic_pair(B, H, W, int(g["seed"]))
-            with torch.no_grad(), torch.backends.cudnn.flags(enabled=True, benchmark=False,
-                                                             deterministic=True):
+            with torch.no_grad(), torch.backends.cudnn.flags(enabled=bool(opts["--cudnn"]),
+                                                             benchmark=False, deterministic=True,
+                                                             allow_tf32=bool(opts["--tf32"])):
                 pyr = m(left.cuda(), right.cuda())
             for i, d in enumerate(pyr):
                 ours = d.cpu().numpy().astype(np.float64)
                 r32, r64 = g[f"disp{i}"].astype(np.float64), g[f"disp64_{i}"]
-                print(f"{tag} winograd={env} {'fused' if fuse else 'ref-order'} L{i} "
+                print(f"{tag} {env} {'fused' if fuse else 'ref-order'} L{i} "
                       f"ours-vs-64 {stats(np.abs(ours - r64))} | ref32-vs-64 {stats(np.abs(r32 - r64))}"
                       f" | ours-vs-32 {stats(np.abs(ours - r32))} | n {ours.size}", flush=True)
 
