@@ -54,7 +54,12 @@ _lib = None
 
 
 class AanetError(RuntimeError):
-    pass
+    def __init__(self, msg, status=None):
+        super().__init__(msg)
+        self.status = status
+
+
+EUNSUPPORTED = -2  # AANET_EUNSUPPORTED (include/aanet_mi355x.h)
 
 
 def lib():
@@ -98,7 +103,7 @@ def call(name, *args):
     if rc != 0:
         msg = lib().aanet_status_string(rc).decode()
         ints = [a for a in args if isinstance(a, int)]
-        raise AanetError(f"{name} failed: {msg} (status {rc}); integer args {ints}")
+        raise AanetError(f"{name} failed: {msg} (status {rc}); integer args {ints}", rc)
 
 
 def ptr(t):
@@ -140,11 +145,18 @@ def conv_flags(*packed):
     return 0
 
 
+class PostStage(ctypes.Structure):
+    """aanet_post_stage_t (include/aanet_mi355x.h)."""
+    _fields_ = [("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("act", ctypes.c_int),
+                ("out_nhwc", ctypes.c_void_p), ("disp", ctypes.c_void_p)]
+
+
 class CsaEpilogue(ctypes.Structure):
     """aanet_csa_epilogue_t (include/aanet_mi355x.h)."""
     _fields_ = [("out", ctypes.c_void_p), ("num_up", ctypes.c_int),
                 ("up", ctypes.c_void_p * 3), ("up_h", ctypes.c_int * 3),
-                ("up_w", ctypes.c_int * 3), ("act", ctypes.c_int)]
+                ("up_w", ctypes.c_int * 3), ("act", ctypes.c_int),
+                ("post", ctypes.POINTER(PostStage))]
 
 
 def stream_of(t):

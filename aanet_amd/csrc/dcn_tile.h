@@ -25,6 +25,17 @@ struct DcnTileArgs {
   float *csa_out;           // cross-scale sum output or NULL
   const float *up[2];
   int up_h[2], up_w[2], up_r[2], num_up, csa_act;
+  // optional post stage on the block's branch output v (csa_out's values when csa_out is set,
+  // else out's): the next pointwise conv of the path, so its input never makes a second HBM trip
+  //   t = post_w . v + post_b   (post_w: pre-split fragments of a [64][64] 1x1 weight, BN folded)
+  //   post_out (channels-last [N][H][W][64]) = post_act(t)          -- the next module's conv1
+  //   post_disp ([N][H][W]) = sum_d d softmax_d(t)                  -- final_conv + regression
+  // (either output may be NULL; needs Co2 == 64)
+  const void *post_wsplit;
+  const float *post_b;
+  int post_act;
+  float *post_out;
+  float *post_disp;
   int N, C, H, W, Co, Co2, dil, dg;
   int dbg;  // AANET_DCN_DBG timing-attribution switches (wrong results; tools/dcn_tile_bench.py)
 };

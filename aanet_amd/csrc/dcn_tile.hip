@@ -125,7 +125,7 @@ __device__ __forceinline__ TapState tap_state(float oh, float ow, float ml, int 
 // CG = channels per deformable group (two groups): 32 (scale 0: C = 64) or 16 (scale 1: C = 32).
 // A chunk is one tap of a 32-channel K slice ("phase"): with CG = 32 a phase is one group, with
 // CG = 16 it holds both groups (lane groups kr = 0, 1 carry group 0's channels, kr = 2, 3 group 1's).
-template <int DIL, int CG>
+template <int DIL, int CG, bool POST>
 __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   constexpr int CT = 2 * CG;             // channels = Co = Co2
   constexpr int NPH = CT / 32;           // phases
@@ -444,6 +444,8 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) sO[(16 * m2 + 4 * kr + r) * OP + wave * 16 + jj] = acc2[m2][r];
   __syncthreads();
+  // post stage: its own instantiation (POST), so the common form keeps its register allocation
+  constexpr bool post = POST && CT == 64;
   // every global load of the thread's items (the CSA terms' source segments; identity and bias
   // above) is issued before the first use: the item loop would otherwise pay one L2/HBM round
   // trip per item and term (the stores may alias the sources, so the compiler cannot hoist them)
@@ -472,6 +474,18 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
         eu[i][j][0] = load_seg(im + (long)h1 * iw, iw, s0);
         eu[i][j][1] = load_seg(im + (long)(h1 + h1p) * iw, iw, s0);
       }
+    }
+  }
+  // post stage (next pointwise conv): its A fragments into the A slots, free since the conv3 MFMAs
+  // (every wave passed the barrier before the item loops).  Issued here, after the items' loads:
+  // issued before them it raised the register pressure into main-loop spills
+  if (post) {
+    const char *src = reinterpret_cast<const char *>(a.post_wsplit) + lane * 16;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int pc = wave + 8 * r;  // 2 K chunks x 4 co blocks x 3 pieces
+      char *dst = pc < 12 ? sA0 + pc * 1024 : sA1 + (pc - 12) * 1024;
+      __builtin_amdgcn_global_load_lds((const void *)(src + pc * 1024), (lds_void *)dst, 16, 0, 0);
     }
   }
 #pragma unroll
@@ -503,7 +517,102 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       for (int u = 0; u < 4; ++u) v[u] = act_f(v[u], a.csa_act);
       *reinterpret_cast<f32x4 *>(a.csa_out + eo[i]) = v;
     }
+    if (post)  // the branch output back into the item's own slot: the post stage's B operand
+      *reinterpret_cast<f32x4 *>(sO + (e >> 5) * OP + (qi >> 2) * 16 + 4 * (qi & 3)) = v;
   }
+  if constexpr (!post) return;
+
+  // ---- post stage: next pointwise conv (+ act) -> NHWC, or final_conv -> soft-argmin ---------
+  // B of lane (kr, jj): channels {32h2 + 4kr + r, 32h2 + 16 + 4kr + r} of pixel (wave, jj), the
+  // conv3 K permutation (rows 4kr apart: 4 OP = 16 mod 32 banks, conflict-free)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's post-weight DMA landed ...
+  __syncthreads();                                   // ... every wave's, and every v slot written
+  // lane and pixel coordinates recomputed here (the asm hides tid from CSE): kept live from the
+  // prologue, they raised the main loop's register pressure into spills
+  int ptid = threadIdx.x;
+  asm volatile("" : "+v"(ptid));
+  const int plane_ = ptid & 63, pwave = __builtin_amdgcn_readfirstlane(ptid >> 6);
+  const int pkr = plane_ >> 4, pjj = plane_ & 15;
+  int pn, ppy, ppx;
+  {
+    const int tx2 = (W + TC - 1) / TC, nt2 = tx2 * ((H + TR - 1) / TR);
+    const int nwg2 = gridDim.x, bb = blockIdx.x, q82 = nwg2 >> 3, r82 = nwg2 & 7, xc2 = bb & 7;
+    const int bid2 = (xc2 < r82 ? xc2 * (q82 + 1) : r82 * (q82 + 1) + (xc2 - r82) * q82) + (bb >> 3);
+    const int t2 = bid2 % nt2;
+    pn = bid2 / nt2;
+    ppy = (t2 / tx2) * TR + pwave;
+    ppx = (t2 % tx2) * TC + pjj;
+  }
+  const bool ppv = ppy < H && ppx < W;
+  bf16x8 B3[2][3];
+#pragma unroll
+  for (int h2 = 0; h2 < 2; ++h2) {
+    float v[8];
+#pragma unroll
+    for (int half = 0; half < 2; ++half)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[4 * half + r] = sO[(32 * h2 + 16 * half + 4 * pkr + r) * OP + pwave * 16 + pjj];
+    split8(v, B3[h2]);
+  }
+  f32x4 acc3[4];
+  {
+    const int tl = (((pkr >> 1) << 4) | pjj) * 16 + 8 * (pkr & 1);
+#pragma unroll
+    for (int m3 = 0; m3 < 4; ++m3) {
+      acc3[m3] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        bf16x8 A[3];
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) {
+          const char *f = (h2 ? sA1 : sA0) + tl + (m3 * 3 + pc) * 1024;
+          const u32x2 lo = *reinterpret_cast<const u32x2 *>(f);
+          const u32x2 hi = *reinterpret_cast<const u32x2 *>(f + 512);
+          A[pc] = __builtin_bit_cast(bf16x8, u32x4{lo.x, lo.y, hi.x, hi.y});
+        }
+        acc3[m3] = mfma_split6(A, B3[h2], acc3[m3]);
+      }
+    }
+  }
+  // acc3[m3][r]: output channel 16 m3 + 4 pkr + r of pixel (ppy, ppx)
+#pragma unroll
+  for (int m3 = 0; m3 < 4; ++m3) {
+    const f32x4 pb = a.post_b ? *reinterpret_cast<const f32x4 *>(a.post_b + 16 * m3 + 4 * pkr)
+                              : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc3[m3][r] = act_f(acc3[m3][r] + pb[r], a.post_act);
+  }
+  if (a.post_out && ppv) {
+    float *po = a.post_out + ((long)(pn * H + ppy) * W + ppx) * 64 + 4 * pkr;
+#pragma unroll
+    for (int m3 = 0; m3 < 4; ++m3) *reinterpret_cast<f32x4 *>(po + 16 * m3) = acc3[m3];
+  }
+  if (a.post_disp) {
+    // soft-argmin over the 64 channels of the pixel (nets/estimation.ppy:13-30, similarity form):
+    // the four lanes pjj, pjj+16, pjj+32, pjj+48 hold 16 channels each
+    float mx = acc3[0][0];
+#pragma unroll
+    for (int m3 = 0; m3 < 4; ++m3)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc3[m3][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float z = 0.f, sacc = 0.f;
+#pragma unroll
+    for (int m3 = 0; m3 < 4; ++m3)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ev = __expf(acc3[m3][r] - mx);
+        z += ev;
+        sacc += ev * (float)(16 * m3 + 4 * pkr + r);
+      }
+    z += __shfl_xor(z, 16);
+    sacc += __shfl_xor(sacc, 16);
+    z += __shfl_xor(z, 32);
+    sacc += __shfl_xor(sacc, 32);
+    if (pkr == 0 && ppv) a.post_disp[(long)(pn * H + ppy) * W + ppx] = sacc / z;
+  }
+
 }
 
 int window_enabled() {
@@ -554,9 +663,12 @@ int dcn_tile_launch(const DcnTileArgs &a, hipStream_t stream) {
 #endif
   DcnTileArgs b = a;
   b.dbg = dbg;
-  if (a.C == 64)
-    hipLaunchKernelGGL((dcn_tile_kernel<2, 32>), dim3((unsigned)(a.N * tiles)), dim3(NT), 0, stream, b);
+  if (a.post_wsplit && a.C != 64) return AANET_EUNSUPPORTED;
+  if (a.C == 64 && a.post_wsplit)
+    hipLaunchKernelGGL((dcn_tile_kernel<2, 32, true>), dim3((unsigned)(a.N * tiles)), dim3(NT), 0, stream, b);
+  else if (a.C == 64)
+    hipLaunchKernelGGL((dcn_tile_kernel<2, 32, false>), dim3((unsigned)(a.N * tiles)), dim3(NT), 0, stream, b);
   else
-    hipLaunchKernelGGL((dcn_tile_kernel<2, 16>), dim3((unsigned)(a.N * tiles)), dim3(NT), 0, stream, b);
+    hipLaunchKernelGGL((dcn_tile_kernel<2, 16, false>), dim3((unsigned)(a.N * tiles)), dim3(NT), 0, stream, b);
   return aanet_launch_status();
 }

@@ -59,6 +59,7 @@ struct MdcnArgs {
   float *csa_out;
   const float *up[3];
   int up_h[3], up_w[3], up_r[3], num_up, csa_act;
+  const aanet_post_stage_t *post;  // post stage on csa_out (window DCN tail only; else unsupported)
 };
 
 // Bilinear sampling state of one (pixel, tap, deformable group).  Invalid corners get
@@ -2222,6 +2223,7 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
   a.csa_out = nullptr;
   a.num_up = 0;
   a.csa_act = 0;
+  a.post = nullptr;
   for (int j = 0; j < 3; ++j) {
     a.up[j] = nullptr;
     a.up_h[j] = a.up_w[j] = a.up_r[j] = 1;
@@ -2556,6 +2558,10 @@ __global__ void pack_split_kernel(const float *__restrict__ w, bf16x8_t *__restr
 
 int set_csa(MdcnArgs &a, const aanet_csa_epilogue_t *csa) {
   if (!csa) return AANET_OK;
+  a.post = csa->post;
+  if (a.post && ((!a.post->out_nhwc && !a.post->disp) || !a.post->weight || a.post->act < 0 ||
+                 a.post->act > 2))
+    return AANET_EINVAL;
   if (!csa->out || csa->num_up < 0 || csa->num_up > 3 || csa->act < 0 || csa->act > 2)
     return AANET_EINVAL;
   a.csa_out = csa->out;
@@ -2638,6 +2644,7 @@ extern "C" int aanet_conv2d_pw_f32(const float *x, const float *weight_packed, c
   a.layout = layout;
   const int rc = set_csa(a, csa);
   if (rc) return rc;
+  if (a.post) return AANET_EUNSUPPORTED;  // the plain tail has no post stage (caller runs it apart)
   a.tail_w = pw_weight_packed;
   a.tail_b = pw_bias;
   a.tail_act = pw_act;
@@ -2712,9 +2719,22 @@ extern "C" int aanet_mdcn_pw_f32(const float *x, const float *offset, long offse
     t.dil = dil;
     t.dg = dg;
     t.dbg = 0;
+    t.post_wsplit = nullptr;
+    t.post_b = nullptr;
+    t.post_act = 0;
+    t.post_out = t.post_disp = nullptr;
+    if (a.post) {
+      if (co2 != 64) return AANET_EUNSUPPORTED;
+      t.post_wsplit = reinterpret_cast<const char *>(a.post->weight) + split_frag_offset(64, 64, 1);
+      t.post_b = a.post->bias;
+      t.post_act = a.post->act;
+      t.post_out = a.post->out_nhwc;
+      t.post_disp = a.post->disp;
+    }
     const int rc2 = (a.csa_out && a.num_up > 2) ? AANET_EUNSUPPORTED : dcn_tile_launch(t, as_hip(stream));
     if (rc2 != AANET_EUNSUPPORTED) return rc2;
   }
+  if (a.post) return AANET_EUNSUPPORTED;  // the generic engine has no post stage
   return launch_fwd<1>(a, 1, as_hip(stream));
 }
 

@@ -157,7 +157,15 @@ class AANet(FoldCacheMixin, nn.Module):
         left_feature = self.feature_extraction(left_img)
         right_feature = self.feature_extraction(right_img)
         cost_volume = self.cost_volume_construction(left_feature, right_feature)
-        aggregation = self.aggregation(cost_volume)
-        disparity_pyramid = self.disparity_computation(aggregation)
+        disp = None
+        if isinstance(self.aggregation, AdaptiveAggregation):
+            # eval, one output scale: final_conv + the soft-argmin may run in the last tail
+            # kernel's epilogue (AdaptiveAggregation._run)
+            regress = (not self.aggregation.intermediate_supervision and not self.training and
+                       self.disparity_estimation.match_similarity)
+            aggregation, disp = self.aggregation._run(cost_volume, regress=regress)
+        else:
+            aggregation = self.aggregation(cost_volume)
+        disparity_pyramid = [disp] if disp is not None else self.disparity_computation(aggregation)
         disparity_pyramid += self.disparity_refinement(left_img, right_img, disparity_pyramid[-1])
         return disparity_pyramid

@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from ._fuse import FoldCacheMixin, conv_bn_act, s2_conv_ok, s2_pack, use_fused
+from ._fuse import FoldCacheMixin, conv_bn_act, folded, s2_conv_ok, s2_pack, use_fused
 from .deform import DeformSimpleBottleneck, SimpleBottleneck
 
 
@@ -36,6 +36,12 @@ def concurrent_scales():
     """AANET_CONCURRENT_SCALES=0 runs the whole eval aggregation on one stream (A/B switch);
     AANET_SIDE_STREAMS=1 puts every coarse scale on one shared side stream (round-2 schedule)."""
     return os.environ.get("AANET_CONCURRENT_SCALES", "1") != "0"
+
+
+def post_fusion():
+    """AANET_POST_FUSION=0 disables the tail kernels' post stage (the next module's conv1 and the
+    final_conv + regression in the previous tail kernel's epilogue): A/B switch."""
+    return os.environ.get("AANET_POST_FUSION", "1") != "0"
 
 
 def num_side_streams(num_scales):
@@ -166,7 +172,7 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
             return self._down(heads[i], i, 0, start=1)
         return self._down(x[0], i, 0)
 
-    def _forward_eval(self, x, streams=None, keep=None):
+    def _forward_eval(self, x, streams=None, keep=None, conv1_pre=None, post=None):
         """Eval ISA + CSA.  The coarser scales run first, so that their exchange terms for output
         branch 0 exist when the scale-0 bottleneck runs: its tail kernel then writes both the
         block output and the cross-scale sum of branch 0 (aanet_csa_epilogue_t), which removes
@@ -185,7 +191,11 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
         own streams, and with them the next module's coarse blocks and exchange terms: that is
         the dependency chain between two scale-0 tail kernels.  Tensors read
         across streams are appended to `keep` (alive until the caller joins the streams, so the
-        caching allocator cannot hand their memory to another stream)."""
+        caching allocator cannot hand their memory to another stream).
+
+        conv1_pre: the scale-0 bottleneck's conv1 output, already computed by the previous
+        module's tail kernel (its post stage); post: this module's scale-0 tail post stage (the
+        next module's conv1, or final_conv + regression), result in post["result"]."""
         S = len(self.branches)
         nout = len(self.fuse_layers)
         if streams is None:
@@ -196,8 +206,12 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
             terms = {(0, j): t for j, t in zip(range(1, S), up0)}
             for j in range(self.num_blocks - 1):
                 x[0] = self.branches[0][j](x[0])
+            ok = csa_epilogue_ok(x[0], up0)
             x[0], csa0 = self.branches[0][self.num_blocks - 1].forward_csa(
-                x[0], up0 if csa_epilogue_ok(x[0], up0) else None)
+                x[0], up0 if ok else None, conv1_out=conv1_pre if self.num_blocks == 1 else None,
+                post=post if ok else None)
+            if post is not None and not ok:
+                post["result"] = None
             return self._fuse_eval(x, {0: csa0} if csa0 is not None else {}, terms)
 
         main = streams[0]
@@ -225,8 +239,14 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
 
         for b in range(self.num_blocks - 1):
             x[0] = self.branches[0][b](x[0])
+        ok = csa_epilogue_ok(x[0], up0)
         x[0], csa0 = self.branches[0][self.num_blocks - 1].forward_csa(
-            x[0], up0 if csa_epilogue_ok(x[0], up0) else None, before_tail=join)
+            x[0], up0 if ok else None, before_tail=join,
+            conv1_out=conv1_pre if self.num_blocks == 1 else None, post=post if ok else None)
+        if post is not None and not ok:
+            post["result"] = None
+        if post is not None and post.get("result") is not None:
+            keep.extend(v for v in post["result"].values() if v is not None)
         keep.append(x[0])
         if "coarse" not in mark:  # the tail kernel did not take the block
             join()
@@ -284,12 +304,15 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
             x_fused.append(ops.csa_sum([t.contiguous() for t in terms], act="leaky"))
         return x_fused
 
-    def forward(self, x, streams=None, keep=None):
+    def forward(self, x, streams=None, keep=None, conv1_pre=None, post=None):
         """aggregation.py:375-402.  streams / keep: the concurrent-scale schedule of
-        AdaptiveAggregation (eval only, see _forward_eval)."""
+        AdaptiveAggregation (eval only, see _forward_eval); conv1_pre / post: the cross-module
+        pointwise fusions of AdaptiveAggregation (eval only)."""
         assert len(self.branches) == len(x)
         if self.num_scales > 1 and use_fused(self, x[0]) and getattr(self, "aanet_fuse_csa", True):
-            return self._forward_eval(x, streams, keep)
+            return self._forward_eval(x, streams, keep, conv1_pre, post)
+        if post is not None:
+            post["result"] = None
         if streams is not None:  # reference op sequence: one stream
             for st in streams[1:]:
                 streams[0].wait_stream(st)
@@ -355,8 +378,43 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
             if not self.intermediate_supervision:
                 break
 
+    def _post_for(self, i, regress):
+        """The post stage of fusion i's scale-0 tail kernel (eval, fused): the next module's
+        bottleneck conv1 + BN1 + ReLU (NHWC), or for the last fusion, with `regress`, final_conv +
+        the soft-argmin.  None when the shapes do not fit (64 channels at scale 0, 1x1, one
+        stage block)."""
+        if i + 1 < self.num_fusions:
+            nxt = self.fusions[i + 1]
+            if nxt.num_blocks != 1 or len(nxt.branches) == 0:
+                return None
+            blk = nxt.branches[0][0]
+            c1 = blk.conv1
+            if tuple(c1.weight.shape) != (64, 64, 1, 1):
+                return None
+            _, b1, p1 = folded(c1, blk.bn1)
+            if not getattr(p1, "_aanet_split", False):
+                return None
+            return {"packed": p1, "bias": b1, "act": "relu", "nhwc": True}
+        if not regress:
+            return None
+        fc = self.final_conv[0]
+        if tuple(fc.weight.shape) != (64, 64, 1, 1):
+            return None
+        _, bf, pf = folded(fc, None)
+        if not getattr(pf, "_aanet_split", False):
+            return None
+        return {"packed": pf, "bias": bf, "act": None, "disp": True}
+
     def forward(self, cost_volume):
         """aggregation.py:452-464 (final 1x1 conv with bias on the HIP conv engine in eval)."""
+        return self._run(cost_volume)[0]
+
+    def _run(self, cost_volume, regress=False):
+        """-> (aggregated cost volumes, disparity or None).  In eval on the fused path each
+        fusion's scale-0 tail kernel also computes the next fusion's conv1 (post stage); with
+        `regress` (the caller's DisparityEstimation is the plain similarity soft-argmin and there
+        is one output scale) the last tail computes final_conv + the regression too, and the
+        cost-volume list is then None."""
         assert isinstance(cost_volume, list)
         fused = use_fused(self, cost_volume[0])
         streams = None
@@ -369,17 +427,31 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
             for st in ss:
                 st.wait_stream(main)  # the cost volumes are written on the current stream
             keep = list(cost_volume)
+        pre, disp = None, None
+        post_ok = fused and cost_volume[0].is_cuda and post_fusion()
         for i in range(self.num_fusions):
             fusion = self.fusions[i]
-            cost_volume = fusion(cost_volume, streams, keep) if streams is not None else fusion(cost_volume)
+            post = self._post_for(i, regress) if post_ok else None
+            if streams is not None:
+                cost_volume = fusion(cost_volume, streams, keep, conv1_pre=pre, post=post)
+            elif post_ok:
+                cost_volume = fusion(cost_volume, conv1_pre=pre, post=post)
+            else:
+                cost_volume = fusion(cost_volume)
+            res = post.get("result") if post is not None else None
+            pre = res["out"] if res is not None else None
+            if res is not None and res.get("disp") is not None:
+                disp = res["disp"]
         if streams is not None:
             for st in ss:
                 main.wait_stream(st)
             del keep
+        if disp is not None:
+            return None, disp
         out = []  # 1/3, 1/6, 1/12
         for i in range(len(self.final_conv)):
             if fused:
                 out = out + [conv_bn_act(cost_volume[i], self.final_conv[i])]
             else:
                 out = out + [self.final_conv[i](cost_volume[i])]
-        return out
+        return out, None

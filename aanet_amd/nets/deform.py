@@ -102,6 +102,17 @@ class DeformConv2d(FoldCacheMixin, nn.Module):
                                       groups=dc.groups)
 
 
+def _take_post(r, post):
+    """(out, csa_out[, post results]) of a tail op -> (out, csa_out) or out, with the post
+    stage's results stored in post["result"]."""
+    if isinstance(r, tuple) and len(r) == 3:
+        post["result"] = r[2]
+        return r[0], r[1]
+    if post is not None:
+        post["result"] = None
+    return r
+
+
 class _BottleneckBase(FoldCacheMixin, nn.Module):
     def _forward_ref(self, x):
         identity = x
@@ -119,7 +130,7 @@ class _BottleneckBase(FoldCacheMixin, nn.Module):
         out = self.relu(out)
         return out
 
-    def _forward_fused(self, x, deform, conv1_out=None, csa_up=None, before_tail=None):
+    def _forward_fused(self, x, deform, conv1_out=None, csa_up=None, before_tail=None, post=None):
         """conv1+bn1+relu, then conv2+bn2+relu -> conv3+bn3 (+identity) + relu as ONE HIP kernel
         (the conv3 GEMM runs in conv2's epilogue).  When the tail kernel takes the block, conv1
         writes its output channels-last (NHWC) so that conv2 / offset_conv / the DCN read each
@@ -128,7 +139,9 @@ class _BottleneckBase(FoldCacheMixin, nn.Module):
         then also writes that branch's cross-scale sum, and (out, csa_out) is returned
         (csa_out None when the tail kernel does not take the block).  before_tail: called just
         before the tail kernel is launched (the stream join of the concurrent-scale schedule,
-        AdaptiveAggregation: csa_up is produced on the side stream)."""
+        AdaptiveAggregation: csa_up is produced on the side stream).  post (with csa_up): the
+        tail kernel's post stage on the CSA output (ops._post_stage); its results are stored in
+        post["result"] (None when the kernel did not take the stage)."""
         w3, b3, p3 = folded(self.conv3, self.bn3)
         width = self.conv1.weight.shape[0]
         c2 = self.conv2
@@ -154,10 +167,11 @@ class _BottleneckBase(FoldCacheMixin, nn.Module):
             if pw:
                 if before_tail is not None:
                     before_tail()
-                return ops.mdcn_pw(out, offset_mask, dc.weight, wp, dc.bias, ps, psh, "relu", p3, b3,
-                                   identity, "relu", dc.stride, dc.padding, dc.dilation,
-                                   c2.deformable_groups, 2.0 if c2.double_mask else 1.0,
-                                   csa_up=csa_up)
+                r = ops.mdcn_pw(out, offset_mask, dc.weight, wp, dc.bias, ps, psh, "relu", p3, b3,
+                                identity, "relu", dc.stride, dc.padding, dc.dilation,
+                                c2.deformable_groups, 2.0 if c2.double_mask else 1.0,
+                                csa_up=csa_up, post=post if csa_up is not None else None)
+                return _take_post(r, post)
             out = c2.forward_fused(out, self.bn2, act="relu")
         elif deform:
             out = F.relu_(self.bn2(self.conv2(out)))
@@ -166,17 +180,20 @@ class _BottleneckBase(FoldCacheMixin, nn.Module):
             if pw:
                 if before_tail is not None:
                     before_tail()
-                return ops.conv2d_pw(out, w2, p2, b2, None, None, "relu", p3, b3, identity, "relu",
-                                     c2.stride[0], c2.padding[0], c2.dilation[0], csa_up=csa_up)
+                r = ops.conv2d_pw(out, w2, p2, b2, None, None, "relu", p3, b3, identity, "relu",
+                                  c2.stride[0], c2.padding[0], c2.dilation[0], csa_up=csa_up,
+                                  post=post if csa_up is not None else None)
+                return _take_post(r, post)
             out = conv_bn_act(out, self.conv2, self.bn2, "relu")
         out = conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity)
         return out if csa_up is None else (out, None)
 
-    def forward_csa(self, x, csa_up, before_tail=None):
-        """Eval-only: (block output, its output branch's CSA sum or None); see _forward_fused."""
+    def forward_csa(self, x, csa_up, before_tail=None, conv1_out=None, post=None):
+        """Eval-only: (block output, its output branch's CSA sum or None); see _forward_fused.
+        conv1_out: this block's conv1 output, computed by the previous tail's post stage."""
         deform = isinstance(self, DeformSimpleBottleneck) or isinstance(self, DeformBottleneck)
         r = self._forward_fused(x, deform=deform, csa_up=None if csa_up is None else list(csa_up),
-                                before_tail=before_tail)
+                                before_tail=before_tail, conv1_out=conv1_out, post=post)
         return r if isinstance(r, tuple) else (r, None)
 
 

@@ -58,5 +58,13 @@ class AANetHotPath(FoldCacheMixin, nn.Module):
 
     def forward(self, left_feature, right_feature):
         cost_volume = self.cost_volume_construction(left_feature, right_feature)
-        aggregation = self.aggregation(cost_volume)
+        aggregation, disp = self.aggregation._run(cost_volume, regress=self.regress_in_tail())
+        if disp is not None:  # final_conv + soft-argmin ran in the last tail kernel's epilogue
+            return [disp]
         return self.disparity_computation(aggregation)
+
+    def regress_in_tail(self):
+        """Whether the last aggregation tail kernel may also run final_conv + the regression
+        (eval; one output scale; the similarity soft-argmin of nets/estimation.py:13-30)."""
+        return (not self.aggregation.intermediate_supervision and
+                self.disparity_estimation.match_similarity and not self.training)

@@ -313,6 +313,46 @@ def conv2d_fused(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1
     return out
 
 
+def _post_stage(out, post):
+    """(aanet_post_stage_t, {"out": NHWC tensor or None, "disp": tensor or None}) for a tail
+    kernel's post stage; post = dict(packed=<pack_weight_split buffer of a [64][64][1][1]
+    weight, BN folded>, bias=<[64] or None>, act="relu"/None, nhwc=bool, disp=bool)."""
+    if post is None:
+        return None, None
+    require_gpu(post["packed"], post.get("bias"))
+    N, _, H, W = out.shape
+    res = {"out": None, "disp": None}
+    ps = _lib.PostStage()
+    ps.weight = post["packed"].data_ptr()
+    ps.bias = 0 if post.get("bias") is None else post["bias"].data_ptr()
+    ps.act = ACT[post.get("act")]
+    if post.get("nhwc"):
+        res["out"] = torch.empty((N, 64, H, W), device=out.device, dtype=out.dtype,
+                                 memory_format=torch.channels_last)
+        ps.out_nhwc = res["out"].data_ptr()
+    if post.get("disp"):
+        res["disp"] = torch.empty((N, H, W), device=out.device, dtype=out.dtype)
+        ps.disp = res["disp"].data_ptr()
+    return ps, res
+
+
+def _call_tail(name, desc, ps, args_before, args_after):
+    """Call a tail kernel with its CSA descriptor; a post stage the kernel cannot take
+    (AANET_EUNSUPPORTED, returned before any launch) is dropped and the call repeated without
+    it.  -> whether the post stage ran."""
+    if desc is not None and ps is not None:
+        desc.post = _lib.ctypes.pointer(ps)
+        try:
+            call(name, *args_before, _lib.ctypes.byref(desc), *args_after)
+            return True
+        except _lib.AanetError as e:
+            if e.status != _lib.EUNSUPPORTED:
+                raise
+        desc.post = None
+    call(name, *args_before, None if desc is None else _lib.ctypes.byref(desc), *args_after)
+    return False
+
+
 def _csa_epilogue(out, csa_up, csa_act):
     """(aanet_csa_epilogue_t, its output) for the tail kernels; csa_up: the coarser exchange
     terms [n][co2][h/r][w/r] (r = 2 or 4) summed into this output branch."""
@@ -336,10 +376,12 @@ def _csa_epilogue(out, csa_up, csa_act):
 
 def conv2d_pw(x, weight, packed_weight, bias, post_scale, post_shift, act, pw_packed, pw_bias,
               residual=None, pw_act=None, stride=1, padding=0, dilation=1, csa_up=None,
-              csa_act="leaky"):
+              csa_act="leaky", post=None):
     """Plain conv + fused pointwise tail (bottleneck conv2 -> conv3, aanet_conv2d_pw_f32).
     x may be channels_last (NHWC staging); the output is NCHW.  csa_up (list of coarser
-    exchange terms): also return the CSA sum act(out + up(csa_up...)) -> (out, csa_out)."""
+    exchange terms): also return the CSA sum act(out + up(csa_up...)) -> (out, csa_out).
+    post (with csa_up; see _post_stage): -> (out, csa_out, post results or None when the kernel
+    did not take the stage)."""
     require_gpu(x, packed_weight, bias, post_scale, post_shift, pw_packed, pw_bias, residual,
                 nhwc_ok=(0,))
     N, C, H, W = x.shape
@@ -348,20 +390,25 @@ def conv2d_pw(x, weight, packed_weight, bias, post_scale, post_shift, act, pw_pa
     Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
     out = torch.empty((N, Co2, Ho, Wo), device=x.device, dtype=x.dtype)
     desc, csa_out = _csa_epilogue(out, csa_up, csa_act)
-    call("aanet_conv2d_pw_f32", ptr(x), ptr(packed_weight), ptr(bias), ptr(post_scale),
-         ptr(post_shift), ACT[act], ptr(pw_packed), ptr(pw_bias), ptr(residual), ACT[pw_act], Co2,
-         ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation,
-         None if desc is None else _lib.ctypes.byref(desc),
-         (_lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0) | _lib.conv_flags(packed_weight, pw_packed),
-         stream_of(x))
-    return out if desc is None else (out, csa_out)
+    ps, pres = _post_stage(out, post if desc is not None else None)
+    ran = _call_tail("aanet_conv2d_pw_f32",
+                     desc, ps,
+                     (ptr(x), ptr(packed_weight), ptr(bias), ptr(post_scale), ptr(post_shift),
+                      ACT[act], ptr(pw_packed), ptr(pw_bias), ptr(residual), ACT[pw_act], Co2,
+                      ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation),
+                     ((_lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0)
+                      | _lib.conv_flags(packed_weight, pw_packed), stream_of(x)))
+    if desc is None:
+        return out
+    return (out, csa_out) if post is None else (out, csa_out, pres if ran else None)
 
 
 def mdcn_pw(x, offset_mask, weight, packed_weight, bias, post_scale, post_shift, act, pw_packed,
             pw_bias, residual=None, pw_act=None, stride=1, padding=0, dilation=1,
-            deformable_groups=1, mask_scale=2.0, csa_up=None, csa_act="leaky", generic_dcn=False):
+            deformable_groups=1, mask_scale=2.0, csa_up=None, csa_act="leaky", generic_dcn=False,
+            post=None):
     """DCN (offset/mask read in place from offset_conv's output) + fused pointwise tail.
-    x may be channels_last (NHWC corner loads); the output is NCHW.  csa_up: as conv2d_pw.
+    x may be channels_last (NHWC corner loads); the output is NCHW.  csa_up, post: as conv2d_pw.
     generic_dcn: keep the generic engine where the LDS-window tail would run (A/B, tests)."""
     require_gpu(x, offset_mask, packed_weight, bias, post_scale, post_shift, pw_packed, pw_bias,
                 residual, nhwc_ok=(0,))
@@ -374,17 +421,21 @@ def mdcn_pw(x, offset_mask, weight, packed_weight, bias, post_scale, post_shift,
         raise ValueError(f"offset_mask shape {tuple(offset_mask.shape)} unexpected")
     out = torch.empty((N, Co2, Ho, Wo), device=x.device, dtype=x.dtype)
     desc, csa_out = _csa_epilogue(out, csa_up, csa_act)
+    ps, pres = _post_stage(out, post if desc is not None else None)
     bs = offset_mask.stride(0)
     mask_ptr = offset_mask.data_ptr() + 4 * deformable_groups * 2 * K * Ho * Wo
-    call("aanet_mdcn_pw_f32", ptr(x), ptr(offset_mask), bs, _lib.ctypes.c_void_p(mask_ptr), bs, 1,
-         float(mask_scale), ptr(packed_weight), ptr(bias), ptr(post_scale), ptr(post_shift),
-         ACT[act], ptr(pw_packed), ptr(pw_bias), ptr(residual), ACT[pw_act], Co2, ptr(out), N, C,
-         H, W, Co, kh, kw, stride, padding, dilation, deformable_groups,
-         None if desc is None else _lib.ctypes.byref(desc),
-         (_lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0) | _lib.conv_flags(packed_weight, pw_packed)
-         | (_lib.CONV_GENERIC_DCN if generic_dcn else 0),
-         stream_of(x))
-    return out if desc is None else (out, csa_out)
+    ran = _call_tail("aanet_mdcn_pw_f32", desc, ps,
+                     (ptr(x), ptr(offset_mask), bs, _lib.ctypes.c_void_p(mask_ptr), bs, 1,
+                      float(mask_scale), ptr(packed_weight), ptr(bias), ptr(post_scale),
+                      ptr(post_shift), ACT[act], ptr(pw_packed), ptr(pw_bias), ptr(residual),
+                      ACT[pw_act], Co2, ptr(out), N, C, H, W, Co, kh, kw, stride, padding,
+                      dilation, deformable_groups),
+                     ((_lib.LAYOUT_IN_NHWC if _lib.is_nhwc(x) else 0)
+                      | _lib.conv_flags(packed_weight, pw_packed)
+                      | (_lib.CONV_GENERIC_DCN if generic_dcn else 0), stream_of(x)))
+    if desc is None:
+        return out
+    return (out, csa_out) if post is None else (out, csa_out, pres if ran else None)
 
 
 def pack_conv3x3s2(weight):

@@ -165,12 +165,31 @@ int aanet_conv2d_fused_f32(const float *x, const float *weight, const float *bia
  * (up_h * r == ho and up_w * r == wo); each up[j] is [n][co2][up_h][up_w].  Needs wo % 4 == 0
  * and num_up <= 2 in this build (AANET_EUNSUPPORTED otherwise; 3 scales give at most 2 terms).
  * act: 0 none, 1 ReLU, 2 LeakyReLU(0.2). */
+/* Post stage of the CSA epilogue (round 3): the next pointwise conv of the path applied to the
+ * CSA output in the same kernel, so the branch output is not read back from HBM:
+ *   t = weight . csa_out + bias                (1x1, 64 -> 64 channels, BN folded by the caller)
+ *   out_nhwc[n][y][x][:] = act(t)              -- the next AAModule's bottleneck conv1 + BN1 + ReLU
+ *                                                 (nets/deform.py:207-209), channels-last
+ *   disp[n][y][x] = sum_d d * softmax_d(t)     -- final_conv (nets/aggregation.py:443-447) +
+ *                                                 DisparityEstimation (nets/estimation.py:13-30)
+ * weight: an aanet_conv_weight_pack_split_f32 buffer of the [64][64][1][1] weight.  Either output
+ * may be NULL.  Tail kernels that cannot run it return AANET_EUNSUPPORTED (the caller then runs
+ * the stage as separate kernels). */
+typedef struct {
+  const void *weight;
+  const float *bias;
+  int act;
+  float *out_nhwc;
+  float *disp;
+} aanet_post_stage_t;
+
 typedef struct {
   float *out;
   int num_up;
   const float *up[3];
   int up_h[3], up_w[3];
   int act;
+  const aanet_post_stage_t *post; /* optional post stage on out (NULL: none) */
 } aanet_csa_epilogue_t;
 
 /* Bottleneck tail fusion (nets/deform.py:171-184 / 223-236 in eval): the pointwise conv3

@@ -157,6 +157,24 @@ def test_shift_volume_c5_shape_and_backward(concat):
     close(t2n(Rt.grad), gr, 1e-5, 1e-5, "grad_right")
 
 
+@pytest.mark.parametrize("concat", [True, False])
+def test_shift_volume_c5_full_size_bit_exact(concat):
+    """BASELINE configs[4] (PSMNet-AA / GwcNet-AA concat path) at its own size: PSMNet features
+    [1,32,96,312] (384x1248 at 1/4), D = 192/4 = 48 -> [1,64,48,96,312] (368 MB) / [1,32,48,...],
+    bit-exact against the oracle over the whole volume (nets/cost.py:22-38), plus the x < d zero
+    fill checked directly."""
+    rng = np.random.default_rng(55)
+    B, C, H, W, D = 1, 32, 96, 312, 48
+    L = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    R = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    out = t2n(ops.shift_volume(g2t(L), g2t(R), D, concat))
+    ref = (oracle.concat_volume if concat else oracle.diff_volume)(L, R, D)
+    assert out.shape == ref.shape == ((B, 2 * C, D, H, W) if concat else (B, C, D, H, W))
+    assert np.array_equal(out, ref)
+    for d in (1, 17, 47):
+        assert not out[:, :, d, :, :d].any()
+
+
 # --------------------------------------------------------------------- regression --------
 @pytest.mark.parametrize("name", golden_names("regress_"))
 def test_regression_vs_reference_golden(name):

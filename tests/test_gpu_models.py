@@ -83,8 +83,11 @@ def test_full_model_vs_reference_golden(tag, fuse):
     against the reference's fp32 output."""
     g, m, left, right = build(tag, fuse)
     # the reference-order run puts every conv on MIOpen: deterministic algorithms, so the result
-    # does not move with MIOpen's per-run algorithm choice (p99 moved 0.026-0.035 px on PSMNet-AA)
-    with torch.no_grad(), torch.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=True):
+    # does not move with MIOpen's per-run algorithm choice (p99 moved 0.026-0.035 px on PSMNet-AA),
+    # and no TF32 (cudnn.flags() would re-enable it: on gfx950 MIOpen's TF32 convolutions gave
+    # PSMNet-AA 2.8x the reference's own near-tie flips; fp32: 1.05x, tools/flip_report.py)
+    with torch.no_grad(), torch.backends.cudnn.flags(enabled=True, benchmark=False,
+                                                     deterministic=True, allow_tf32=False):
         pyr = m(left, right)
     n = len([k for k in g if k.startswith("disp") and not k.startswith("disp64")])
     assert len(pyr) == n
@@ -97,10 +100,9 @@ def test_full_model_vs_reference_golden(tag, fuse):
         e64 = _stats(np.abs(ours - ref64))
         sens = _stats(np.abs(ref32.astype(np.float64) - ref64))
         report.append((i, e32, e64, sens))
-        # p99 within 2x the reference's own fp32 distance; the mean within 2.5x (on PSMNet-AA it
-        # is a count of sparse near-tie flips: 2.0-2.1x run to run on the reference-order path);
-        # the max (a single flip, a noisy one-sample statistic) within 4x
-        for got, bound, k, slack in zip(e64, sens, (2.5, 2, 4), (1e-5, 1e-4, 1e-3)):
+        # mean and p99 within 2x the reference's own fp32 distance; the max (a single near-tie
+        # flip, a noisy one-sample statistic) within 4x
+        for got, bound, k, slack in zip(e64, sens, (2, 2, 4), (1e-5, 1e-4, 1e-3)):
             assert got <= k * bound + slack, (i, "vs fp64", e64, "ref fp32 vs fp64", sens)
         if tag in STRICT:
             assert e32[2] <= 1e-3, (i, e32)
