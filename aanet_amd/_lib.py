@@ -148,7 +148,8 @@ def conv_flags(*packed):
 class PostStage(ctypes.Structure):
     """aanet_post_stage_t (include/aanet_mi355x.h)."""
     _fields_ = [("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("act", ctypes.c_int),
-                ("out_nhwc", ctypes.c_void_p), ("disp", ctypes.c_void_p)]
+                ("out_nhwc", ctypes.c_void_p), ("disp", ctypes.c_void_p),
+                ("skip_outputs", ctypes.c_int)]
 
 
 class CsaEpilogue(ctypes.Structure):

@@ -36,6 +36,7 @@ struct DcnTileArgs {
   int post_act;
   float *post_out;
   float *post_disp;
+  int post_skip;  // the post stage's outputs only (out / csa_out not stored)
   int N, C, H, W, Co, Co2, dil, dg;
   int dbg;  // AANET_DCN_DBG timing-attribution switches (wrong results; tools/dcn_tile_bench.py)
 };

@@ -503,7 +503,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       if (res) t += er[i][u];
       v[u] = act_f(t, a.tail_act);
     }
-    *reinterpret_cast<f32x4 *>(a.out + eo[i]) = v;
+    if (!post || !a.post_skip) *reinterpret_cast<f32x4 *>(a.out + eo[i]) = v;
     if (csa) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -515,7 +515,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) v[u] = act_f(v[u], a.csa_act);
-      *reinterpret_cast<f32x4 *>(a.csa_out + eo[i]) = v;
+      if (!post || !a.post_skip) *reinterpret_cast<f32x4 *>(a.csa_out + eo[i]) = v;
     }
     if (post)  // the branch output back into the item's own slot: the post stage's B operand
       *reinterpret_cast<f32x4 *>(sO + (e >> 5) * OP + (qi >> 2) * 16 + 4 * (qi & 3)) = v;

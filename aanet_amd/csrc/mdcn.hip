@@ -403,8 +403,10 @@ __device__ __forceinline__ f32x4 mfma_split6(const bf16x8 (&A)[3], const bf16x8 
 // stored to LDS ONCE, and all nine taps read their B operand from it at shifted positions (the
 // im2col form stages, splits and synchronises once per tap).  The next chunk's halo is in flight
 // in registers during the nine taps; A fragments are double-buffered across taps.
+// POST (HALO 1/2 tails with the CSA epilogue, CO_T = Co2 = 64): the post stage of
+// aanet_post_stage_t on the CSA output, NHWC out only (the next module's conv1).
 template <int MODE, int CO_T, int PTT, int PACKED, int TAIL, int SCHED, int FULL, int LAYOUT,
-          int CFG = 0, int PREC = 0, int HALO = 0>
+          int CFG = 0, int PREC = 0, int HALO = 0, int POST = 0>
 __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   constexpr int CK = CFG == 1 ? 16 : 32;   // channels per K chunk
   constexpr int GPC = CFG == 2 ? 2 : 1;    // deformable groups per chunk
@@ -1225,6 +1227,8 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) v[u] = apply_act(v[u], a.csa_act);
         *reinterpret_cast<f32x4 *>(a.csa_out + o) = v;
+        // post stage: the CSA output back into the item's own slot (its B operand)
+        if constexpr (POST) *reinterpret_cast<f32x4 *>(sO + col * OP + 4 * q) = v;
       }
     }
   }
@@ -1246,6 +1250,69 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
         if (esc) t = t * sc + sh;
         if (a.residual) t += a.residual[o];
         a.out[o] = apply_act(t, eact);
+      }
+    }
+  }
+  if constexpr (POST && TAIL && HALO && CO_T == 64 && PTT == 128 && SPL) {
+    // ---- post stage (aanet_post_stage_t, NHWC out): t = W . csa + b, act, channels-last ------
+    // The wave keeps its (co blocks wc0.., px blocks wp0..) layout.  B of lane (kr, jj): channels
+    // {32h2 + 4kr + r, 32h2 + 16 + 4kr + r} of the pixel (rows 4kr apart in sO: 4 OP = 16 mod 32
+    // banks); A: the same permutation read from the standard fragments in global memory.
+    __syncthreads();  // every item's CSA value is in sO
+    bf16x8 pb3[NPB][2][3];
+#pragma unroll
+    for (int b = 0; b < NPB; ++b)
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        f32x4 lo4, hi4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          lo4[r] = sO[(32 * h2 + 4 * kr + r) * OP + 16 * (wp0 + b) + jj];
+          hi4[r] = sO[(32 * h2 + 16 + 4 * kr + r) * OP + 16 * (wp0 + b) + jj];
+        }
+        bf16x4 h0, m0, l0, h1, m1, l1;
+        split3(lo4, h0, m0, l0);
+        split3(hi4, h1, m1, l1);
+        pb3[b][h2][0] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+        pb3[b][h2][1] = __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7);
+        pb3[b][h2][2] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    const char *pw = reinterpret_cast<const char *>(a.post->weight) + split_frag_offset(64, 64, 1) +
+                     ((((kr >> 1) << 4) | jj) * 16 + 8 * (kr & 1));
+    typedef unsigned pu32x2 __attribute__((ext_vector_type(2)));
+    typedef unsigned pu32x4 __attribute__((ext_vector_type(4)));
+    f32x4 pacc[NCB][NPB];
+#pragma unroll
+    for (int m = 0; m < NCB; ++m) {
+#pragma unroll
+      for (int b = 0; b < NPB; ++b) pacc[m][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        bf16x8 A[3];
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) {
+          const char *f = pw + ((h2 * 4 + wc0 + m) * 3 + pc) * 1024;
+          const pu32x2 lo = *reinterpret_cast<const pu32x2 *>(f);
+          const pu32x2 hi = *reinterpret_cast<const pu32x2 *>(f + 512);
+          A[pc] = __builtin_bit_cast(bf16x8, pu32x4{lo.x, lo.y, hi.x, hi.y});
+        }
+#pragma unroll
+        for (int b = 0; b < NPB; ++b) pacc[m][b] = mfma_split6(A, pb3[b][h2], pacc[m][b]);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < NCB; ++m) {
+      const int co = 16 * (wc0 + m) + 4 * kr;
+      const f32x4 bb = a.post->bias ? *reinterpret_cast<const f32x4 *>(a.post->bias + co)
+                                    : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int b = 0; b < NPB; ++b) {
+        const long pe = pix(16 * (wp0 + b) + jj);
+        if (pe < 0) continue;
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = apply_act(pacc[m][b][r] + bb[r], a.post->act);
+        *reinterpret_cast<f32x4 *>(a.post->out_nhwc + ((long)n * P + pe) * 64 + co) = v;
       }
     }
   }
@@ -2268,7 +2335,9 @@ void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
     if constexpr (MODE == 0 && PTT == 128) {
       if (a.split && packed && a.halo == 1) {  // 3x3 stride-1 halo-tile form (NHWC input), HALO = dil
         if (a.dil == 1) {
-          if (a.tail_w)
+          if (a.tail_w && a.post && CO_T == 64)
+            hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 1, 1, 1, 1, CFG, 1, 1, 1>), grid, blk, 0, st, a);
+          else if (a.tail_w)
             hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 1, 1, 1, 1, CFG, 1, 1>), grid, blk, 0, st, a);
           else if (a.layout == 3)
             hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 0, 1, 1, 3, CFG, 1, 1>), grid, blk, 0, st, a);
@@ -2389,6 +2458,11 @@ int launch_fwd(const MdcnArgs &a_in, int packed, hipStream_t st) {
   a.halo = !nohalo && MODE == 0 && a.split && packed && (a.layout & 1) && a.kh == 3 && a.kw == 3 &&
            a.stride == 1 && a.pad == a.dil && a.dil <= 2 && co_t >= 32 && full_cfg(a, 0, co_t) == 0;
   if (a.halo) ptt = 128;
+  // post stage (aanet_post_stage_t): the HALO 1 tail with the CSA epilogue, 64 -> 64 channels,
+  // NHWC output only; anything else is left to the caller before any launch
+  if (a.post && (MODE != 0 || !a.csa_out || !a.halo || a.dil != 1 || co_t != 64 || a.Co2 != 64 ||
+                 a.post->disp || !a.post->out_nhwc || a.post->skip_outputs || !a.split || !packed))
+    return AANET_EUNSUPPORTED;
   // stride-2 halo form (the CSA down-sampling convs, aggregation.py:364-372): NCHW input.  Opt-in
   // (AANET_HALO_S2=1): alone it is 9-16 % faster than the im2col form at the C2 scale-0 shapes,
   // but in the two-stream eval schedule its 57 KB workgroups take LDS from the scale-0 chain's
@@ -2644,7 +2718,6 @@ extern "C" int aanet_conv2d_pw_f32(const float *x, const float *weight_packed, c
   a.layout = layout;
   const int rc = set_csa(a, csa);
   if (rc) return rc;
-  if (a.post) return AANET_EUNSUPPORTED;  // the plain tail has no post stage (caller runs it apart)
   a.tail_w = pw_weight_packed;
   a.tail_b = pw_bias;
   a.tail_act = pw_act;
@@ -2723,6 +2796,7 @@ extern "C" int aanet_mdcn_pw_f32(const float *x, const float *offset, long offse
     t.post_b = nullptr;
     t.post_act = 0;
     t.post_out = t.post_disp = nullptr;
+    t.post_skip = 0;
     if (a.post) {
       if (co2 != 64) return AANET_EUNSUPPORTED;
       t.post_wsplit = reinterpret_cast<const char *>(a.post->weight) + split_frag_offset(64, 64, 1);
@@ -2730,6 +2804,7 @@ extern "C" int aanet_mdcn_pw_f32(const float *x, const float *offset, long offse
       t.post_act = a.post->act;
       t.post_out = a.post->out_nhwc;
       t.post_disp = a.post->disp;
+      t.post_skip = a.post->skip_outputs != 0;
     }
     const int rc2 = (a.csa_out && a.num_up > 2) ? AANET_EUNSUPPORTED : dcn_tile_launch(t, as_hip(stream));
     if (rc2 != AANET_EUNSUPPORTED) return rc2;

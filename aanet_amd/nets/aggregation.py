@@ -403,7 +403,8 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
         _, bf, pf = folded(fc, None)
         if not getattr(pf, "_aanet_split", False):
             return None
-        return {"packed": pf, "bias": bf, "act": None, "disp": True}
+        # the last module's block output and CSA sum feed nothing but final_conv: not stored
+        return {"packed": pf, "bias": bf, "act": None, "disp": True, "skip_outputs": True}
 
     def forward(self, cost_volume):
         """aggregation.py:452-464 (final 1x1 conv with bias on the HIP conv engine in eval)."""

@@ -316,7 +316,8 @@ def conv2d_fused(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1
 def _post_stage(out, post):
     """(aanet_post_stage_t, {"out": NHWC tensor or None, "disp": tensor or None}) for a tail
     kernel's post stage; post = dict(packed=<pack_weight_split buffer of a [64][64][1][1]
-    weight, BN folded>, bias=<[64] or None>, act="relu"/None, nhwc=bool, disp=bool)."""
+    weight, BN folded>, bias=<[64] or None>, act="relu"/None, nhwc=bool, disp=bool,
+    skip_outputs=bool: the tail's own outputs are left unwritten)."""
     if post is None:
         return None, None
     require_gpu(post["packed"], post.get("bias"))
@@ -326,6 +327,7 @@ def _post_stage(out, post):
     ps.weight = post["packed"].data_ptr()
     ps.bias = 0 if post.get("bias") is None else post["bias"].data_ptr()
     ps.act = ACT[post.get("act")]
+    ps.skip_outputs = int(bool(post.get("skip_outputs")))
     if post.get("nhwc"):
         res["out"] = torch.empty((N, 64, H, W), device=out.device, dtype=out.dtype,
                                  memory_format=torch.channels_last)

@@ -181,6 +181,8 @@ typedef struct {
   int act;
   float *out_nhwc;
   float *disp;
+  int skip_outputs; /* 1: the tail's out / csa out are not stored (only the post stage's are;
+                       the last module with disp: nothing else reads them) */
 } aanet_post_stage_t;
 
 typedef struct {

@@ -57,21 +57,33 @@ def test_dcn_tail_post_stage_matches_separate_kernels(kind):
         ref = ops.disp_regress(t)
         err = (pres["disp"] - ref).abs().max().item()
         assert err <= 1e-4, err
+        # skip_outputs: the same disparities, the tail's own outputs left unwritten
+        post_s = dict(post, skip_outputs=True)
+        _, _, pres_s = ops.mdcn_pw(x, om, w3, p3, None, b, b, "relu", p1, b, res, "relu", 1, 2, 2,
+                                   2, csa_up=ups, post=post_s)
+        assert torch.equal(pres_s["disp"], pres["disp"])
 
 
-def test_plain_tail_post_stage_falls_back():
-    """The plain 3x3 tail without a post stage implementation: the op repeats the call without
-    it and reports None (the caller then runs the stage itself)."""
-    x, res, w3, w1, b, om, ups, wn, bn_ = _tail_inputs()
-    w2 = torch.randn(64, 64, 3, 3, device=DEV) * 0.04
+def test_plain_tail_post_stage_matches_separate_kernel():
+    """The plain 3x3 halo tail (SimpleBottleneck, nets/deform.py:171-184) with the conv1 post
+    stage; the regression form is not implemented there: the op repeats the call without it and
+    reports None (the caller then runs the stage itself)."""
+    x, res, w3, w1, b, om, ups, wn, bn_ = _tail_inputs(seed=3)
+    w2 = torch.randn(64, 64, 3, 3, device=DEV, generator=torch.Generator(device=DEV).manual_seed(4)) * 0.04
     p2, p1, pn = ops.pack_weight_split(w2), ops.pack_weight_split(w1), ops.pack_weight_split(wn)
+    out, csa, pres = ops.conv2d_pw(x, w2, p2, b, None, None, "relu", p1, b, res, "relu", 1, 1, 1,
+                                   csa_up=ups,
+                                   post={"packed": pn, "bias": bn_, "act": "relu", "nhwc": True})
+    assert pres is not None, "the halo tail must take the conv1 post stage at this shape"
+    out0, csa0 = ops.conv2d_pw(x, w2, p2, b, None, None, "relu", p1, b, res, "relu", 1, 1, 1,
+                               csa_up=ups)
+    assert torch.equal(out, out0) and torch.equal(csa, csa0)
+    t = ops.conv2d_fused(csa0, wn, bn_, packed_weight=pn, act="relu")
+    err = (pres["out"] - t).abs().max().item()
+    assert err <= 2e-5 * max(1.0, t.abs().max().item()), err
     r = ops.conv2d_pw(x, w2, p2, b, None, None, "relu", p1, b, res, "relu", 1, 1, 1, csa_up=ups,
-                      post={"packed": pn, "bias": bn_, "act": "relu", "nhwc": True})
-    assert len(r) == 3
-    if r[2] is None:
-        out0, csa0 = ops.conv2d_pw(x, w2, p2, b, None, None, "relu", p1, b, res, "relu", 1, 1, 1,
-                                   csa_up=ups)
-        assert torch.equal(r[0], out0) and torch.equal(r[1], csa0)
+                      post={"packed": pn, "bias": bn_, "act": None, "disp": True})
+    assert r[2] is None and torch.equal(r[0], out0) and torch.equal(r[1], csa0)
 
 
 def test_hot_path_post_fusion_matches_unfused(monkeypatch):
