@@ -59,7 +59,12 @@ struct MdcnArgs {
   float *csa_out;
   const float *up[3];
   int up_h[3], up_w[3], up_r[3], num_up, csa_act;
-  const aanet_post_stage_t *post;  // post stage on csa_out (window DCN tail only; else unsupported)
+  const aanet_post_stage_t *post;  // HOST pointer (launch checks only): the post stage on csa_out
+  // its fields for the device (HALO 1 tail, POST instantiation)
+  const char *post_w;     // split fragments of the [64][64] 1x1 weight
+  const float *post_b;
+  int post_act;
+  float *post_out;        // NHWC [N][Ho][Wo][64]
 };
 
 // Bilinear sampling state of one (pixel, tap, deformable group).  Invalid corners get
@@ -1277,8 +1282,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
         pb3[b][h2][1] = __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7);
         pb3[b][h2][2] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
       }
-    const char *pw = reinterpret_cast<const char *>(a.post->weight) + split_frag_offset(64, 64, 1) +
-                     ((((kr >> 1) << 4) | jj) * 16 + 8 * (kr & 1));
+    const char *pw = a.post_w + ((((kr >> 1) << 4) | jj) * 16 + 8 * (kr & 1));
     typedef unsigned pu32x2 __attribute__((ext_vector_type(2)));
     typedef unsigned pu32x4 __attribute__((ext_vector_type(4)));
     f32x4 pacc[NCB][NPB];
@@ -1303,16 +1307,16 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
 #pragma unroll
     for (int m = 0; m < NCB; ++m) {
       const int co = 16 * (wc0 + m) + 4 * kr;
-      const f32x4 bb = a.post->bias ? *reinterpret_cast<const f32x4 *>(a.post->bias + co)
-                                    : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 bb = a.post_b ? *reinterpret_cast<const f32x4 *>(a.post_b + co)
+                                : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int b = 0; b < NPB; ++b) {
         const long pe = pix(16 * (wp0 + b) + jj);
         if (pe < 0) continue;
         f32x4 v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = apply_act(pacc[m][b][r] + bb[r], a.post->act);
-        *reinterpret_cast<f32x4 *>(a.post->out_nhwc + ((long)n * P + pe) * 64 + co) = v;
+        for (int r = 0; r < 4; ++r) v[r] = apply_act(pacc[m][b][r] + bb[r], a.post_act);
+        *reinterpret_cast<f32x4 *>(a.post_out + ((long)n * P + pe) * 64 + co) = v;
       }
     }
   }
@@ -2291,6 +2295,10 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
   a.num_up = 0;
   a.csa_act = 0;
   a.post = nullptr;
+  a.post_w = nullptr;
+  a.post_b = nullptr;
+  a.post_act = 0;
+  a.post_out = nullptr;
   for (int j = 0; j < 3; ++j) {
     a.up[j] = nullptr;
     a.up_h[j] = a.up_w[j] = a.up_r[j] = 1;
@@ -2636,6 +2644,12 @@ int set_csa(MdcnArgs &a, const aanet_csa_epilogue_t *csa) {
   if (a.post && ((!a.post->out_nhwc && !a.post->disp) || !a.post->weight || a.post->act < 0 ||
                  a.post->act > 2))
     return AANET_EINVAL;
+  if (a.post) {  // copied by value: the kernel never dereferences the host descriptor
+    a.post_w = reinterpret_cast<const char *>(a.post->weight) + split_frag_offset(64, 64, 1);
+    a.post_b = a.post->bias;
+    a.post_act = a.post->act;
+    a.post_out = a.post->out_nhwc;
+  }
   if (!csa->out || csa->num_up < 0 || csa->num_up > 3 || csa->act < 0 || csa->act > 2)
     return AANET_EINVAL;
   a.csa_out = csa->out;
