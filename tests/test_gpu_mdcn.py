@@ -308,3 +308,23 @@ def test_mdcn_backward_window_form_vs_oracle(case, window, monkeypatch):
             err = np.abs(t2n(gt) - r)
             scale = np.abs(r).max() + 1e-12
             assert err.max() <= 1e-4 * scale + 1e-6, f"{name} det={det}: max err {err.max():.3g}"
+
+
+@pytest.mark.parametrize("form", ["atomic", "window", "deterministic"])
+def test_mdcn_backward_c4_agg_s0_vs_oracle(form, monkeypatch):
+    """SURVEY C4 at the aggregation's scale-0 shape: one image of 64 channels at 128x416,
+    dg 2, 3x3, dil 2 (the C2 bottleneck DCN), against the oracle, for the float-atomic
+    (NHWC workspace scatter), LDS-window float (AANET_DCN_BWD_WINDOW=2) and fixed-point
+    deterministic forms.  Grids ~100x those of BWD_CASES (deform_conv_cuda_kernel.cu:635-767)."""
+    N, C, H, W, Co, k, s, p, d, dg = 1, 64, 128, 416, 64, 3, 1, 2, 2, 2
+    x, off, msk, w, b = make_case(11, N, C, H, W, Co, k, s, p, d, dg, off_scale=0.7)
+    go = np.random.default_rng(12).standard_normal((N, Co, H, W)).astype(np.float32)
+    if form == "window":
+        monkeypatch.setenv("AANET_DCN_BWD_WINDOW", "2")
+    got = ops.mdcn_backward(g2t(x), g2t(off), g2t(msk), g2t(w), g2t(go), True, s, p, d, 1, dg,
+                            deterministic=form == "deterministic")
+    ref = oracle.mdcn_backward(x, off, msk, w, go, True, s, p, d, 1, dg)
+    for name, gt, r in zip(("grad_input", "grad_offset", "grad_mask", "grad_weight", "grad_bias"), got, ref):
+        err = np.abs(t2n(gt) - r)
+        scale = np.abs(r).max() + 1e-12
+        assert err.max() <= 1e-4 * scale + 1e-6, f"{form} {name}: max err {err.max():.3g} (scale {scale:.3g})"

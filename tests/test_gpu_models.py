@@ -65,6 +65,7 @@ def build(tag, fuse=True):
 
 # the north-star models: held to the 1e-3 px bar against the reference's fp32 output itself
 STRICT = {"model_aanet", "model_aanet_inter", "model_aanetplus"}
+FLIP = 0.05  # px: a near-tie soft-argmin flip
 
 
 def _stats(e):
@@ -79,8 +80,16 @@ def test_full_model_vs_reference_golden(tag, fuse):
     (PSMNet's 25 un-normalised residual blocks turn it into sparse 0.1-0.7 px flips of near-tie
     soft-argmins -- in the reference's OWN fp32 run, measured against its fp64 run), so the
     test holds our fp32 result to the exact (fp64) answer no worse than the reference's own fp32
-    distance times 2 (mean, p99) / 4 (max), and the AANet / AANet+ models additionally to max 1e-3 px
-    against the reference's fp32 output."""
+    distance, per level:
+      * flips (|d - d64| > 0.05 px): at most 2x the reference's count + 4;
+      * mean over the pixels that neither run flips: at most 2x the reference's;
+      * p99 within 2x, max (a single flip, a one-sample statistic) within 4x;
+    and the AANet / AANet+ models additionally to max 1e-3 px against the reference's fp32 output.
+    The whole-level mean mixed the two: at PSMNet-AA's 1/3 level (4096 px) it is 3 flips of
+    0.2-0.45 px, so ONE extra flip moved it from 1.2e-4 to 2.3e-4 against a 2.3e-4 bound
+    (r02/r03 failures).  Counted instead: fused 3 / 33 / 633 flips, reference order 2 / 39 / 735,
+    the reference's own fp32 3 / 29 / 697 (levels 0-2); with MIOpen's TF32 convolutions the
+    reference order had 4 / 137 / 1966, which this bound rejects (tools/flip_report.py)."""
     g, m, left, right = build(tag, fuse)
     # the reference-order run puts every conv on MIOpen: deterministic algorithms, so the result
     # does not move with MIOpen's per-run algorithm choice (p99 moved 0.026-0.035 px on PSMNet-AA),
@@ -100,9 +109,17 @@ def test_full_model_vs_reference_golden(tag, fuse):
         e64 = _stats(np.abs(ours - ref64))
         sens = _stats(np.abs(ref32.astype(np.float64) - ref64))
         report.append((i, e32, e64, sens))
-        # mean and p99 within 2x the reference's own fp32 distance; the max (a single near-tie
-        # flip, a noisy one-sample statistic) within 4x
-        for got, bound, k, slack in zip(e64, sens, (2, 2, 4), (1e-5, 1e-4, 1e-3)):
+
+        err64 = np.abs(ours - ref64)
+        errref = np.abs(ref32.astype(np.float64) - ref64)
+        flips, flips_ref = int((err64 > FLIP).sum()), int((errref > FLIP).sum())
+        assert flips <= 2 * flips_ref + 4, (i, "flips", flips, "reference's own", flips_ref)
+        calm = (err64 <= FLIP) & (errref <= FLIP)
+        m_calm, m_calm_ref = float(err64[calm].mean()), float(errref[calm].mean())
+        assert m_calm <= 2 * m_calm_ref + 1e-6, (i, "mean over non-flipped px", m_calm, m_calm_ref)
+        # p99 within 2x the reference's own fp32 distance; the max (a single near-tie flip, a
+        # noisy one-sample statistic) within 4x
+        for got, bound, k, slack in zip(e64[1:], sens[1:], (2, 4), (1e-4, 1e-3)):
             assert got <= k * bound + slack, (i, "vs fp64", e64, "ref fp32 vs fp64", sens)
         if tag in STRICT:
             assert e32[2] <= 1e-3, (i, e32)
