@@ -46,6 +46,7 @@ _SIGNATURES = {
     "aanet_csa_sum_f32": [_P, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P],
     "aanet_conv3x3s2_pack_f32": [_P, _I, _I, _P, _P],
     "aanet_conv3x3s2_f32": [_P, _P, _P] + [_I] * 6 + [_P, _I, _P, _I, _P],
+    "aanet_conv3x3s2_terms_f32": [_P, _P, _P] + [_I] * 6 + [_P, _I, _P, _I, _P, _P],
     "aanet_mdcn_im2col_f32": [_P, _P, _P, _P] + [_I] * 9 + [_P],
     "aanet_mdcn_sample_index": [_P, _P, _P, _P] + [_I] * 9 + [_P],
 }
@@ -71,7 +72,10 @@ def lib():
                 f"aanet_amd: HIP library not found at {LIB_PATH}; build it with "
                 "`python -c 'import __graft_entry__ as g; g.build()'` (make -C aanet_amd/csrc)")
         L = ctypes.CDLL(LIB_PATH)
+        ab_build = "AANET_MI355X_LIB" in os.environ  # an older build under A/B timing
         for name, argtypes in _SIGNATURES.items():
+            if ab_build and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.argtypes = argtypes
             f.restype = _I
@@ -158,6 +162,12 @@ class CsaEpilogue(ctypes.Structure):
                 ("up", ctypes.c_void_p * 3), ("up_h", ctypes.c_int * 3),
                 ("up_w", ctypes.c_int * 3), ("act", ctypes.c_int),
                 ("post", ctypes.POINTER(PostStage))]
+
+
+class S2Terms(ctypes.Structure):
+    """aanet_s2_terms_t (include/aanet_mi355x.h)."""
+    _fields_ = [("x2", ctypes.c_void_p), ("c2", ctypes.c_int), ("identity", ctypes.c_void_p),
+                ("up", ctypes.c_void_p), ("up_h", ctypes.c_int), ("up_w", ctypes.c_int)]
 
 
 def stream_of(t):

@@ -29,6 +29,8 @@
 // products, fp32 accumulation), taps and chunks in ascending order.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "common.h"
 #include "split.h"
 
@@ -38,14 +40,34 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int NT = 512;         // 8 waves, one output row each
 constexpr int TR = 8, TC = 16;  // output tile
+constexpr unsigned OOB = 0x80000000u;  // buffer offset past any num_records: loads return 0
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// raw buffer resource (stride 0): base, num_records bytes, the flags of make_buffer_rsrc above
+__device__ __forceinline__ u32x4 make_rsrc(const float *base, int bytes) {
+  const unsigned long p = reinterpret_cast<unsigned long>(base);
+  // wave-uniform by construction; readfirstlane keeps the "s" asm operand in SGPRs
+  return u32x4{(unsigned)__builtin_amdgcn_readfirstlane((int)p),
+               (unsigned)__builtin_amdgcn_readfirstlane((int)((p >> 32) & 0xffffu)),
+               (unsigned)__builtin_amdgcn_readfirstlane(bytes), 0x00020000u};
+}
 
 struct S2Args {
-  const float *x;      // [N][C][H][W]
+  const float *x;      // [N][C1][H][W]
+  const float *x2;     // [N][C - C1][H][W] (channels appended after x's), or NULL
   const char *wsplit;  // [C/32][9][NCB][3][64 lanes][16 B]
   const float *bias;   // [Co] or NULL
   float *out[2];
   int co_a, act[2];
-  int N, C, H, W, Ho, Wo, Co;
+  // CSA terms of output a, added before act[0] (aggregation.py:388-400 order): the same-size
+  // identity, then the bilinearly resized coarser term
+  const float *id;     // [N][co_a][Ho][Wo] or NULL
+  const float *up;     // [N][co_a][up_h][up_w] or NULL
+  int up_h, up_w;
+  float up_sh, up_sw;  // up_h / Ho, up_w / Wo
+  int N, C, C1, H, W, Ho, Wo, Co;
+  int ncbt;            // Co / 16: co blocks per weight step (a workgroup takes NCB of them)
 };
 
 __device__ __forceinline__ float s2_act(float v, int act) {
@@ -54,11 +76,27 @@ __device__ __forceinline__ float s2_act(float v, int act) {
   return v;
 }
 
-template <int NCB>
+// compile-time step loop: f(integral_constant<int, S>) for S = 0 .. N-1 (straight-line code)
+template <typename F, int... S>
+__device__ __forceinline__ void for_steps(F &&f, std::integer_sequence<int, S...>) {
+  (f(std::integral_constant<int, S>{}), ...);
+}
+
+// NCH: input channels / 32 (1..4, the loop is unrolled over its 9 * NCH steps).  RING: steps in
+// the pipeline (step s computes while s+1 .. s+RING-1 load).
+template <int NCB, int NCH, int RING>
 __global__ __launch_bounds__(NT, 4) void conv3x3s2_kernel(S2Args a) {
-  constexpr int AB = NCB * 3 * 1024;  // A fragments of one (chunk, tap) step
+  constexpr int AB = NCB * 3 * 1024;  // this workgroup's A fragments of one (chunk, tap) step
+  // 1-KB weight DMA pieces per step: wave w issues pieces w, w + 8, ...: ND_HI of them for the
+  // first NPC % 8 waves, ND_LO for the others (each wave's s_waitcnt immediate picks its count)
+  constexpr int NPC = 3 * NCB, ND_LO = NPC / 8, ND_HI = (NPC + 7) / 8;
+  constexpr int NB = 8;  // B-operand dword loads per lane and step
+  constexpr int NS = 9 * NCH;
+  static_assert(RING == 2 || RING == 3, "pipeline depth");
+  // one __shared__ object per slot (see dcn_tile.hip for why separate objects)
   __shared__ __attribute__((aligned(16))) char sA0[AB];
   __shared__ __attribute__((aligned(16))) char sA1[AB];
+  __shared__ __attribute__((aligned(16))) char sA2[RING > 2 ? AB : 16];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -70,52 +108,104 @@ __global__ __launch_bounds__(NT, 4) void conv3x3s2_kernel(S2Args a) {
   const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b0 & 7;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b0 >> 3);
   const int n = bid / ntiles, tile = bid % ntiles;
+  const int cot = blockIdx.y, co_base = 16 * NCB * cot;  // this workgroup's output-channel tile
+  const bool nd_hi = wave < NPC % 8;                    // wave-uniform
   const int y = (tile / tx) * TR + wave, x = (tile % tx) * TC + jj;
   const bool pv = y < Ho && x < Wo;
   const int HW = H * W;
-  const int img_bytes = a.C * HW * 4;  // < 2^31 (launcher)
-  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void *)(a.x + (long)n * a.C * HW), (short)0,
-                                                     img_bytes, 0x00020000);
+  const int C1 = a.C1, C2 = a.C - a.C1, nc1 = C1 / 32;
+  // buffer resources built by hand: the B loads are inline asm (see load_b)
+  const float *xb2 = a.x2 ? a.x2 + (long)n * C2 * HW : a.x;
+  const u32x4 xr = make_rsrc(a.x + (long)n * C1 * HW, C1 * HW * 4);
+  const u32x4 xr2 = make_rsrc(xb2, a.x2 ? C2 * HW * 4 : 0);
   // lane base: channel 8kr of the chunk, input row 2y-1, column 2x-1 (tap (ti, tj) adds ti*W+tj)
   const int yy0 = 2 * y - 1, xx0 = 2 * x - 1;
   const int lbase = (8 * kr * HW + yy0 * W + xx0) * 4;
-  bool rok[3], cok[3];
+  // bit k: tap k = (k / 3, k % 3) lies inside the image (a branch-free test in the loop: an
+  // exec-masked branch there makes the compiler wait for every load in flight at its join)
+  unsigned okmask = 0;
 #pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    rok[t] = pv && (unsigned)(yy0 + t) < (unsigned)H;
-    cok[t] = (unsigned)(xx0 + t) < (unsigned)W;
-  }
-  const int nsteps = (a.C / 32) * 9;
+  for (int k = 0; k < 9; ++k)
+    okmask |= (pv && (unsigned)(yy0 + k / 3) < (unsigned)H && (unsigned)(xx0 + k % 3) < (unsigned)W) ? 1u << k : 0u;
 
-  // the eight channel values of this lane's B fragment at step s = (chunk s/9, tap s%9);
-  // out of the image: the out-of-range offset, whose buffer load returns 0 (zero padding)
+  // the eight channel values of this lane's B fragment at step s = (chunk s/9, tap s%9); out of
+  // the image: the out-of-range offset, whose buffer load returns 0 (zero padding).  Inline asm:
+  // with LDS-DMA loads in flight the compiler's waitcnt pass treats the vector-memory counter as
+  // unordered and waits for EVERY load before the first use of a B value (vmcnt(0)), which
+  // would cut the pipeline to one step.  The waits are explicit instead (wait_b): the values of
+  // step s+1 pass through the counted s_waitcnt at the end of step s as asm operands, so no use
+  // can be scheduled ahead of it.
   auto load_b = [&](int s, float (&v)[8]) {
     const int cc = s / 9, k = s - 9 * (s / 9), ti = k / 3, tj = k - 3 * (k / 3);
-    const bool ok = rok[ti] && cok[tj];
-    const int off = ok ? lbase + (ti * W + tj) * 4 : img_bytes;
+    const unsigned keep = 0u - ((okmask >> k) & 1u);  // all ones inside the image
+    const unsigned off = ((unsigned)(lbase + (ti * W + tj) * 4) & keep) | (OOB & ~keep);
+    const bool second = cc >= nc1;
+    const int c0 = second ? cc - nc1 : cc;
+    u32x4 rs = second ? xr2 : xr;
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-          xr, off, __builtin_amdgcn_readfirstlane((32 * cc + u) * HW * 4), 0));
+    for (int q = 0; q < 4; ++q) rs[q] = (unsigned)__builtin_amdgcn_readfirstlane((int)rs[q]);
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int so = __builtin_amdgcn_readfirstlane((32 * c0 + u) * HW * 4);
+      asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(v[u]) : "v"(off), "s"(rs), "s"(so) : "memory");
+    }
   };
+  // this wave's loads issued before the last CNT steps' landed (CNT = the steps issued after the
+  // one awaited), then the workgroup barrier (every wave's DMA of that step landed) in the SAME
+  // asm statement: the bare s_barrier intrinsic does not order memory for the compiler, and an A
+  // read hoisted between the wait and the barrier would race with the other waves' DMAs.
+  // __syncthreads' fence is not used: it waits for every load in flight (vmcnt(0)).  The
+  // awaited step's B values pass through the asm as operands, so no use is scheduled before it.
+  // ONE asm statement for every wave (a branch between two would make the compiler copy the
+  // pending registers into common ones before it, reading them before they land): the count
+  // assumes ND_LO pieces per step, so the waves with ND_HI wait for one load more than needed.
+  auto wait_step = [&](auto cnt_c, float (&v)[8]) {
+    constexpr int CNT = decltype(cnt_c)::value;
+    asm volatile("s_waitcnt vmcnt(%8)\n\ts_barrier"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+                 : "n"(CNT * (NB + ND_LO)) : "memory");
+  };
+  // weight DMA, inline asm as well: the compiler then sees no vector-memory op in the loop and
+  // inserts no wait of its own (it cannot count LDS-DMA loads against ordinary loads, and waited
+  // for all of them before reading an A slot); every wait is explicit (wait_b)
   auto issue_a = [&](int s, char *dst) {
-    const char *src = a.wsplit + (long)s * AB + lane * 16;
-    for (int pc = wave; pc < 3 * NCB; pc += 8)
-      __builtin_amdgcn_global_load_lds((const void *)(src + pc * 1024), (lds_void *)(dst + pc * 1024), 16, 0, 0);
+    const char *src = a.wsplit + ((long)s * a.ncbt + NCB * cot) * 3072 + lane * 16;
+#pragma unroll
+    for (int r = 0; r < ND_HI; ++r) {
+      const int pc = wave + 8 * r;
+      if (r == ND_LO && !nd_hi) break;  // wave-uniform
+      const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void *)(dst + pc * 1024));
+      asm volatile("global_load_lds_dwordx4 %0, off" :: "v"(src + pc * 1024), "{m0}"(m0) : "memory");
+    }
   };
 
   f32x4 acc[NCB];
 #pragma unroll
   for (int m = 0; m < NCB; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto step = [&](int s, const char *cur, char *nxt, const float (&vc)[8], float (&vn)[8]) {
-    if (s + 1 < nsteps) {  // next step's weights and input, behind this step's MFMAs
-      issue_a(s + 1, nxt);
-      load_b(s + 1, vn);
+  // step s: issue step s+RING-1's weights and input (into the slot step s-1 used: every wave
+  // passed the barrier after reading it), contract step s, then wait for step s+1 (only the
+  // steps issued after it stay in flight) and barrier.
+  auto slot = [&](int i) -> char * { return i == 0 ? sA0 : (i == 1 ? sA1 : sA2); };
+  float v[RING][8];
+  for_steps([&](auto j_c) {
+    constexpr int J = decltype(j_c)::value;
+    if constexpr (J < RING - 1) {
+      issue_a(J, slot(J));
+      load_b(J, v[J]);
+    }
+  }, std::make_integer_sequence<int, RING>{});
+  wait_step(std::integral_constant<int, RING - 2>{}, v[0]);  // step 0 landed
+  for_steps([&](auto s_c) {
+    constexpr int S = decltype(s_c)::value;
+    constexpr int NX = S + RING - 1;  // the step issued now
+    if constexpr (NX < NS) {
+      issue_a(NX, slot(NX % RING));
+      load_b(NX, v[NX % RING]);
     }
     bf16x8 B[3];
-    split8(vc, B);
-    const char *ab = cur + lane * 16;
+    split8(v[S % RING], B);
+    const char *ab = slot(S % RING) + lane * 16;
 #pragma unroll
     for (int m = 0; m < NCB; ++m) {
       bf16x8 A[3];
@@ -123,39 +213,68 @@ __global__ __launch_bounds__(NT, 4) void conv3x3s2_kernel(S2Args a) {
       for (int pc = 0; pc < 3; ++pc) A[pc] = *reinterpret_cast<const bf16x8 *>(ab + (m * 3 + pc) * 1024);
       acc[m] = mfma_split6(A, B, acc[m]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's loads of step s+1 landed ...
-    __syncthreads();                                   // ... and every other wave's DMA
-  };
+    if constexpr (S + 1 < NS) {
+      constexpr int LAST = NX < NS ? NX : NS - 1;  // the newest step issued
+      wait_step(std::integral_constant<int, LAST - (S + 1)>{}, v[(S + 1) % RING]);
+    }
+  }, std::make_integer_sequence<int, NS>{});
 
-  float v0[8], v1[8];
-  issue_a(0, sA0);
-  load_b(0, v0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-#pragma unroll 1
-  for (int s = 0; s < nsteps; s += 2) {
-    step(s, sA0, sA1, v0, v1);
-    if (s + 1 < nsteps) step(s + 1, sA1, sA0, v1, v0);
-  }
-
-  // epilogue: channel co = 16m + 4kr + r of pixel (y, x); rows of 16 pixels = 64-byte segments
+  // epilogue: channel co = 16m + 4kr + r of pixel (y, x); rows of 16 pixels = 64-byte segments.
+  // Two passes: every value (with its CSA terms) first, then the stores -- the term loads of all
+  // the lane's channels are then in flight together (a store between them could alias their
+  // sources, so the compiler would otherwise wait for each in turn).
   if (!pv) return;
   const long P = (long)Ho * Wo, pix = (long)y * Wo + x;
   const int cb = a.Co - a.co_a;
+  // the resize stencil of this pixel (PyTorch upsample_bilinear2d, align_corners=False, as in
+  // csa.hip's bilinear_resize): the same four offsets and weights for every channel plane
+  int o00 = 0, o01 = 0, o10 = 0, o11 = 0;
+  float h0l = 0.f, h1l = 0.f, w0l = 0.f, w1l = 0.f;
+  if (a.up) {
+    float hr = a.up_sh * ((float)y + 0.5f) - 0.5f;
+    hr = hr < 0.f ? 0.f : hr;
+    float wr = a.up_sw * ((float)x + 0.5f) - 0.5f;
+    wr = wr < 0.f ? 0.f : wr;
+    const int h1 = (int)hr, w1 = (int)wr;
+    const int h1p = h1 < a.up_h - 1 ? 1 : 0, w1p = w1 < a.up_w - 1 ? 1 : 0;
+    h1l = hr - (float)h1, h0l = 1.f - h1l;
+    w1l = wr - (float)w1, w0l = 1.f - w1l;
+    o00 = h1 * a.up_w + w1, o01 = o00 + w1p;
+    o10 = (h1 + h1p) * a.up_w + w1, o11 = o10 + w1p;
+  }
+  float res[NCB][4];
 #pragma unroll
   for (int m = 0; m < NCB; ++m) {
-    const int c4 = 16 * m + 4 * kr;
+    const int c4 = co_base + 16 * m + 4 * kr;
     const f32x4 bs = a.bias ? *reinterpret_cast<const f32x4 *>(a.bias + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int co = c4 + r;
-      const float v = acc[m][r] + bs[r];
-      if (co < a.co_a)
-        a.out[0][((long)n * a.co_a + co) * P + pix] = s2_act(v, a.act[0]);
-      else
-        a.out[1][((long)n * cb + co - a.co_a) * P + pix] = s2_act(v, a.act[1]);
+      float v = acc[m][r] + bs[r];
+      if (co < a.co_a) {
+        const long plane = (long)n * a.co_a + co;
+        if (a.id) v += a.id[plane * P + pix];
+        if (a.up) {
+          const float *im = a.up + plane * a.up_h * a.up_w;
+          v += h0l * (w0l * im[o00] + w1l * im[o01]) + h1l * (w0l * im[o10] + w1l * im[o11]);
+        }
+        v = s2_act(v, a.act[0]);
+      } else {
+        v = s2_act(v, a.act[1]);
+      }
+      res[m][r] = v;
     }
   }
+#pragma unroll
+  for (int m = 0; m < NCB; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co_base + 16 * m + 4 * kr + r;
+      if (co < a.co_a)
+        a.out[0][((long)n * a.co_a + co) * P + pix] = res[m][r];
+      else
+        a.out[1][((long)n * cb + co - a.co_a) * P + pix] = res[m][r];
+    }
 }
 
 // w [Co][C][3][3] fp32 -> [C/32][9][Co/16][3][64 lanes][8 bf16]: lane l of block m holds row
@@ -178,6 +297,23 @@ __global__ void conv3x3s2_pack_kernel(const float *__restrict__ w, bf16x8 *__res
   }
 }
 
+// Pipeline depth: three steps for the narrow tiles (their steps are short: a third step in
+// flight hides the load latency), two for the wide ones (whose LDS and registers it would cost
+// occupancy; A/B build: -DAANET_S2_WIDE_RING=3)
+#ifndef AANET_S2_WIDE_RING
+#define AANET_S2_WIDE_RING 2
+#endif
+template <int NCB>
+void launch_s2(int nch, dim3 grid, dim3 blk, hipStream_t st, const S2Args &a) {
+  constexpr int R = NCB <= 2 ? 3 : AANET_S2_WIDE_RING;
+  switch (nch) {  // the AANet pyramid: 32 / 64 / 96 input channels
+    case 1: hipLaunchKernelGGL((conv3x3s2_kernel<NCB, 1, R>), grid, blk, 0, st, a); break;
+    case 2: hipLaunchKernelGGL((conv3x3s2_kernel<NCB, 2, R>), grid, blk, 0, st, a); break;
+    case 3: hipLaunchKernelGGL((conv3x3s2_kernel<NCB, 3, R>), grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL((conv3x3s2_kernel<NCB, 4, R>), grid, blk, 0, st, a); break;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -195,16 +331,24 @@ int aanet_conv3x3s2_pack_f32(const float *w, int co, int c, void *wsplit, aanet_
   return aanet_launch_status();
 }
 
-int aanet_conv3x3s2_f32(const float *x, const void *wsplit, const float *bias, int n, int c, int h,
-                        int w, int co, int co_a, float *out_a, int act_a, float *out_b, int act_b,
-                        aanet_stream_t stream) {
+int aanet_conv3x3s2_terms_f32(const float *x, const void *wsplit, const float *bias, int n,
+                              int c, int h, int w, int co, int co_a, float *out_a, int act_a,
+                              float *out_b, int act_b, const aanet_s2_terms_t *terms,
+                              aanet_stream_t stream) {
   if (!x || !wsplit || n < 0 || h < 0 || w < 0 || co_a < 0 || co_a > co) return AANET_EINVAL;
-  if (co <= 0 || co % 16 || c <= 0 || c % 32) return AANET_EUNSUPPORTED;
+  const int c2 = terms && terms->x2 ? terms->c2 : 0;
+  if (c2 < 0 || (terms && terms->x2 == nullptr && terms->c2 != 0)) return AANET_EINVAL;
+  if (co <= 0 || co % 16 || c <= 0 || c % 32 || c2 % 32 || c + c2 > 128) return AANET_EUNSUPPORTED;
   if ((co_a > 0 && !out_a) || (co_a < co && !out_b)) return AANET_EINVAL;
-  if ((long)c * h * w * 4 >= (1L << 31)) return AANET_EUNSUPPORTED;
+  if ((long)c * h * w * 4 >= (1L << 31) || (long)c2 * h * w * 4 >= (1L << 31)) return AANET_EUNSUPPORTED;
+  const int ho = (h + 1) / 2, wo = (w + 1) / 2;
+  const bool has_terms = terms && (terms->identity || terms->up);
+  if (has_terms && co_a == 0) return AANET_EINVAL;
+  if (terms && terms->up && (terms->up_h <= 0 || terms->up_w <= 0)) return AANET_EINVAL;
   if (n == 0 || h == 0 || w == 0) return AANET_OK;
   S2Args a;
   a.x = x;
+  a.x2 = c2 ? terms->x2 : nullptr;
   a.wsplit = reinterpret_cast<const char *>(wsplit);
   a.bias = bias;
   a.out[0] = out_a;
@@ -212,23 +356,41 @@ int aanet_conv3x3s2_f32(const float *x, const void *wsplit, const float *bias, i
   a.co_a = co_a;
   a.act[0] = act_a;
   a.act[1] = act_b;
-  a.N = n, a.C = c, a.H = h, a.W = w, a.Co = co;
-  a.Ho = (h + 1) / 2;
-  a.Wo = (w + 1) / 2;
+  a.id = terms ? terms->identity : nullptr;
+  a.up = terms ? terms->up : nullptr;
+  a.up_h = a.up ? terms->up_h : 1;
+  a.up_w = a.up ? terms->up_w : 1;
+  a.up_sh = (float)a.up_h / (float)ho;
+  a.up_sw = (float)a.up_w / (float)wo;
+  a.N = n, a.C = c + c2, a.C1 = c, a.H = h, a.W = w, a.Co = co;
+  a.Ho = ho;
+  a.Wo = wo;
   const long tiles = (long)host_div_up(a.Wo, TC) * host_div_up(a.Ho, TR) * n;
   if (tiles > 0x7fffffffL) return AANET_EUNSUPPORTED;
+  a.ncbt = co / 16;
+  // one workgroup takes every output channel (co tiles of 48 sharing the input through L2
+  // measured 114 vs 93 us for the C2 heads launch)
+  const int ncb = a.ncbt;
   const dim3 grid((unsigned)tiles), blk(NT);
   hipStream_t st = as_hip(stream);
-  switch (co / 16) {
-    case 1: hipLaunchKernelGGL(conv3x3s2_kernel<1>, grid, blk, 0, st, a); break;
-    case 2: hipLaunchKernelGGL(conv3x3s2_kernel<2>, grid, blk, 0, st, a); break;
-    case 3: hipLaunchKernelGGL(conv3x3s2_kernel<3>, grid, blk, 0, st, a); break;
-    case 4: hipLaunchKernelGGL(conv3x3s2_kernel<4>, grid, blk, 0, st, a); break;
-    case 5: hipLaunchKernelGGL(conv3x3s2_kernel<5>, grid, blk, 0, st, a); break;
-    case 6: hipLaunchKernelGGL(conv3x3s2_kernel<6>, grid, blk, 0, st, a); break;
+  const int nch = a.C / 32;
+  switch (ncb) {
+    case 1: launch_s2<1>(nch, grid, blk, st, a); break;
+    case 2: launch_s2<2>(nch, grid, blk, st, a); break;
+    case 3: launch_s2<3>(nch, grid, blk, st, a); break;
+    case 4: launch_s2<4>(nch, grid, blk, st, a); break;
+    case 5: launch_s2<5>(nch, grid, blk, st, a); break;
+    case 6: launch_s2<6>(nch, grid, blk, st, a); break;
     default: return AANET_EUNSUPPORTED;
   }
   return aanet_launch_status();
+}
+
+int aanet_conv3x3s2_f32(const float *x, const void *wsplit, const float *bias, int n, int c, int h,
+                        int w, int co, int co_a, float *out_a, int act_a, float *out_b, int act_b,
+                        aanet_stream_t stream) {
+  return aanet_conv3x3s2_terms_f32(x, wsplit, bias, n, c, h, w, co, co_a, out_a, act_a, out_b,
+                                   act_b, nullptr, stream);
 }
 
 }  // extern "C"

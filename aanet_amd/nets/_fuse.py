@@ -37,7 +37,8 @@ def clear_fold_caches(module):
     """Drop every folded-weight / BN-affine cache in `module`'s subtree (called on each
     train()/eval() switch of the drop-in modules, see FoldCacheMixin)."""
     for m in module.modules():
-        for attr in ("_aanet_fold", "_aanet_fold_dense", "_aanet_affine", "_aanet_s2pack"):
+        for attr in ("_aanet_fold", "_aanet_fold_dense", "_aanet_affine", "_aanet_s2pack",
+                     "_aanet_s2pack_k"):
             if attr in m.__dict__:
                 del m.__dict__[attr]
 
@@ -126,6 +127,30 @@ def s2_pack(owner, pairs):
         wsplit = ops.pack_conv3x3s2(w)
     val = None if wsplit is None else (wsplit, b)
     owner.__dict__["_aanet_s2pack"] = (key, val)
+    return val
+
+
+def s2_pack_k(owner, pairs):
+    """(pre-split fragments, bias) of the 3x3 stride-2 convs `pairs` = [(conv, bn), ...] (BN
+    folded) concatenated along the INPUT channels, biases summed: one conv over the channel-
+    concatenated inputs whose output is the sum of theirs (ops.conv3x3_s2 with x2).  Cached on
+    `owner` like s2_pack; None outside the kernel."""
+    fs = [folded(c, b) for c, b in pairs]
+    key = tuple(c._aanet_fold[0] for c, _ in pairs)
+    cache = owner.__dict__.get("_aanet_s2pack_k")
+    if cache is not None and cache[0] == key:
+        return cache[1]
+    with torch.no_grad():
+        w = torch.cat([f[0] for f in fs], 1)
+        b = None
+        for f in fs:
+            if f[1] is not None:
+                b = f[1].clone() if b is None else b + f[1]
+        if b is None:
+            b = torch.zeros(w.shape[0], device=w.device)
+        wsplit = ops.pack_conv3x3s2(w)
+    val = None if wsplit is None else (wsplit, b.contiguous())
+    owner.__dict__["_aanet_s2pack_k"] = (key, val)
     return val
 
 

@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from ._fuse import FoldCacheMixin, conv_bn_act, folded, s2_conv_ok, s2_pack, use_fused
+from ._fuse import FoldCacheMixin, conv_bn_act, folded, s2_conv_ok, s2_pack, s2_pack_k, use_fused
 from .deform import DeformSimpleBottleneck, SimpleBottleneck
 
 
@@ -42,6 +42,12 @@ def post_fusion():
     """AANET_POST_FUSION=0 disables the tail kernels' post stage (the next module's conv1 and the
     final_conv + regression in the previous tail kernel's epilogue): A/B switch."""
     return os.environ.get("AANET_POST_FUSION", "1") != "0"
+
+
+def s2_sums():
+    """AANET_S2_SUMS=0 keeps the coarse branches' CSA sums in aanet_csa_sum_f32 kernels instead of
+    the stride-2 kernels' epilogues (A/B switch)."""
+    return os.environ.get("AANET_S2_SUMS", "1") != "0"
 
 
 def num_side_streams(num_scales):
@@ -166,6 +172,50 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
                                 acts[1] if len(acts) > 1 else None)
         return {heads[0]: ya, **({heads[1]: yb} if len(heads) > 1 else {})}
 
+    def _s2_sums_ok(self, x):
+        """Whether output branches 1 and 2 (S = 3) are summed inside the stride-2 kernels:
+          branch 1 = LeakyReLU(down(x0) + x1 + resize(up(x2))): the scale-0 heads launch, with x1
+            and the up term as CSA terms of its first output (ops.conv3x3_s2 identity / up);
+          branch 2 = LeakyReLU(down(down(x0)) + down(x1) + x2): ONE conv over the channel-
+            concatenated inputs [head output, x1] (weights concatenated along the input
+            channels, biases summed: the two down terms' sum), x2 as its identity term.
+        Needs the reference's S = 3 structure (one conv from scale 0 to 1, two from 0 to 2, one
+        from 1 to 2), every conv on the stride-2 kernel, and sizes that need no resize of the
+        same-resolution terms (aggregation.py:395: x1 / x2 already have the down terms' size)."""
+        if len(self.branches) != 3 or len(self.fuse_layers) != 3 or not s2_sums():
+            return False
+        l10, l20, l21 = self.fuse_layers[1][0], self.fuse_layers[2][0], self.fuse_layers[2][1]
+        if len(l10) != 1 or len(l20) != 2 or len(l21) != 1:
+            return False
+        convs = [l10[0][0], l20[0][0], l20[1][0], l21[0][0]]
+        if not all(s2_conv_ok(c) for c in convs) or \
+                l10[0][0].out_channels + l20[0][0].out_channels > 96 or \
+                l20[1][0].out_channels != l21[0][0].out_channels:
+            return False
+        h1, w1 = (x[0].shape[2] + 1) // 2, (x[0].shape[3] + 1) // 2
+        h2, w2 = (h1 + 1) // 2, (w1 + 1) // 2
+        return tuple(x[1].shape[2:]) == (h1, w1) and tuple(x[2].shape[2:]) == (h2, w2) and \
+            x[1].shape[1] == l10[0][0].out_channels and x[2].shape[1] == l21[0][0].out_channels
+
+    def _heads_sum1(self, x0, x1, t12):
+        """The scale-0 heads launch (see _down0_heads) that also completes output branch 1:
+        -> (branch 1 output, first conv of the branch-2 chain)."""
+        l10, l20 = self.fuse_layers[1][0], self.fuse_layers[2][0]
+        pairs = [(l10[0][0], l10[0][1]), (l20[0][0], l20[0][1])]
+        pk = s2_pack(l10, pairs)
+        co_a = pairs[0][0].out_channels
+        return ops.conv3x3_s2(x0.contiguous(), pk[0], pk[1], co_a + pairs[1][0].out_channels,
+                              co_a, "leaky", "leaky", identity=x1.contiguous(),
+                              up=t12.contiguous())
+
+    def _branch2_sum(self, hb, x1, x2):
+        """Output branch 2 as one stride-2 conv over [hb, x1] + x2 (see _s2_sums_ok)."""
+        l20, l21 = self.fuse_layers[2][0], self.fuse_layers[2][1]
+        pk = s2_pack_k(l21, [(l20[1][0], l20[1][1]), (l21[0][0], l21[0][1])])
+        co = l21[0][0].out_channels
+        return ops.conv3x3_s2(hb, pk[0], pk[1], co, co, "leaky", None, x2=x1.contiguous(),
+                              identity=x2.contiguous())[0]
+
     def _term_down0(self, x, i, heads):
         """Exchange term (i, 0) given the head outputs of _down0_heads."""
         if i in heads:
@@ -250,8 +300,14 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
         keep.append(x[0])
         if "coarse" not in mark:  # the tail kernel did not take the block
             join()
-        heads = self._down0_heads(x[0])  # on the current stream: both branches need them
-        keep.extend(heads.values())
+        sums = self._s2_sums_ok(x)
+        if sums:  # heads + branch 1's sum (x[1] and the up term exist: the join above)
+            out1, hb = self._heads_sum1(x[0], x[1], terms[(1, 2)])
+            keep.extend((out1, hb))
+            heads = {}
+        else:
+            heads = self._down0_heads(x[0])  # on the current stream: both branches need them
+            keep.extend(heads.values())
         b0_ev = _record(main)
         out = [None] * nout
         if csa0 is None:  # no tail epilogue: branch 0's sum on the current stream
@@ -259,11 +315,17 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
         else:
             out[0] = csa0
         # coarse branches: the down terms from the coarse scales (concurrent with the scale-0
-        # tail), then the one from scale 0, then the sum, on the branch's stream
+        # tail), then the one from scale 0, then the sum, on the branch's stream (with the
+        # stride-2 sums: branch 1 comes from the heads launch, branch 2 is one launch)
         for i in range(1, nout):
             st = streams[i]
             with torch.cuda.stream(st):
                 st.wait_event(mark["coarse"])
+                if sums:
+                    st.wait_event(b0_ev)
+                    out[i] = out1 if i == 1 else self._branch2_sum(hb, x[1], x[2])
+                    keep.append(out[i])
+                    continue
                 for j in range(1, i):
                     terms[(i, j)] = self._down(x[j], i, j)
                 st.wait_event(b0_ev)
@@ -280,8 +342,14 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
         one aanet_csa_sum_f32 kernel (same term order as aggregation.py:388-400).  done: output
         branches already summed (by a tail-kernel epilogue); terms_cache: exchange terms already
         computed, keyed (i, j)."""
-        done = done or {}
+        done = dict(done or {})
         terms_cache = terms_cache or {}
+        if 1 not in done and 2 not in done and self._s2_sums_ok(x):
+            t12 = terms_cache.get((1, 2))
+            if t12 is None:
+                t12 = self._exchange_up(x, 1, 2)
+            done[1], hb = self._heads_sum1(x[0], x[1], t12)
+            done[2] = self._branch2_sum(hb, x[1], x[2])
         heads = self._down0_heads(x[0]) if any(i not in done for i in range(1, len(self.fuse_layers))) else {}
         x_fused = []
         for i in range(len(self.fuse_layers)):

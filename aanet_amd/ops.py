@@ -3,6 +3,8 @@
 Each op allocates its outputs with torch (caching allocator, device memory) and launches on
 torch's current HIP stream through ``_lib.call`` -- capturable into a HIP graph.
 """
+import ctypes
+
 import torch
 from torch.autograd import Function
 from torch.autograd.function import once_differentiable
@@ -453,18 +455,37 @@ def pack_conv3x3s2(weight):
     return out
 
 
-def conv3x3_s2(x, wsplit, bias, co, co_a, act_a=None, act_b=None):
+def conv3x3_s2(x, wsplit, bias, co, co_a, act_a=None, act_b=None, x2=None, identity=None,
+               up=None):
     """3x3 stride-2 pad-1 conv (BN folded) with its output channels split over two outputs:
     [0, co_a) -> out_a (act_a), [co_a, co) -> out_b (act_b); returns (out_a, out_b), either None
     when empty.  The CSA down exchange convs that share an input run as one launch
-    (aanet_conv3x3s2_f32, nets/aggregation.py:362-371)."""
-    require_gpu(x, bias)
+    (aanet_conv3x3s2_f32, nets/aggregation.py:362-371).  With the CSA terms
+    (aanet_conv3x3s2_terms_f32): x2 is a second input whose channels follow x's in the
+    contraction (wsplit packs the [co][C + C2][3][3] weight: two down terms of one branch as one
+    conv); out_a = act_a(conv + bias [+ identity] [+ bilinear resize of up to out_a's size])."""
+    require_gpu(x, bias, x2, identity, up)
     N, C, H, W = x.shape
     Ho, Wo = (H + 1) // 2, (W + 1) // 2
     out_a = torch.empty((N, co_a, Ho, Wo), device=x.device, dtype=x.dtype) if co_a > 0 else None
     out_b = torch.empty((N, co - co_a, Ho, Wo), device=x.device, dtype=x.dtype) if co_a < co else None
-    call("aanet_conv3x3s2_f32", ptr(x), ptr(wsplit), ptr(bias), N, C, H, W, co, co_a, ptr(out_a),
-         ACT[act_a], ptr(out_b), ACT[act_b], stream_of(x))
+    if x2 is None and identity is None and up is None:
+        call("aanet_conv3x3s2_f32", ptr(x), ptr(wsplit), ptr(bias), N, C, H, W, co, co_a,
+             ptr(out_a), ACT[act_a], ptr(out_b), ACT[act_b], stream_of(x))
+        return out_a, out_b
+    if x2 is not None and (x2.shape[0] != N or tuple(x2.shape[2:]) != (H, W)):
+        raise ValueError("conv3x3_s2: x2 must match x's batch and spatial size")
+    if identity is not None and tuple(identity.shape) != (N, co_a, Ho, Wo):
+        raise ValueError("conv3x3_s2: identity must have out_a's shape")
+    if up is not None and tuple(up.shape[:2]) != (N, co_a):
+        raise ValueError("conv3x3_s2: up must have out_a's batch and channels")
+    x2c = None if x2 is None else x2.contiguous()
+    idc = None if identity is None else identity.contiguous()
+    upc = None if up is None else up.contiguous()
+    t = _lib.S2Terms(ptr(x2c), 0 if x2c is None else x2c.shape[1], ptr(idc), ptr(upc),
+                     1 if upc is None else upc.shape[2], 1 if upc is None else upc.shape[3])
+    call("aanet_conv3x3s2_terms_f32", ptr(x), ptr(wsplit), ptr(bias), N, C, H, W, co, co_a,
+         ptr(out_a), ACT[act_a], ptr(out_b), ACT[act_b], ctypes.byref(t), stream_of(x))
     return out_a, out_b
 
 

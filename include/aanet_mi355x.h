@@ -255,6 +255,27 @@ int aanet_conv3x3s2_f32(const float *x, const void *wsplit, const float *bias, i
                         int w, int co, int co_a, float *out_a, int act_a, float *out_b, int act_b,
                         aanet_stream_t stream);
 
+/* aanet_conv3x3s2_f32 with the CSA sum of output a in its epilogue (aggregation.py:388-400 for an
+ * output branch whose finer-scale term is this conv):
+ *   out_a = act_a(conv + bias [+ identity] [+ resize(up)])
+ * in that order, resize = F.interpolate(up, (ho, wo), mode='bilinear', align_corners=False).
+ * x2 (optional, c2 % 32 == 0 channels, same n/h/w as x): a second input whose channels follow
+ * x's in the contraction (wsplit packs the [co][c + c2][3][3] weight), so two down terms that
+ * land on the same branch are one launch whose output is their sum (C2 branch 2: the 64->16
+ * conv of the scale-0 chain and the 32->16 conv from scale 1).  identity: [n][co_a][ho][wo];
+ * up: [n][co_a][up_h][up_w].  terms may be NULL (= aanet_conv3x3s2_f32). */
+typedef struct aanet_s2_terms {
+  const float *x2;
+  int c2;
+  const float *identity;
+  const float *up;
+  int up_h, up_w;
+} aanet_s2_terms_t;
+int aanet_conv3x3s2_terms_f32(const float *x, const void *wsplit, const float *bias, int n, int c,
+                              int h, int w, int co, int co_a, float *out_a, int act_a,
+                              float *out_b, int act_b, const aanet_s2_terms_t *terms,
+                              aanet_stream_t stream);
+
 /* Backward of F.interpolate(x, size=(out_h, out_w), mode='bilinear', align_corners=False)
  * (aggregation.py:395-396 in training; the loss's upsampling, model.py:115-117):
  * grad_in [planes, in_h, in_w] is OVERWRITTEN with the gather-form sum over grad_out

@@ -21,6 +21,8 @@ CASES = [
     (1, 32, 5, 7, 48, 16, "relu", "leaky"),   # 3 co blocks, partial tiles
     (1, 64, 6, 10, 64, 0, None, "leaky"),     # every channel to the second output
     (1, 64, 128, 416, 96, 32, None, "leaky"),  # C2 scale 0, one image
+    (2, 96, 11, 26, 16, 16, None, None),      # three chunks (the merged branch-2 contraction)
+    (1, 128, 7, 18, 32, 16, "leaky", None),   # four chunks: the runtime-loop instantiation
 ]
 
 ACTS = {None: lambda t: t, "relu": lambda t: t.clamp_min(0),
@@ -63,6 +65,64 @@ def test_conv3x3_s2_vs_fp64(case):
     again = ops.conv3x3_s2(xd, ws, bd, co, co_a, act_a, act_b)
     for a1, a2 in zip((got_a, got_b), again):
         assert (a1 is None and a2 is None) or torch.equal(a1, a2)
+
+
+TERM_CASES = [
+    # N, C, C2, H, W, co, co_a, identity, up (h, w) or None, act_a, act_b
+    (2, 64, 0, 24, 52, 96, 32, True, (6, 13), "leaky", "leaky"),  # branch 1 sum in the heads launch
+    (2, 64, 32, 24, 52, 16, 16, True, None, "leaky", None),        # branch 2: both down terms + x2
+    (1, 64, 0, 17, 23, 48, 16, True, (4, 5), "leaky", None),       # odd sizes, non-integer ratio
+    (1, 32, 64, 9, 14, 16, 16, False, (3, 4), None, None),         # x2 first chunk boundary, up only
+    (1, 64, 0, 128, 416, 96, 32, True, (32, 104), "leaky", "leaky"),  # C2 scale 0, one image
+    (1, 64, 32, 64, 208, 16, 16, True, None, "leaky", None),       # C2 scale 1 -> 2, one image
+]
+
+
+@pytest.mark.parametrize("case", TERM_CASES, ids=[f"c{c[1]}+{c[2]}co{c[5]}h{c[3]}w{c[4]}" for c in TERM_CASES])
+def test_conv3x3_s2_csa_terms_vs_fp64(case):
+    """aanet_conv3x3s2_terms_f32: out_a = act(conv(x ++ x2) + bias + identity + resize(up)) in
+    the reference's term order (aggregation.py:388-400), against fp64 with the same error bar as
+    the plain form plus the fp32 rounding of the added terms."""
+    N, C, C2, H, W, co, co_a, with_id, up_hw, act_a, act_b = case
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(N, C, H, W, generator=g) * 2
+    x2 = torch.randn(N, C2, H, W, generator=g) * 2 if C2 else None
+    CT = C + C2
+    w = torch.randn(co, CT, 3, 3, generator=g) / (3 * CT ** 0.5)
+    b = torch.randn(co, generator=g)
+    Ho, Wo = (H + 1) // 2, (W + 1) // 2
+    ident = torch.randn(N, co_a, Ho, Wo, generator=g) if with_id else None
+    up = torch.randn(N, co_a, *up_hw, generator=g) if up_hw else None
+    xin = x if x2 is None else torch.cat([x, x2], 1)
+    y = F.conv2d(xin.double(), w.double(), b.double(), stride=2, padding=1)
+    scale = F.conv2d(xin.double().abs(), w.double().abs(), stride=2, padding=1) + 1.0
+    ya = y[:, :co_a].clone()
+    if ident is not None:
+        ya = ya + ident.double()
+    if up is not None:
+        ya = ya + F.interpolate(up.double(), size=(Ho, Wo), mode="bilinear", align_corners=False)
+    dev = lambda t: None if t is None else t.to(DEV)  # noqa: E731
+    wd = w.to(DEV)
+    ws = ops.pack_conv3x3s2(wd)
+    got_a, got_b = ops.conv3x3_s2(dev(x), ws, dev(b), co, co_a, act_a, act_b, x2=dev(x2),
+                                  identity=dev(ident), up=dev(up))
+    with exact_f32():
+        ref_e = ops.conv2d_fused(dev(xin), wd, dev(b), 2, 1, 1, 1, None,
+                                 packed_weight=ops.pack_weight(wd))
+    err_e = ((ref_e.cpu().double() - y).abs() / scale).max().item()
+    tol = max(4 * err_e, 2e-7)
+    ref_a = ACTS[act_a](ya)
+    err = ((got_a.cpu().double() - ref_a).abs() / (scale[:, :co_a] + ya.abs())).max().item()
+    assert err <= tol, (err, err_e)
+    if co_a < co:
+        ref_b = ACTS[act_b](y[:, co_a:])
+        err = ((got_b.cpu().double() - ref_b).abs() / scale[:, co_a:]).max().item()
+        assert err <= tol, (err, err_e)
+    else:
+        assert got_b is None
+    again = ops.conv3x3_s2(dev(x), ws, dev(b), co, co_a, act_a, act_b, x2=dev(x2),
+                           identity=dev(ident), up=dev(up))
+    assert torch.equal(again[0], got_a)
 
 
 def test_conv3x3_s2_rejects_unsupported_shapes():

@@ -7,11 +7,11 @@ path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof_step/run_kernel_tr
 rows = list(csv.DictReader(open(path)))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
 # a step starts with the one-launch correlation pyramid
-idx = [i for i, r in enumerate(rows) if 'corr_pyramid_kernel' in r['Kernel_Name']]
+idx = [i for i, r in enumerate(rows) if 'corr_pyramid' in r['Kernel_Name']]
 # the bench's roofline loops repeat single kernels after the timed steps: take the last pair of
 # pyramid launches with a whole step between them
-pairs = [(i, j) for i, j in zip(idx[:-1], idx[1:]) if j - i > 50]
-a, b = pairs[-1]
+pairs = [(i, j) for i, j in zip(idx[:-1], idx[1:]) if 50 < j - i < 400]
+a, b = pairs[len(pairs) // 2]  # a step from the middle of the timed run
 seg = rows[a:b]
 t0 = int(seg[0]['Start_Timestamp'])
 t1 = int(rows[b]['Start_Timestamp'])
