@@ -452,6 +452,11 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
         the soft-argmin.  None when the shapes do not fit (64 channels at scale 0, 1x1, one
         stage block)."""
         if i + 1 < self.num_fusions:
+            # the window DCN tail (dcn_tile.hip) pays more for the conv1 stage (spills of its POST
+            # instantiation: +60-65 us per launch) than the separate 1x1 launch costs (46-56 us);
+            # the plain 3x3 tail takes it for +25-30 us
+            if isinstance(self.fusions[i].branches[0][-1], DeformSimpleBottleneck):
+                return None
             nxt = self.fusions[i + 1]
             if nxt.num_blocks != 1 or len(nxt.branches) == 0:
                 return None
