@@ -16,15 +16,17 @@ dst = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 
 os.makedirs(dst, exist_ok=True)
 
 # bench.py kernel_rooflines keys -> kernel names
-KMAP = {"corr_volume_s0": r"corr_volume_kernel<5, 1>", "disp_regress_s0": r"disp_regress_fixed_kernel<64>",
-        "corr_pyramid": r"corr_pyramid_kernel",
+KMAP = {"corr_volume_s0": r"corr_reg_kernel<5, 8, 2>", "disp_regress_s0": r"disp_regress_fixed_kernel<64>",
+        "corr_pyramid": r"corr_pyramid_reg_kernel",
         # the streaming 1x1 conv (pointwise.hip), NCHW input, 4 output-channel blocks, NHWC out
         "conv1x1_s0": r"pw_conv_nchw_kernel<64, 4, 1>",
-        # the LDS-window deformable tail (dcn_tile.hip; the generic engine's split form was
-        # conv_fwd_kernel<1, 64, 128, 1, 1, 1, 1, 1, 0, 1, 0>)
-        "mdcn_pw_s0": r"dcn_tile_kernel<2, 32>",
-        # MODE, CO_T, PTT, PACKED, TAIL, SCHED, FULL, LAYOUT, CFG, PREC (1: split-bf16), HALO (= dil)
-        "conv3x3_pw_s0": r"conv_fwd_kernel<0, 64, 128, 1, 1, 1, 1, 1, 0, 1, 1>"}
+        # the LDS-window deformable tail (dcn_tile.hip), common form (no post stage)
+        "mdcn_pw_s0": r"dcn_tile_kernel<2, 32, false>",
+        # MODE, CO_T, PTT, PACKED, TAIL, SCHED, FULL, LAYOUT, CFG, PREC (1: split-bf16), HALO (= dil),
+        # POST (0: no post stage)
+        "conv3x3_pw_s0": r"conv_fwd_kernel<0, 64, 128, 1, 1, 1, 1, 1, 0, 1, 1, 0>",
+        # the C5 concat volume (shift_volume_band_kernel, concat form)
+        "concat_volume_c5": r"shift_volume_band_kernel<true>"}
 
 # 1. kernel stats of the bench command
 stats = list(csv.DictReader(open(os.path.join(src, "trace", "bench_kernel_stats.csv"))))
