@@ -41,6 +41,16 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 
+#ifndef DCN_PFWAIT
+#define DCN_PFWAIT 0
+#endif
+#ifndef DCN_PRIO
+#define DCN_PRIO 0
+#endif
+#ifndef DCN_UNROLL
+#define DCN_UNROLL 0
+#endif
+
 constexpr int NT = 512;          // 8 waves, one tile row each
 constexpr int TR = 8, TC = 16;   // tile: 8 rows x 16 columns of output pixels
 constexpr int RW = 2;            // window margin beyond the taps: offsets in [-RW, RW) stay inside
@@ -206,12 +216,19 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   const int pt = CG == 32 ? kr : (kr & 1);
   const int lgrp = CG == 32 ? 0 : (kr >> 1);  // this lane's group within the phase
   float poh = 0.f, pow_ = 0.f, pml = 0.f;  // prefetched offsets / mask of the next pass
+  // All three byte offsets are formed before the first load, in 32-bit 24-bit-multiply form: as
+  // (plane * P * 4 + p4) the compiler chose v_mad_u64_u32 with a 64-bit addend register pair whose
+  // high half was the destination of the offset load just issued, i.e. an s_waitcnt vmcnt(0) (a
+  // full memory round trip) in every sampling pass.  Plane indices are < 2 * 2 * 9, P * 4 < 2^24.
   auto load_pass = [&](int g, int t0) {
     const int t = min(t0 + pt, K - 1), gr = CG == 32 ? g : (kr >> 1);
-    const int oplane = (gr * 2 * K + 2 * t) * P * 4, mplane = (gr * K + t) * P * 4;
-    poh = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, p4 + oplane, 0, 0));
-    pow_ = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, p4 + oplane + P * 4, 0, 0));
-    pml = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mskr, p4 + mplane, 0, 0));
+    const unsigned P4 = (unsigned)P * 4u;
+    const int o_h = (int)__umul24((unsigned)(gr * 2 * K + 2 * t), P4) + p4;
+    const int o_w = o_h + (int)P4;
+    const int o_m = (int)__umul24((unsigned)(gr * K + t), P4) + p4;
+    poh = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, o_h, 0, 0));
+    pow_ = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, o_w, 0, 0));
+    pml = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mskr, o_m, 0, 0));
   };
   TapState ps;  // this lane's state for (tap, group) pt(kr) of the current pass
   auto compute_pass = [&](int t0) {
@@ -348,13 +365,27 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       pf_res = a.residual[((long)(n * a.Co2 + co2) * H + yy) * W + x0];
     }
     tap(g, k, cur, s, NPH == 2 && c == K - 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of A(c+1) landed ...
+#if DCN_PFWAIT
+    // the warm-up load (issued after the DMA, so the youngest) is left in flight for a chunk
+    const bool pf = (NPH == 2 && c == 3 && wave * 64 < WR * WC) || (c == NCH - 6 && a.residual);
+    if (pf)
+      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else
+#endif
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of A(c+1) landed ...
     if (!(a.dbg & 8)) __syncthreads();                 // ... and every other wave's
   };
   load_window(0);
   issue_a(0, sA0);
   load_pass(0, 0);
+#if DCN_PRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // MI355X_MICROARCH.md item 4: the younger half
+#endif
+#if DCN_UNROLL
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
   for (int c = 0; c < NCH - 1; c += 2) {
     step(c, sA0, sA1);
     step(c + 1, sA1, sA0);

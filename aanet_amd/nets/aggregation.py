@@ -44,6 +44,12 @@ def post_fusion():
     return os.environ.get("AANET_POST_FUSION", "1") != "0"
 
 
+def post_conv1():
+    """Whether the plain 3x3 tails take the next module's conv1 as their post stage
+    (AANET_POST_FUSION=final keeps only the last module's final_conv + regression stage)."""
+    return os.environ.get("AANET_POST_FUSION", "1") not in ("0", "final")
+
+
 def s2_sums():
     """AANET_S2_SUMS=0 keeps the coarse branches' CSA sums in aanet_csa_sum_f32 kernels instead of
     the stride-2 kernels' epilogues (A/B switch)."""
@@ -452,6 +458,8 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
         the soft-argmin.  None when the shapes do not fit (64 channels at scale 0, 1x1, one
         stage block)."""
         if i + 1 < self.num_fusions:
+            if not post_conv1():
+                return None
             # the window DCN tail (dcn_tile.hip) pays more for the conv1 stage (spills of its POST
             # instantiation: +60-65 us per launch) than the separate 1x1 launch costs (46-56 us);
             # the plain 3x3 tail takes it for +25-30 us
