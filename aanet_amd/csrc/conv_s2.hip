@@ -29,6 +29,8 @@
 // products, fp32 accumulation), taps and chunks in ascending order.
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "common.h"
@@ -80,6 +82,68 @@ __device__ __forceinline__ float s2_act(float v, int act) {
 template <typename F, int... S>
 __device__ __forceinline__ void for_steps(F &&f, std::integer_sequence<int, S...>) {
   (f(std::integral_constant<int, S>{}), ...);
+}
+
+// epilogue: channel co = 16m + 4kr + r of pixel (y, x); rows of 16 pixels = 64-byte segments.
+// Two passes: every value (with its CSA terms) first, then the stores -- the term loads of all
+// the lane's channels are then in flight together (a store between them could alias their
+// sources, so the compiler would otherwise wait for each in turn).
+template <int NCB>
+__device__ __forceinline__ void s2_epilogue(const S2Args &a, const f32x4 (&acc)[NCB], int n, int y, int x,
+                                            int kr, int co_base, bool pv) {
+  const int Ho = a.Ho, Wo = a.Wo;
+  if (!pv) return;
+  const long P = (long)Ho * Wo, pix = (long)y * Wo + x;
+  const int cb = a.Co - a.co_a;
+  // the resize stencil of this pixel (PyTorch upsample_bilinear2d, align_corners=False, as in
+  // csa.hip's bilinear_resize): the same four offsets and weights for every channel plane
+  int o00 = 0, o01 = 0, o10 = 0, o11 = 0;
+  float h0l = 0.f, h1l = 0.f, w0l = 0.f, w1l = 0.f;
+  if (a.up) {
+    float hr = a.up_sh * ((float)y + 0.5f) - 0.5f;
+    hr = hr < 0.f ? 0.f : hr;
+    float wr = a.up_sw * ((float)x + 0.5f) - 0.5f;
+    wr = wr < 0.f ? 0.f : wr;
+    const int h1 = (int)hr, w1 = (int)wr;
+    const int h1p = h1 < a.up_h - 1 ? 1 : 0, w1p = w1 < a.up_w - 1 ? 1 : 0;
+    h1l = hr - (float)h1, h0l = 1.f - h1l;
+    w1l = wr - (float)w1, w0l = 1.f - w1l;
+    o00 = h1 * a.up_w + w1, o01 = o00 + w1p;
+    o10 = (h1 + h1p) * a.up_w + w1, o11 = o10 + w1p;
+  }
+  float res[NCB][4];
+#pragma unroll
+  for (int m = 0; m < NCB; ++m) {
+    const int c4 = co_base + 16 * m + 4 * kr;
+    const f32x4 bs = a.bias ? *reinterpret_cast<const f32x4 *>(a.bias + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = c4 + r;
+      float v = acc[m][r] + bs[r];
+      if (co < a.co_a) {
+        const long plane = (long)n * a.co_a + co;
+        if (a.id) v += a.id[plane * P + pix];
+        if (a.up) {
+          const float *im = a.up + plane * a.up_h * a.up_w;
+          v += h0l * (w0l * im[o00] + w1l * im[o01]) + h1l * (w0l * im[o10] + w1l * im[o11]);
+        }
+        v = s2_act(v, a.act[0]);
+      } else {
+        v = s2_act(v, a.act[1]);
+      }
+      res[m][r] = v;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < NCB; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co_base + 16 * m + 4 * kr + r;
+      if (co < a.co_a)
+        a.out[0][((long)n * a.co_a + co) * P + pix] = res[m][r];
+      else
+        a.out[1][((long)n * cb + co - a.co_a) * P + pix] = res[m][r];
+    }
 }
 
 // NCH: input channels / 32 (1..4, the loop is unrolled over its 9 * NCH steps).  RING: steps in
@@ -219,62 +283,161 @@ __global__ __launch_bounds__(NT, 4) void conv3x3s2_kernel(S2Args a) {
     }
   }, std::make_integer_sequence<int, NS>{});
 
-  // epilogue: channel co = 16m + 4kr + r of pixel (y, x); rows of 16 pixels = 64-byte segments.
-  // Two passes: every value (with its CSA terms) first, then the stores -- the term loads of all
-  // the lane's channels are then in flight together (a store between them could alias their
-  // sources, so the compiler would otherwise wait for each in turn).
-  if (!pv) return;
-  const long P = (long)Ho * Wo, pix = (long)y * Wo + x;
-  const int cb = a.Co - a.co_a;
-  // the resize stencil of this pixel (PyTorch upsample_bilinear2d, align_corners=False, as in
-  // csa.hip's bilinear_resize): the same four offsets and weights for every channel plane
-  int o00 = 0, o01 = 0, o10 = 0, o11 = 0;
-  float h0l = 0.f, h1l = 0.f, w0l = 0.f, w1l = 0.f;
-  if (a.up) {
-    float hr = a.up_sh * ((float)y + 0.5f) - 0.5f;
-    hr = hr < 0.f ? 0.f : hr;
-    float wr = a.up_sw * ((float)x + 0.5f) - 0.5f;
-    wr = wr < 0.f ? 0.f : wr;
-    const int h1 = (int)hr, w1 = (int)wr;
-    const int h1p = h1 < a.up_h - 1 ? 1 : 0, w1p = w1 < a.up_w - 1 ? 1 : 0;
-    h1l = hr - (float)h1, h0l = 1.f - h1l;
-    w1l = wr - (float)w1, w0l = 1.f - w1l;
-    o00 = h1 * a.up_w + w1, o01 = o00 + w1p;
-    o10 = (h1 + h1p) * a.up_w + w1, o11 = o10 + w1p;
-  }
-  float res[NCB][4];
+  s2_epilogue<NCB>(a, acc, n, y, x, kr, co_base, pv);
+}
+
+// ---- row form for the wide tiles (round 3) ------------------------------------------------
+// A counter pass of the form above at the C2 heads shape (tools/s2_pmc.sh): the matrix pipe busy
+// 37 % of the kernel, the texture unit 47 %, and the L1 sending 8.4x the input's bytes to L2:
+// every (channel, tap) is its own dword gather, so a lane's three taps of one input row are
+// three instructions that touch the same lines three steps apart, and with 16 waves per CU
+// streaming through a 32 KB L1 the lines are gone by the second touch.  (A rolled 64-VGPR
+// variant with twice the waves per SIMD was SLOWER, 102 vs 91 us: more waves, more misses.)
+// Here a lane loads the three columns 2x-1 .. 2x+1 of one (channel, input row) with ONE
+// buffer_load_dwordx3 (dword-aligned; gfx9 buffer loads need no more), i.e. one instruction per
+// (channel, row) instead of three, each touching its lines once.  Steps stay per tap (the A
+// slot of a step is one tap's weights, two steps ahead in a ring of three slots: 2 x 54 KB per CU
+// at NCB = 6, still two workgroups per CU); row r+1 is issued at the first tap of row r, so it
+// has the row's three steps to land.
+// Left border: the x = 0 lane loads columns 0..2 and shifts them (column -1 is padding); right
+// border (odd W): column 2x+1 = W is zeroed.  Same numerics as the form above (taps and chunks
+// in ascending order, the same split and piece products): bit-identical outputs.
+typedef float f32x3 __attribute__((ext_vector_type(3)));
+
+template <int NCB, int NCH>
+__global__ __launch_bounds__(NT, 4) void conv3x3s2_rows_kernel(S2Args a) {
+  constexpr int AB = NCB * 3 * 1024;
+  constexpr int NPC = 3 * NCB, ND_LO = NPC / 8, ND_HI = (NPC + 7) / 8;
+  constexpr int NS = 9 * NCH, NR = 3 * NCH;  // steps (taps), rows
+  __shared__ __attribute__((aligned(16))) char sA0[AB];
+  __shared__ __attribute__((aligned(16))) char sA1[AB];
+  __shared__ __attribute__((aligned(16))) char sA2[AB];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kr = lane >> 4, jj = lane & 15;
+  const int H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
+  const int tx = (Wo + TC - 1) / TC, ntiles = tx * ((Ho + TR - 1) / TR);
+  const int nwg = gridDim.x, b0 = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b0 & 7;
+  const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b0 >> 3);
+  const int n = bid / ntiles, tile = bid % ntiles;
+  const int cot = blockIdx.y, co_base = 16 * NCB * cot;
+  const bool nd_hi = wave < NPC % 8;
+  const int txi = __builtin_amdgcn_readfirstlane(tile % tx);  // x tile (wave-uniform)
+  const int y = (tile / tx) * TR + wave, x = txi * TC + jj;
+  const bool pv = y < Ho && x < Wo;
+  const int HW = H * W;
+  const int C1 = a.C1, C2 = a.C - a.C1, nc1 = C1 / 32;
+  const float *xb2 = a.x2 ? a.x2 + (long)n * C2 * HW : a.x;
+  const u32x4 xr = make_rsrc(a.x + (long)n * C1 * HW, C1 * HW * 4);
+  const u32x4 xr2 = make_rsrc(xb2, a.x2 ? C2 * HW * 4 : 0);
+  // lane base: channel 8kr of the chunk, input row 2y-1, first loaded column 2x-1 (x = 0: 0)
+  const int yy0 = 2 * y - 1, xl = x > 0 ? 2 * x - 1 : 0;
+  const int lbase = (8 * kr * HW + yy0 * W + xl) * 4;
+  // bit ti: input row 2y-1+ti lies inside the image (and the pixel is valid)
+  unsigned rowok = 0;
 #pragma unroll
-  for (int m = 0; m < NCB; ++m) {
-    const int c4 = co_base + 16 * m + 4 * kr;
-    const f32x4 bs = a.bias ? *reinterpret_cast<const f32x4 *>(a.bias + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int ti = 0; ti < 3; ++ti) rowok |= (pv && (unsigned)(yy0 + ti) < (unsigned)H) ? 1u << ti : 0u;
+  const bool fix_left = txi == 0;                                 // wave-uniform
+  const bool fix_right = (W & 1) && txi == tx - 1;                // wave-uniform
+  const bool rz = 2 * x + 1 >= W;                                 // this lane's column 2x+1 is padding
+
+  // the three columns of this lane's eight channels of row r = (chunk r / 3, input row r % 3)
+  auto load_row = [&](int r, f32x3 (&v)[8]) {
+    const int cc = r / 3, ti = r - 3 * (r / 3);
+    const unsigned keep = 0u - ((rowok >> ti) & 1u);
+    const unsigned off = ((unsigned)(lbase + ti * W * 4) & keep) | (OOB & ~keep);
+    const bool second = cc >= nc1;
+    const int c0 = second ? cc - nc1 : cc;
+    u32x4 rs = second ? xr2 : xr;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = c4 + r;
-      float v = acc[m][r] + bs[r];
-      if (co < a.co_a) {
-        const long plane = (long)n * a.co_a + co;
-        if (a.id) v += a.id[plane * P + pix];
-        if (a.up) {
-          const float *im = a.up + plane * a.up_h * a.up_w;
-          v += h0l * (w0l * im[o00] + w1l * im[o01]) + h1l * (w0l * im[o10] + w1l * im[o11]);
-        }
-        v = s2_act(v, a.act[0]);
-      } else {
-        v = s2_act(v, a.act[1]);
-      }
-      res[m][r] = v;
+    for (int q = 0; q < 4; ++q) rs[q] = (unsigned)__builtin_amdgcn_readfirstlane((int)rs[q]);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int so = __builtin_amdgcn_readfirstlane((32 * c0 + u) * HW * 4);
+      asm volatile("buffer_load_dwordx3 %0, %1, %2, %3 offen" : "=v"(v[u]) : "v"(off), "s"(rs), "s"(so) : "memory");
     }
-  }
+  };
+  // wait until this wave has at most CNT vector-memory ops in flight, then the workgroup barrier,
+  // in ONE asm statement (see conv3x3s2_kernel's wait_step); the row values about to be used
+  // pass through as operands so that no use is scheduled ahead of the wait
+  auto wait_bar = [&](auto cnt_c, f32x3 (&v)[8]) {
+    constexpr int CNT = decltype(cnt_c)::value;
+    asm volatile("s_waitcnt vmcnt(%8)\n\ts_barrier"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+                 : "n"(CNT) : "memory");
+  };
+  auto issue_a = [&](int s, char *dst) {
+    const char *src = a.wsplit + ((long)s * a.ncbt + NCB * cot) * 3072 + lane * 16;
 #pragma unroll
-  for (int m = 0; m < NCB; ++m)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = co_base + 16 * m + 4 * kr + r;
-      if (co < a.co_a)
-        a.out[0][((long)n * a.co_a + co) * P + pix] = res[m][r];
-      else
-        a.out[1][((long)n * cb + co - a.co_a) * P + pix] = res[m][r];
+    for (int r = 0; r < ND_HI; ++r) {
+      const int pc = wave + 8 * r;
+      if (r == ND_LO && !nd_hi) break;  // wave-uniform
+      const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void *)(dst + pc * 1024));
+      asm volatile("global_load_lds_dwordx4 %0, off" :: "v"(src + pc * 1024), "{m0}"(m0) : "memory");
     }
+  };
+  auto slot = [&](int i) -> char * { return i == 0 ? sA0 : (i == 1 ? sA1 : sA2); };
+  // border fix-ups of a landed row (wave-uniform branches, taken by the border tiles only)
+  auto fix_row = [&](f32x3 (&v)[8]) {
+    if (fix_left) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (x == 0) v[u] = f32x3{0.f, v[u][0], v[u][1]};
+    }
+    if (fix_right) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (rz) v[u][2] = 0.f;
+    }
+  };
+
+  f32x4 acc[NCB];
+#pragma unroll
+  for (int m = 0; m < NCB; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x3 rv[2][8];
+  // Weights two steps ahead in a ring of three slots: step s issues A(s+2) into slot (s+2) % 3,
+  // the slot step s-1 read (every wave passed the barrier after it).  The first step of row r
+  // also issues row r+1's values, AFTER A(s+2).  vmcnt counts in issue order, so each wait names
+  // exactly the ops younger than the one it needs (a wave that issued ND_HI pieces waits for
+  // one piece more than necessary):
+  //   end of tap 0: A(s+1) landed; A(s+2) and row r+1 may stay in flight
+  //   end of tap 1: A(s+1) landed (issued before row r+1); row r+1 and A(s+2) may stay in flight
+  //   end of tap 2: A(s+1) landed, hence row r+1 too (older); A(s+2) may stay in flight
+  issue_a(0, sA0);
+  issue_a(1, sA1);
+  load_row(0, rv[0]);
+  wait_bar(std::integral_constant<int, 0>{}, rv[0]);
+  for_steps([&](auto s_c) {
+    constexpr int S = decltype(s_c)::value;
+    constexpr int R = S / 3, TJ = S % 3;
+    constexpr bool A2 = S + 2 < NS;                // A(S+2) issued by this step
+    constexpr bool ROWN = TJ == 0 && R + 1 < NR;   // row R+1 issued by this step
+    constexpr bool ROWP = TJ == 1 && R + 1 < NR;   // row R+1 issued by the previous step
+    if constexpr (TJ == 0) fix_row(rv[R % 2]);
+    if constexpr (A2) issue_a(S + 2, slot((S + 2) % 3));
+    if constexpr (ROWN) load_row(R + 1, rv[(R + 1) % 2]);
+    float v8[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v8[u] = rv[R % 2][u][TJ];
+    bf16x8 B[3];
+    split8(v8, B);
+    const char *ab = slot(S % 3) + lane * 16;
+#pragma unroll
+    for (int m = 0; m < NCB; ++m) {
+      bf16x8 A[3];
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc) A[pc] = *reinterpret_cast<const bf16x8 *>(ab + (m * 3 + pc) * 1024);
+      acc[m] = mfma_split6(A, B, acc[m]);
+    }
+    if constexpr (S + 1 < NS) {
+      constexpr int CNT = (A2 ? ND_LO : 0) + ((ROWN || ROWP) ? 8 : 0);
+      wait_bar(std::integral_constant<int, CNT>{}, rv[(TJ == 2 ? R + 1 : R) % 2]);
+    }
+  }, std::make_integer_sequence<int, NS>{});
+
+  s2_epilogue<NCB>(a, acc, n, y, x, kr, co_base, pv);
 }
 
 // w [Co][C][3][3] fp32 -> [C/32][9][Co/16][3][64 lanes][8 bf16]: lane l of block m holds row
@@ -303,8 +466,24 @@ __global__ void conv3x3s2_pack_kernel(const float *__restrict__ w, bf16x8 *__res
 #ifndef AANET_S2_WIDE_RING
 #define AANET_S2_WIDE_RING 2
 #endif
+int s2_rows_enabled() {
+  static const int on = [] {
+    const char *e = getenv("AANET_S2_ROWS");
+    return e ? atoi(e) : 1;
+  }();
+  return on;
+}
+
 template <int NCB>
 void launch_s2(int nch, dim3 grid, dim3 blk, hipStream_t st, const S2Args &a) {
+  if (NCB >= 3 && s2_rows_enabled()) {  // wide tiles: the row form
+    switch (nch) {
+      case 1: hipLaunchKernelGGL((conv3x3s2_rows_kernel<NCB, 1>), grid, blk, 0, st, a); return;
+      case 2: hipLaunchKernelGGL((conv3x3s2_rows_kernel<NCB, 2>), grid, blk, 0, st, a); return;
+      case 3: hipLaunchKernelGGL((conv3x3s2_rows_kernel<NCB, 3>), grid, blk, 0, st, a); return;
+      default: hipLaunchKernelGGL((conv3x3s2_rows_kernel<NCB, 4>), grid, blk, 0, st, a); return;
+    }
+  }
   constexpr int R = NCB <= 2 ? 3 : AANET_S2_WIDE_RING;
   switch (nch) {  // the AANet pyramid: 32 / 64 / 96 input channels
     case 1: hipLaunchKernelGGL((conv3x3s2_kernel<NCB, 1, R>), grid, blk, 0, st, a); break;
