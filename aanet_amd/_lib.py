@@ -47,6 +47,8 @@ _SIGNATURES = {
     "aanet_conv3x3s2_pack_f32": [_P, _I, _I, _P, _P],
     "aanet_conv3x3s2_f32": [_P, _P, _P] + [_I] * 6 + [_P, _I, _P, _I, _P],
     "aanet_conv3x3s2_terms_f32": [_P, _P, _P] + [_I] * 6 + [_P, _I, _P, _I, _P, _P],
+    "aanet_conv3x3_grouped_pack_f32": [_P, _I, _I, _I, _P, _P],
+    "aanet_conv3x3_grouped_nhwc_f32": [_P, _P, _P] + [_I] * 7 + [_P, _P],
     "aanet_mdcn_im2col_f32": [_P, _P, _P, _P] + [_I] * 9 + [_P],
     "aanet_mdcn_sample_index": [_P, _P, _P, _P] + [_I] * 9 + [_P],
 }
@@ -92,6 +94,8 @@ def lib():
         L.aanet_conv_weight_pack_split_bytes.restype = _L
         L.aanet_conv3x3s2_pack_bytes.argtypes = [_I, _I]
         L.aanet_conv3x3s2_pack_bytes.restype = ctypes.c_size_t
+        L.aanet_conv3x3_grouped_pack_bytes.argtypes = [_I, _I, _I]
+        L.aanet_conv3x3_grouped_pack_bytes.restype = ctypes.c_size_t
         _lib = L
     return _lib
 
@@ -99,7 +103,8 @@ def lib():
 def exported_symbols():
     return (["aanet_version", "aanet_status_string", "aanet_mdcn_bwd_det_workspace_size",
              "aanet_mdcn_bwd_ws_workspace_size", "aanet_conv2d_wgrad_workspace_size",
-             "aanet_conv_weight_pack_split_bytes", "aanet_conv3x3s2_pack_bytes"] + list(_SIGNATURES))
+             "aanet_conv_weight_pack_split_bytes", "aanet_conv3x3s2_pack_bytes",
+             "aanet_conv3x3_grouped_pack_bytes"] + list(_SIGNATURES))
 
 
 def call(name, *args):

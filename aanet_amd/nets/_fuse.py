@@ -10,6 +10,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
+from .. import _lib
 from .._lib import is_nhwc
 
 
@@ -152,6 +153,45 @@ def s2_pack_k(owner, pairs):
     val = None if wsplit is None else (wsplit, b.contiguous())
     owner.__dict__["_aanet_s2pack_k"] = (key, val)
     return val
+
+
+def offset_conv_pack(conv):
+    """(pre-split fragments, bias) of a deformable offset_conv for ops.conv3x3_grouped_nhwc,
+    cached on the conv and keyed by its folded weights; None when the conv is outside the kernel
+    (3x3, stride 1, padding = dilation, 32k channels per group, <= 32 outputs per group).
+    Opt-in (AANET_OFFSET_KERNEL=1): in the C2 step it measured slower than the conv engine's
+    halo form (3.57 vs 3.44 ms, same call), so the engine stays the default."""
+    if os.environ.get("AANET_OFFSET_KERNEL", "0") != "1" or type(conv) is not nn.Conv2d or \
+            not engine_conv(conv) or _int(conv.kernel_size) != 3 or _int(conv.stride) != 1 or \
+            _int(conv.padding) != _int(conv.dilation) or \
+            (conv.in_channels // conv.groups) % 32 or (conv.out_channels // conv.groups) > 32:
+        return None
+    w, b, _ = folded(conv, None)
+    key = conv._aanet_fold[0]
+    cache = conv.__dict__.get("_aanet_g3pack")
+    if cache is not None and cache[0] == key:
+        return cache[1]
+    with torch.no_grad():
+        wsplit = ops.pack_conv3x3_grouped(w, conv.groups)
+        bias = b.contiguous() if b is not None else None
+    val = None if wsplit is None else (wsplit, bias)
+    conv.__dict__["_aanet_g3pack"] = (key, val)
+    return val
+
+
+def offset_conv_eval(x, conv):
+    """Eval offset_conv: the grouped direct kernel when x is channels-last and the conv fits
+    (offset_conv_pack), else the conv engine (conv_bn_act)."""
+    pk = offset_conv_pack(conv) if is_nhwc(x) else None
+    if pk is None:
+        return conv_bn_act(x, conv)
+    try:
+        return ops.conv3x3_grouped_nhwc(x, pk[0], pk[1], conv.out_channels, conv.groups,
+                                        _int(conv.dilation))
+    except _lib.AanetError as e:
+        if e.status != _lib.EUNSUPPORTED:
+            raise
+        return conv_bn_act(x, conv)
 
 
 def s2_conv_ok(conv):

@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from ._fuse import FoldCacheMixin, bn_affine, conv_bn_act, folded, use_fused
+from ._fuse import FoldCacheMixin, bn_affine, conv_bn_act, folded, offset_conv_eval, use_fused
 from .deform_conv import DeformConv, ModulatedDeformConv
 
 
@@ -92,7 +92,7 @@ class DeformConv2d(FoldCacheMixin, nn.Module):
     def forward_fused(self, x, bn=None, act=None):
         """Eval path: offset_conv (HIP conv engine) -> one HIP kernel for DCN (+BN, +act)."""
         dc = self.deform_conv
-        offset_mask = conv_bn_act(x, self.offset_conv)
+        offset_mask = offset_conv_eval(x, self.offset_conv)
         ps, psh = bn_affine(bn) if bn is not None else (None, None)
         _, _, wp = folded(dc, None)
         return ops.mdcn_forward_fused(x.contiguous(), offset_mask.contiguous(), dc.weight,
@@ -161,7 +161,7 @@ class _BottleneckBase(FoldCacheMixin, nn.Module):
         identity = (self.downsample(x) if self.downsample is not None else x).contiguous()
         if deform and self.conv2.modulation:
             dc = c2.deform_conv
-            offset_mask = conv_bn_act(out, c2.offset_conv)
+            offset_mask = offset_conv_eval(out, c2.offset_conv)
             ps, psh = bn_affine(self.bn2)
             _, _, wp = folded(dc, None)
             if pw:

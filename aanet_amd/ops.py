@@ -489,6 +489,35 @@ def conv3x3_s2(x, wsplit, bias, co, co_a, act_a=None, act_b=None, x2=None, ident
     return out_a, out_b
 
 
+def pack_conv3x3_grouped(weight, groups):
+    """Pre-split A fragments of a grouped [co][c/groups][3][3] weight for conv3x3_grouped_nhwc
+    (aanet_conv3x3_grouped_pack_f32), or None when the shape is outside the kernel."""
+    co, cg, kh, kw = weight.shape
+    if (kh, kw) != (3, 3) or not weight.is_cuda:
+        return None
+    nbytes = _lib.lib().aanet_conv3x3_grouped_pack_bytes(co, cg * groups, groups)
+    if not nbytes:
+        return None
+    out = torch.empty(nbytes // 2, device=weight.device, dtype=torch.int16)
+    w = weight.contiguous().float()
+    call("aanet_conv3x3_grouped_pack_f32", ptr(w), co, cg * groups, groups, ptr(out), stream_of(w))
+    return out
+
+
+def conv3x3_grouped_nhwc(x, wsplit, bias, co, groups, dilation):
+    """The offset_conv of a deformable bottleneck in eval (deform.py:58-60): 3x3 stride-1 conv
+    with padding = dilation, `groups` groups and bias, from a channels-last x to an NCHW output
+    (aanet_conv3x3_grouped_nhwc_f32)."""
+    require_gpu(x, bias, nhwc_ok=(0,))
+    if not _lib.is_nhwc(x):
+        raise ValueError("conv3x3_grouped_nhwc: x must be channels-last")
+    N, C, H, W = x.shape
+    out = torch.empty((N, co, H, W), device=x.device, dtype=x.dtype)
+    call("aanet_conv3x3_grouped_nhwc_f32", ptr(x), ptr(wsplit), ptr(bias), N, C, H, W, co, groups,
+         dilation, ptr(out), stream_of(x))
+    return out
+
+
 def csa_sum(inputs, act="leaky"):
     """act(inputs[0] + resize(inputs[1]) + ...) at inputs[0]'s size (aggregation.py:387-400)."""
     require_gpu(*inputs)

@@ -255,6 +255,23 @@ int aanet_conv3x3s2_f32(const float *x, const void *wsplit, const float *bias, i
                         int w, int co, int co_a, float *out_a, int act_a, float *out_b, int act_b,
                         aanet_stream_t stream);
 
+/* The deformable bottleneck's offset_conv in eval (nets/deform.py:58-60, 76-79: nn.Conv2d(c, co,
+ * 3, padding=dil, dilation=dil, groups=groups, bias=True); the reference runs it through
+ * cuDNN, deform.py:81 / aggregation.py:418-432): out = conv(x) + bias, x channels-last
+ * ([n][h][w][c], the conv1 output the DCN tail reads next), out NCHW [n][co][h][w] (read in
+ * place as the offset / mask planes).  c / groups % 32 == 0, co % groups == 0,
+ * ceil(co / groups / 16) <= 2 (AANET_EUNSUPPORTED otherwise); the AANet instances are
+ * 64 -> 54 with two groups (scale 0) and 32k -> 27 / 54 with one.  wsplit:
+ * aanet_conv3x3_grouped_pack_f32 of the [co][c / groups][3][3] weight into
+ * aanet_conv3x3_grouped_pack_bytes(co, c, groups) device bytes.  Split-bf16 contraction
+ * (fp32-accurate, see AANET_EXACT_F32 above for the arithmetic). */
+size_t aanet_conv3x3_grouped_pack_bytes(int co, int c, int groups);
+int aanet_conv3x3_grouped_pack_f32(const float *w, int co, int c, int groups, void *wsplit,
+                                   aanet_stream_t stream);
+int aanet_conv3x3_grouped_nhwc_f32(const float *x, const void *wsplit, const float *bias, int n,
+                                   int c, int h, int w, int co, int groups, int dil, float *out,
+                                   aanet_stream_t stream);
+
 /* aanet_conv3x3s2_f32 with the CSA sum of output a in its epilogue (aggregation.py:388-400 for an
  * output branch whose finer-scale term is this conv):
  *   out_a = act_a(conv + bias [+ identity] [+ resize(up)])

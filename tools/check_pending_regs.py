@@ -9,7 +9,7 @@ src = open(sys.argv[1]).read()
 bad = 0
 VMEM = re.compile(r'^(buffer_load|buffer_store|global_load|global_store|scratch_load|scratch_store|'
                   r'buffer_atomic|global_atomic)')
-for m in re.finditer(r'^(_Z\S*conv3x3s2_(?:rows_)?kernel\S*):\n', src, re.M):
+for m in re.finditer(r'^(_Z\S*conv3x3(?:s2_(?:rows_)?|_g3_)kernel\S*):\n', src, re.M):
     body = src[m.end():src.index('.Lfunc_end', m.end())].split('\n')
     ops = []  # in issue order: set of pending destination registers (empty for untracked ops)
     inasm = False
