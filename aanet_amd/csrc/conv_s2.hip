@@ -476,8 +476,9 @@ int s2_rows_enabled() {
 
 template <int NCB>
 void launch_s2(int nch, dim3 grid, dim3 blk, hipStream_t st, const S2Args &a) {
-  // the row form for the wide tiles (AANET_S2_ROWS=0: never, 2: for every width too)
-  if ((NCB >= 3 && s2_rows_enabled()) || s2_rows_enabled() == 2) {
+  // the row form (AANET_S2_ROWS=0: the straight-line form above; the narrow tiles measured
+  // 21 -> 16 us (branch-2 merged conv) and 14 -> 11 us (64 -> 16) alone, the step within noise)
+  if (s2_rows_enabled()) {
     switch (nch) {
       case 1: hipLaunchKernelGGL((conv3x3s2_rows_kernel<NCB, 1>), grid, blk, 0, st, a); return;
       case 2: hipLaunchKernelGGL((conv3x3s2_rows_kernel<NCB, 2>), grid, blk, 0, st, a); return;

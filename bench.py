@@ -231,6 +231,29 @@ def kernel_rooflines(model, left, right, batch, iters):
     flops = 2.0 * B * H * W * (w2.shape[0] * w2.shape[1] * 9 + w3.shape[0] * w3.shape[1])
     res["conv3x3_pw_s0"] = dict(bound="mfma", ms=ms, algo=flops, unit="TFLOP/s",
                                 achieved=flops / ms / 1e9, peak=conv_peak())
+    # the offset_conv of the scale-0 deformable block (3x3, dilation 2, 2 groups, 64 -> 54, the
+    # conv engine's halo form on the channels-last conv1 output)
+    oc = blk.conv2.offset_conv
+    with torch.no_grad():
+        x1 = conv_bn_act(vol, blk.conv1, blk.bn1, "relu", out_nhwc=True)
+        ms = time_events(lambda: conv_bn_act(x1, oc), iters, stream)
+    flops = 2.0 * B * H * W * oc.out_channels * (oc.in_channels // oc.groups) * 9
+    res["offset_conv_s0"] = dict(bound="mfma", ms=ms, algo=flops, unit="TFLOP/s",
+                                 achieved=flops / ms / 1e9, peak=conv_peak())
+    # the scale-0 heads launch of the CSA exchange (conv_s2.hip: the 64 -> 32 branch-1 conv with
+    # branch 1's CSA sum in its epilogue + the 64 -> 64 first conv of the branch-2 chain, 3x3
+    # stride 2), as AdaptiveAggregationModule._heads_sum1 runs it (fusion 4: the last one has a
+    # single output branch)
+    agg = model.aggregation.fusions[4]
+    if agg._s2_sums_ok([vol, torch.empty(B, 32, (H + 1) // 2, (W + 1) // 2, device=vol.device),
+                        torch.empty(B, 16, (H + 3) // 4, (W + 3) // 4, device=vol.device)]):
+        x1s = torch.randn(B, 32, (H + 1) // 2, (W + 1) // 2, device=vol.device)
+        t12 = torch.randn(B, 32, (H + 3) // 4, (W + 3) // 4, device=vol.device)
+        with torch.no_grad():
+            ms = time_events(lambda: agg._heads_sum1(vol, x1s, t12), iters, stream)
+        flops = 2.0 * B * ((H + 1) // 2) * ((W + 1) // 2) * 96 * 64 * 9
+        res["s2_heads_s0"] = dict(bound="mfma", ms=ms, algo=flops, unit="TFLOP/s",
+                                  achieved=flops / ms / 1e9, peak=conv_peak())
     # BASELINE configs[4] (PSMNet-AA / GwcNet-AA, nets/cost.py:31-38): the concat volume of one
     # 384x1248 pair's PSMNet features [B,32,96,312] at D = 192/4 = 48, HBM write-bound:
     # algorithmic bytes = read 2 x 32 x 96 x 312 x 4 + write 64 x 48 x 96 x 312 x 4 = 375.7 MB

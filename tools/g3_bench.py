@@ -31,7 +31,7 @@ def main():
     w = torch.randn(54, 32, 3, 3, device=dev, generator=g) * 0.05
     b = torch.randn(54, device=dev, generator=g)
     ws = ops.pack_conv3x3_grouped(w, 2)
-    pw = ops.pack_weight(w)
+    pw = ops.pack_weight_split(w, 2)  # the engine's split-bf16 halo form, as in the step
     res = {"direct_g3": timed(lambda: ops.conv3x3_grouped_nhwc(x, ws, b, 54, 2, 2)),
            "engine_halo": timed(lambda: ops.conv2d_fused(x, w, b, 1, 2, 2, 2, None, packed_weight=pw))}
     flops = 2.0 * 8 * 128 * 416 * 54 * 32 * 9
