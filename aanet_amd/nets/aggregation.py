@@ -61,6 +61,12 @@ def num_side_streams(num_scales):
     return max(1, min(n, num_scales - 1)) if n > 0 else num_scales - 1
 
 
+def split_heads():
+    """AANET_SPLIT_HEADS=1: the scale-0 heads launch split per output branch, each half on its
+    branch's side stream (A/B switch; the merged launch reads x0 once)."""
+    return os.environ.get("AANET_SPLIT_HEADS", "0") == "1"
+
+
 def _record(stream):
     ev = torch.cuda.Event()
     ev.record(stream)
@@ -214,6 +220,22 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
                               co_a, "leaky", "leaky", identity=x1.contiguous(),
                               up=t12.contiguous())
 
+    def _head1_sum(self, x0, x1, t12):
+        """Output branch 1 alone from the scale-0 block output (the branch-1 half of
+        _heads_sum1: one 64 -> 32 stride-2 conv with x1 and the resized up term in its epilogue)."""
+        l10 = self.fuse_layers[1][0]
+        pk = s2_pack(l10[0][0], [(l10[0][0], l10[0][1])])
+        co = l10[0][0].out_channels
+        return ops.conv3x3_s2(x0.contiguous(), pk[0], pk[1], co, co, "leaky", None,
+                              identity=x1.contiguous(), up=t12.contiguous())[0]
+
+    def _head2(self, x0):
+        """The first conv of the branch-2 chain alone (the other half of _heads_sum1)."""
+        l20 = self.fuse_layers[2][0]
+        pk = s2_pack(l20[0][0], [(l20[0][0], l20[0][1])])
+        co = l20[0][0].out_channels
+        return ops.conv3x3_s2(x0.contiguous(), pk[0], pk[1], co, co, "leaky", None)[0]
+
     def _branch2_sum(self, hb, x1, x2):
         """Output branch 2 as one stride-2 conv over [hb, x1] + x2 (see _s2_sums_ok)."""
         l20, l21 = self.fuse_layers[2][0], self.fuse_layers[2][1]
@@ -307,7 +329,10 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
         if "coarse" not in mark:  # the tail kernel did not take the block
             join()
         sums = self._s2_sums_ok(x)
-        if sums:  # heads + branch 1's sum (x[1] and the up term exist: the join above)
+        split = sums and split_heads() and len(set(id(st) for st in streams[1:3])) == 2
+        if split:  # each branch's head on its own stream, straight after the tail (below)
+            heads = {}
+        elif sums:  # heads + branch 1's sum (x[1] and the up term exist: the join above)
             out1, hb = self._heads_sum1(x[0], x[1], terms[(1, 2)])
             keep.extend((out1, hb))
             heads = {}
@@ -327,6 +352,16 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
             st = streams[i]
             with torch.cuda.stream(st):
                 st.wait_event(mark["coarse"])
+                if split:  # branch i's own head (and, i = 2, its merged sum) on its stream
+                    st.wait_event(b0_ev)
+                    if i == 1:
+                        out[i] = self._head1_sum(x[0], x[1], terms[(1, 2)])
+                    else:
+                        hb = self._head2(x[0])
+                        keep.append(hb)
+                        out[i] = self._branch2_sum(hb, x[1], x[2])
+                    keep.append(out[i])
+                    continue
                 if sums:
                     st.wait_event(b0_ev)
                     out[i] = out1 if i == 1 else self._branch2_sum(hb, x[1], x[2])
