@@ -67,6 +67,13 @@ def split_heads():
     return os.environ.get("AANET_SPLIT_HEADS", "0") == "1"
 
 
+def early_conv1():
+    """AANET_EARLY_CONV1=1: a deformable module's conv1 (when no tail post stage computes it) runs
+    on its own side stream straight after the previous module's scale-0 tail, concurrently with
+    the heads launch, instead of after it on the main stream (A/B switch)."""
+    return os.environ.get("AANET_EARLY_CONV1", "0") == "1"
+
+
 def _record(stream):
     ev = torch.cuda.Event()
     ev.record(stream)
@@ -250,7 +257,7 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
             return self._down(heads[i], i, 0, start=1)
         return self._down(x[0], i, 0)
 
-    def _forward_eval(self, x, streams=None, keep=None, conv1_pre=None, post=None):
+    def _forward_eval(self, x, streams=None, keep=None, conv1_pre=None, post=None, marks=None):
         """Eval ISA + CSA.  The coarser scales run first, so that their exchange terms for output
         branch 0 exist when the scale-0 bottleneck runs: its tail kernel then writes both the
         block output and the cross-scale sum of branch 0 (aanet_csa_epilogue_t), which removes
@@ -326,6 +333,8 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
         if post is not None and post.get("result") is not None:
             keep.extend(v for v in post["result"].values() if v is not None)
         keep.append(x[0])
+        if marks is not None:
+            marks["tail"] = _record(main)  # block output and branch 0's sum are enqueued
         if "coarse" not in mark:  # the tail kernel did not take the block
             join()
         sums = self._s2_sums_ok(x)
@@ -413,13 +422,14 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
             x_fused.append(ops.csa_sum([t.contiguous() for t in terms], act="leaky"))
         return x_fused
 
-    def forward(self, x, streams=None, keep=None, conv1_pre=None, post=None):
+    def forward(self, x, streams=None, keep=None, conv1_pre=None, post=None, marks=None):
         """aggregation.py:375-402.  streams / keep: the concurrent-scale schedule of
         AdaptiveAggregation (eval only, see _forward_eval); conv1_pre / post: the cross-module
-        pointwise fusions of AdaptiveAggregation (eval only)."""
+        pointwise fusions of AdaptiveAggregation (eval only); marks: receives the event recorded
+        on the current stream right after the scale-0 tail ("tail")."""
         assert len(self.branches) == len(x)
         if self.num_scales > 1 and use_fused(self, x[0]) and getattr(self, "aanet_fuse_csa", True):
-            return self._forward_eval(x, streams, keep, conv1_pre, post)
+            return self._forward_eval(x, streams, keep, conv1_pre, post, marks)
         if post is not None:
             post["result"] = None
         if streams is not None:  # reference op sequence: one stream
@@ -522,6 +532,27 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
         # the last module's block output and CSA sum feed nothing but final_conv: not stored
         return {"packed": pf, "bias": bf, "act": None, "disp": True, "skip_outputs": True}
 
+    def _early_conv1(self, i, x0, main, xs, tail_ev, keep):
+        """The next (deformable, one-block) fusion's scale-0 conv1 + BN1 + ReLU (NHWC) on the
+        side stream xs as soon as fusion i's tail has written x0, concurrently with fusion i's
+        heads launch on the main stream; the main stream waits for it before the next fusion's
+        offset conv.  None when the next fusion does not take it."""
+        if i + 1 >= self.num_fusions:
+            return None
+        nxt = self.fusions[i + 1]
+        if nxt.num_blocks != 1 or len(nxt.branches) == 0 or \
+                not isinstance(nxt.branches[0][0], DeformSimpleBottleneck):
+            return None
+        blk = nxt.branches[0][0]
+        if tuple(blk.conv1.weight.shape) != (64, 64, 1, 1):
+            return None
+        xs.wait_event(tail_ev)
+        with torch.cuda.stream(xs):
+            out = conv_bn_act(x0, blk.conv1, blk.bn1, "relu", out_nhwc=True)
+        main.wait_event(_record(xs))
+        keep.extend((x0, out))
+        return out
+
     def forward(self, cost_volume):
         """aggregation.py:452-464 (final 1x1 conv with bias on the HIP conv engine in eval)."""
         return self._run(cost_volume)[0]
@@ -534,11 +565,14 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
         cost-volume list is then None."""
         assert isinstance(cost_volume, list)
         fused = use_fused(self, cost_volume[0])
-        streams = None
+        streams, xs = None, None
         if fused and cost_volume[0].is_cuda and self.num_scales > 1 and concurrent_scales():
             dev = cost_volume[0].device
             main = torch.cuda.current_stream(dev)
-            ss = side_streams(dev, num_side_streams(self.num_scales))
+            nss = num_side_streams(self.num_scales)
+            ss = side_streams(dev, nss + (1 if early_conv1() else 0))
+            xs = ss[nss] if early_conv1() else None  # the early-conv1 stream
+            ss = ss[:nss]
             # scale i >= 1 on side stream (i - 1) mod n
             streams = [main] + [ss[(i - 1) % len(ss)] for i in range(1, self.num_scales)]
             for st in ss:
@@ -549,8 +583,10 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
         for i in range(self.num_fusions):
             fusion = self.fusions[i]
             post = self._post_for(i, regress) if post_ok else None
+            marks = {}
             if streams is not None:
-                cost_volume = fusion(cost_volume, streams, keep, conv1_pre=pre, post=post)
+                cost_volume = fusion(cost_volume, streams, keep, conv1_pre=pre, post=post,
+                                     marks=marks)
             elif post_ok:
                 cost_volume = fusion(cost_volume, conv1_pre=pre, post=post)
             else:
@@ -559,9 +595,13 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
             pre = res["out"] if res is not None else None
             if res is not None and res.get("disp") is not None:
                 disp = res["disp"]
+            if pre is None and streams is not None and xs is not None and "tail" in marks:
+                pre = self._early_conv1(i, cost_volume[0], main, xs, marks["tail"], keep)
         if streams is not None:
             for st in ss:
                 main.wait_stream(st)
+            if xs is not None:
+                main.wait_stream(xs)
             del keep
         if disp is not None:
             return None, disp
