@@ -91,12 +91,14 @@ def test_full_model_vs_reference_golden(tag, fuse):
     the reference's own fp32 3 / 29 / 697 (levels 0-2); with MIOpen's TF32 convolutions the
     reference order had 4 / 137 / 1966, which this bound rejects (tools/flip_report.py)."""
     g, m, left, right = build(tag, fuse)
-    # the reference-order run puts every conv on MIOpen: deterministic algorithms, so the result
-    # does not move with MIOpen's per-run algorithm choice (p99 moved 0.026-0.035 px on PSMNet-AA),
-    # and no TF32 (cudnn.flags() would re-enable it: on gfx950 MIOpen's TF32 convolutions gave
-    # PSMNet-AA 2.8x the reference's own near-tie flips; fp32: 1.05x, tools/flip_report.py)
-    with torch.no_grad(), torch.backends.cudnn.flags(enabled=True, benchmark=False,
-                                                     deterministic=True, allow_tf32=False):
+    # the plain convs of the reference-order run (those that are not ours) go through PyTorch's
+    # native fp32 convolution (im2col + fp32 GEMM), not MIOpen: which MIOpen solver runs a conv
+    # differs from box to box even with deterministic=True, benchmark=False, and some of its
+    # gfx950 fp32 solvers round like TF32 -- PSMNet-AA level 1 went from 39 flips to 103-118
+    # (bound 62) on boxes that picked them, and with MIOPEN_DEBUG_CONV_WINOGRAD=0 every time
+    # (tools/diag_psmnet_flips.sh); TF32 proper gave 137.  A third-party algorithm choice is
+    # not what this test measures, so it is taken out of the run.
+    with torch.no_grad(), torch.backends.cudnn.flags(enabled=False, allow_tf32=False):
         pyr = m(left, right)
     n = len([k for k in g if k.startswith("disp") and not k.startswith("disp64")])
     assert len(pyr) == n
