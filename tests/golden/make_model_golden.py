@@ -58,6 +58,18 @@ MODELS = {
 # max_disp per config (the image-resolution disparity range; GC-Net needs D/2 divisible by 16)
 MAX_DISP_OF = {"gcnet_3d": 64, "psmnet_aa": 64, "psmnet_hg": 64, "psmnet_basic": 64}
 MAX_DISP = 48
+# Fixture conditioning ({state-dict name: factor}, applied after the name-keyed fill and saved in
+# the fixture as `scales`).  PSMNet-AA's plain fill gives un-normalised PSMNet features (std 31)
+# and a correlation volume up to 1.7e3, which the random-weight aggregation (BN with fixed
+# running statistics does not renormalise; DCN offsets grow with the activations) turns into
+# soft-argmin logits of +-1.5e4: the reference's OWN fp32 logits are 7.5e-5 (normwise) off its
+# fp64 ones -- 100x the cost volume's 7e-7 -- and the top-2 logit gap goes down to 0.48, so the
+# disparity is a hard argmax with near-ties (its own fp32 run flipped 3/29/697 pixels by up to
+# 0.2/0.3/0.7 px).  The feature extractor's last 1x1 conv (linear, no bias) scaled by 2^-5
+# (exact) brings the cost volume to |c| <= 1.6 like the AANet fixtures; the reference's own
+# fp32-vs-fp64 distance is then 3.4e-5 / 4.4e-5 / 2.1e-4 px, and the model is held to the same
+# strict 1e-3 px bar as AANet (tests/test_gpu_models.py).  DESIGN.md §4.
+SCALES_OF = {"psmnet_aa": {"feature_extractor.lastconv.2.weight": 2.0 ** -5}}
 
 
 def checksum(sd):
@@ -111,7 +123,8 @@ def main():
         torch.manual_seed(seed)
         max_disp = MAX_DISP_OF.get(tag, MAX_DISP)
         model = aanet.AANet(max_disp, 1, **kw)
-        names = fill_synthetic(model, seed)
+        scales = SCALES_OF.get(tag, {})
+        names = fill_synthetic(model, seed, scales)
         model.eval()
         left, right = synthetic_pair(B, H, W, seed)
         with torch.no_grad():
@@ -124,6 +137,7 @@ def main():
              names=np.array([n for n, _ in names]),
              shapes=np.array([",".join(map(str, s)) for _, s in names]),
              checksum=checksum(model.state_dict()), seed=seed, max_disp=max_disp,
+             **({"scales": np.array(json.dumps(scales))} if scales else {}),
              **{f"disp{i}": d for i, d in enumerate(pyr)},
              **{f"disp64_{i}": d for i, d in enumerate(pyr64)})
         print(f"  {tag}: {len(names)} entries, pyramid " +

@@ -49,15 +49,27 @@ def synthetic_value(name, shape, seed):
     return (2 * torch.rand(shape, generator=g) - 1) * (3.0 / fan_in) ** 0.5
 
 
-def fill_synthetic(module, seed):
+def fill_synthetic(module, seed, scales=None):
     """Overwrite every parameter and buffer of `module` with synthetic_value; returns the
-    (name, shape) list in state-dict order."""
+    (name, shape) list in state-dict order.  `scales` ({state-dict name: factor}, a fixture's
+    `scales` entry) multiplies named entries after the fill: the conditioning of a fixture whose
+    plain fill drives the network into a near-tie regime (make_model_golden.py, psmnet_aa)."""
     import torch
     sd = module.state_dict()
+    scales = dict(scales or {})
     with torch.no_grad():
         for k, v in sd.items():
             v.copy_(synthetic_value(k, v.shape, seed).to(v.dtype))
+            if k in scales:
+                v.mul_(float(scales.pop(k)))
+    assert not scales, f"scaled names not in the model: {sorted(scales)}"
     return [(k, tuple(v.shape)) for k, v in sd.items()]
+
+
+def fixture_scales(g):
+    """The conditioning scales a model fixture was generated with ({} when none)."""
+    import json
+    return json.loads(str(g["scales"])) if "scales" in g else {}
 
 
 def synthetic_pair(B, H, W, seed):

@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from aanet_amd import checkpoint, nets
-from tests.golden_io import fill_synthetic, golden, golden_names, synthetic_pair
+from tests.golden_io import fill_synthetic, fixture_scales, golden, golden_names, synthetic_pair
 
 MODEL_FIXTURES = golden_names("model_")
 
@@ -19,7 +19,7 @@ MODEL_FIXTURES = golden_names("model_")
 def build(tag):
     g = golden(tag)
     m = nets.AANet(int(g["max_disp"]), 1, **json.loads(str(g["config"])))
-    names = fill_synthetic(m, int(g["seed"]))
+    names = fill_synthetic(m, int(g["seed"]), fixture_scales(g))
     return g, m, names
 
 

@@ -23,7 +23,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 from aanet_amd import nets  # noqa: E402
-from tests.golden_io import fill_synthetic, golden, golden_names, synthetic_pair  # noqa: E402
+from tests.golden_io import fill_synthetic, fixture_scales, golden, golden_names, synthetic_pair  # noqa: E402
 
 FLIP = 0.05
 
@@ -45,7 +45,7 @@ def main():
         g = golden(tag)
         for fuse in (True, False):
             m = nets.AANet(int(g["max_disp"]), 1, **json.loads(str(g["config"])))
-            fill_synthetic(m, int(g["seed"]))
+            fill_synthetic(m, int(g["seed"]), fixture_scales(g))
             m = m.to("cuda").eval()
             for mod in m.modules():
                 mod.aanet_fuse = fuse
