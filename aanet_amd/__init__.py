@@ -10,13 +10,8 @@ import torch
 from . import _lib, ops  # noqa: F401
 from . import torch_ops  # noqa: F401  (registers torch.ops.aanet.*)
 
-# fp32 semantics for the convolutions left to MIOpen (transposed convs; every conv of the
-# reference-order / training path): torch allows TF32 for cudnn (= MIOpen) convolutions by
-# default, and on gfx950 MIOpen then computes them below fp32 precision -- the PSMNet-AA
-# reference-order path had 2.8x the reference's own near-tie flips at full resolution with it,
-# 1.05x without (tools/flip_report.py).  The reference is fp32 (cuDNN 7.6, no TF32).
-# A caller may switch it back on after importing this package.
-torch.backends.cudnn.allow_tf32 = False
+# fp32 convolutions on MIOpen: scoped to this package's module forwards (_precision.fp32_convs);
+# importing the package changes no global torch setting.
 
 __version__ = "0.1.0"
 

@@ -53,6 +53,17 @@ _SIGNATURES = {
     "aanet_mdcn_sample_index": [_P, _P, _P, _P] + [_I] * 9 + [_P],
 }
 
+# size / query functions (not int-status): name, argtypes, restype
+_SIZE_FUNCTIONS = [
+    ("aanet_version", [], _I),
+    ("aanet_mdcn_bwd_det_workspace_size", [_I] * 12, ctypes.c_size_t),
+    ("aanet_mdcn_bwd_ws_workspace_size", [_I] * 12, ctypes.c_size_t),
+    ("aanet_conv2d_wgrad_workspace_size", [_I] * 11, ctypes.c_size_t),
+    ("aanet_conv_weight_pack_split_bytes", [_I] * 5, _L),
+    ("aanet_conv3x3s2_pack_bytes", [_I, _I], ctypes.c_size_t),
+    ("aanet_conv3x3_grouped_pack_bytes", [_I, _I, _I], ctypes.c_size_t),
+]
+
 _lib = None
 
 
@@ -81,30 +92,22 @@ def lib():
             f = getattr(L, name)
             f.argtypes = argtypes
             f.restype = _I
+        if not ab_build and L.aanet_version() != ABI_VERSION:
+            raise ImportError(f"aanet_amd: {LIB_PATH} has ABI version {L.aanet_version()}, "
+                              f"this package needs {ABI_VERSION}; rebuild it (make -C aanet_amd/csrc)")
         L.aanet_status_string.argtypes = [_I]
         L.aanet_status_string.restype = ctypes.c_char_p
-        L.aanet_mdcn_bwd_det_workspace_size.argtypes = [_I] * 12
-        L.aanet_mdcn_bwd_det_workspace_size.restype = ctypes.c_size_t
-        L.aanet_mdcn_bwd_ws_workspace_size.argtypes = [_I] * 12
-        L.aanet_mdcn_bwd_ws_workspace_size.restype = ctypes.c_size_t
-        L.aanet_conv2d_wgrad_workspace_size.argtypes = [_I] * 11
-        L.aanet_conv2d_wgrad_workspace_size.restype = ctypes.c_size_t
-        L.aanet_version.restype = _I
-        L.aanet_conv_weight_pack_split_bytes.argtypes = [_I] * 5
-        L.aanet_conv_weight_pack_split_bytes.restype = _L
-        L.aanet_conv3x3s2_pack_bytes.argtypes = [_I, _I]
-        L.aanet_conv3x3s2_pack_bytes.restype = ctypes.c_size_t
-        L.aanet_conv3x3_grouped_pack_bytes.argtypes = [_I, _I, _I]
-        L.aanet_conv3x3_grouped_pack_bytes.restype = ctypes.c_size_t
+        for name, argtypes, restype in _SIZE_FUNCTIONS:
+            if ab_build and not hasattr(L, name):  # an older build under A/B timing
+                continue
+            f = getattr(L, name)
+            f.argtypes, f.restype = argtypes, restype
         _lib = L
     return _lib
 
 
 def exported_symbols():
-    return (["aanet_version", "aanet_status_string", "aanet_mdcn_bwd_det_workspace_size",
-             "aanet_mdcn_bwd_ws_workspace_size", "aanet_conv2d_wgrad_workspace_size",
-             "aanet_conv_weight_pack_split_bytes", "aanet_conv3x3s2_pack_bytes",
-             "aanet_conv3x3_grouped_pack_bytes"] + list(_SIGNATURES))
+    return ["aanet_status_string"] + [n for n, _, _ in _SIZE_FUNCTIONS] + list(_SIGNATURES)
 
 
 def call(name, *args):
@@ -154,25 +157,38 @@ def conv_flags(*packed):
     return 0
 
 
-class PostStage(ctypes.Structure):
+class _Descriptor(ctypes.Structure):
+    """A descriptor struct of the C ABI: `struct_size` (the first member) is filled in with the
+    struct's size, which the library checks against its own (AANET_EABI on a mismatch)."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(ctypes.sizeof(self), *args, **kwargs)
+
+
+class PostStage(_Descriptor):
     """aanet_post_stage_t (include/aanet_mi355x.h)."""
-    _fields_ = [("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("act", ctypes.c_int),
-                ("out_nhwc", ctypes.c_void_p), ("disp", ctypes.c_void_p),
-                ("skip_outputs", ctypes.c_int)]
+    _fields_ = [("struct_size", ctypes.c_size_t), ("weight", ctypes.c_void_p),
+                ("bias", ctypes.c_void_p), ("act", ctypes.c_int), ("out_nhwc", ctypes.c_void_p),
+                ("disp", ctypes.c_void_p), ("skip_outputs", ctypes.c_int)]
 
 
-class CsaEpilogue(ctypes.Structure):
+class CsaEpilogue(_Descriptor):
     """aanet_csa_epilogue_t (include/aanet_mi355x.h)."""
-    _fields_ = [("out", ctypes.c_void_p), ("num_up", ctypes.c_int),
-                ("up", ctypes.c_void_p * 3), ("up_h", ctypes.c_int * 3),
-                ("up_w", ctypes.c_int * 3), ("act", ctypes.c_int),
+    _fields_ = [("struct_size", ctypes.c_size_t), ("out", ctypes.c_void_p),
+                ("num_up", ctypes.c_int), ("up", ctypes.c_void_p * 3),
+                ("up_h", ctypes.c_int * 3), ("up_w", ctypes.c_int * 3), ("act", ctypes.c_int),
                 ("post", ctypes.POINTER(PostStage))]
 
 
-class S2Terms(ctypes.Structure):
+class S2Terms(_Descriptor):
     """aanet_s2_terms_t (include/aanet_mi355x.h)."""
-    _fields_ = [("x2", ctypes.c_void_p), ("c2", ctypes.c_int), ("identity", ctypes.c_void_p),
-                ("up", ctypes.c_void_p), ("up_h", ctypes.c_int), ("up_w", ctypes.c_int)]
+    _fields_ = [("struct_size", ctypes.c_size_t), ("x2", ctypes.c_void_p), ("c2", ctypes.c_int),
+                ("identity", ctypes.c_void_p), ("up", ctypes.c_void_p), ("up_h", ctypes.c_int),
+                ("up_w", ctypes.c_int)]
+
+
+ABI_VERSION = 4  # AANET_ABI_VERSION (include/aanet_mi355x.h)
+EABI = -3  # AANET_EABI
 
 
 def stream_of(t):

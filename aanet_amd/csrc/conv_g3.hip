@@ -1,20 +1,25 @@
 // conv_g3.hip -- the deformable bottleneck's offset_conv (nets/deform.py:58-60, 76-79: 3x3,
 // dilation d, padding d, groups = deformable_groups, bias, no BN / activation) for gfx950, read
-// straight from the channels-last conv1 output that the DCN tail reads next.
+// from the channels-last conv1 output that the DCN tail reads next.
 //
 // Why not the conv engine.  The engine's halo tile holds ONE 32-channel group per workgroup
 // (grid.y = groups): at C2 scale 0 (64 -> 54, two groups of 32 -> 27, dilation 2) every
 // workgroup stages, splits and contracts a single K chunk, so its prologue and epilogue latency
-// are never hidden (≈115 us alone, 0.28 of the split ceiling, 208-222 us inside the step where
+// are never hidden (95-111 us alone, 0.33 of the split ceiling, 208-222 us inside the step where
 // it shares the CUs with the coarse-scale work).  Here a workgroup owns an 8 x 16 output tile
-// and EVERY group and output channel, and walks (group, chunk, tap) steps like the stride-2
-// row kernel (conv_s2.hip): wave w = tile row w, lane (kr = lane / 16, jj = lane % 16) = pixel
-// jj and channels 8kr..8kr+7 of the chunk -- exactly its B fragment of v_mfma_f32_16x16x32_bf16,
-// read from NHWC as two 16-byte loads (no im2col, no LDS staging of the input) -- and the
-// step's pre-split A fragments (the group's ceil(Cog / 16) co blocks x 3 pieces) arrive by
-// LDS-DMA two steps ahead into a ring of three slots.  Every wave issues exactly one DMA piece
-// per step (waves past the step's piece count copy into a dummy slot), so the counted
-// s_waitcnt of every wave names exactly the loads it needs.
+// and EVERY group and output channel, and walks its K chunks (group, 32-channel chunk) in turn.
+//
+// Per chunk the tile's (8 + 2d) x (16 + 2d) input halo is loaded once, split into three bf16
+// pieces once and stored in LDS (the engine's XOR-swizzled 64-byte rows: conflict-free
+// ds_read_b128 for any tap shift); the next chunk's halo loads are in flight in registers during
+// this chunk's taps.  Wave w = tile row w, lane (kr = lane / 16, jj = lane % 16) = pixel jj and
+// channels 8kr..8kr+7: tap (ti, tj) reads its B fragment (3 pieces) at halo position
+// (w + ti d, jj + tj d).  A step = one tap of one chunk; its pre-split A fragments (the group's
+// ceil(Cog / 16) co blocks x 3 pieces) arrive by LDS-DMA two steps ahead into a ring of three
+// slots, every wave issuing exactly one piece per step (waves past the step's piece count copy
+// into a dummy slot), so the counted s_waitcnt of every wave names exactly the loads it needs.
+// (The round-3 form of this kernel read and split the B values per tap -- 9x the split VALU --
+// and ran at 160 us.)
 //
 // Numerics: the split-bf16 contraction of the conv engine (split.h), taps ascending within a
 // chunk and chunks ascending within a group; output NCHW + bias.
@@ -54,13 +59,34 @@ struct G3Args {
   int N, C, H, W, Co, dil;
 };
 
-// G groups of NCC 32-channel chunks, NCB 16-row co blocks per group (Cog <= 16 NCB)
-template <int G, int NCC, int NCB>
-__global__ __launch_bounds__(NT, 4) void conv3x3_g3_kernel(G3Args a) {
+// put 4 channels (quad q4 of a 32-channel row) of halo position pos into the three piece planes
+// (plane stride pe bf16), at the engine's swizzled offset (mdcn.hip swz / put_split)
+__device__ __forceinline__ int g3_swz(int row, int q8) { return row * 32 + ((q8 ^ (((row >> 2) & 1) << 1)) << 3); }
+__device__ __forceinline__ void g3_put(__bf16 *plane, int pe, int pos, int q4, f32x4 v) {
+  float a[8] = {v[0], v[1], v[2], v[3], 0.f, 0.f, 0.f, 0.f};
+  bf16x8 b[3];
+  split8(a, b);
+  const int o = g3_swz(pos, q4 >> 1) + ((q4 & 1) << 2);
+#pragma unroll
+  for (int pc = 0; pc < 3; ++pc) {
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    const u32x4 w = __builtin_bit_cast(u32x4, b[pc]);
+    *reinterpret_cast<u32x2 *>(plane + pc * pe + o) = u32x2{w[0], w[1]};
+  }
+}
+
+// G groups of NCC 32-channel chunks, NCB 16-row co blocks per group (Cog <= 16 NCB), dilation D
+template <int G, int NCC, int NCB, int D>
+__global__ __launch_bounds__(NT, 2) void conv3x3_g3_kernel(G3Args a) {
   constexpr int NPC = 3 * NCB;             // 1-KB DMA pieces per step (<= 8)
   constexpr int AB = NPC * 1024;
-  constexpr int NS = G * NCC * 9;          // steps
+  constexpr int NCH = G * NCC;             // K chunks
+  constexpr int NS = NCH * 9;              // steps
+  constexpr int HWW = TC + 2 * D, HR = TR + 2 * D, NPOS = HR * HWW;  // halo
+  constexpr int HIT = (NPOS * 8 + NT - 1) / NT;  // halo quads per thread
+  constexpr int PE = NPOS * 32;            // bf16 per piece plane
   static_assert(NPC <= 8, "one DMA piece per wave and step");
+  __shared__ __attribute__((aligned(16))) __bf16 sH[3 * PE];
   __shared__ __attribute__((aligned(16))) char sA0[AB];
   __shared__ __attribute__((aligned(16))) char sA1[AB];
   __shared__ __attribute__((aligned(16))) char sA2[AB];
@@ -69,32 +95,42 @@ __global__ __launch_bounds__(NT, 4) void conv3x3_g3_kernel(G3Args a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kr = lane >> 4, jj = lane & 15;
-  const int H = a.H, W = a.W, C = a.C, d = a.dil;
+  const int H = a.H, W = a.W, C = a.C;
   const int tx = (W + TC - 1) / TC, ntiles = tx * ((H + TR - 1) / TR);
   const int nwg = gridDim.x, b0 = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b0 & 7;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b0 >> 3);
   const int n = bid / ntiles, tile = bid % ntiles;
-  const int y = (tile / tx) * TR + wave, x = (tile % tx) * TC + jj;
+  const int y0 = (tile / tx) * TR, x0 = (tile % tx) * TC;
+  const int y = y0 + wave, x = x0 + jj;
   const bool pv = y < H && x < W;
   const long HW = (long)H * W;
   const u32x4 xr = make_rsrc(a.x + n * HW * C, (int)(HW * C * 4));
-  // lane base: pixel (y - d, x - d), channel 8kr (tap (ti, tj) adds (ti W + tj) d pixels)
-  const int lbase = (((y - d) * W + (x - d)) * C + 8 * kr) * 4;
-  unsigned okmask = 0;  // bit k: tap k's input pixel lies inside the image
-#pragma unroll
-  for (int k = 0; k < 9; ++k)
-    okmask |= (pv && (unsigned)(y + (k / 3 - 1) * d) < (unsigned)H &&
-               (unsigned)(x + (k % 3 - 1) * d) < (unsigned)W) ? 1u << k : 0u;
+  const int Cg = C / G;
 
-  // step s = (group s / (9 NCC), chunk, tap s % 9): the lane's eight channels of its tap pixel
-  auto load_b = [&](int s, f32x4 (&v)[2]) {
-    const int g = s / (9 * NCC), cc = (s / 9) % NCC, k = s % 9, ti = k / 3, tj = k % 3;
-    const unsigned keep = 0u - ((okmask >> k) & 1u);
-    const unsigned off = ((unsigned)(lbase + (ti * W + tj) * d * C * 4) & keep) | (OOB & ~keep);
-    const int so = __builtin_amdgcn_readfirstlane((g * NCC + cc) * 32 * 4);
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(v[0]) : "v"(off), "s"(xr), "s"(so) : "memory");
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen offset:16" : "=v"(v[1]) : "v"(off), "s"(xr), "s"(so) : "memory");
+  // halo item i of this thread: position e >> 3, channel quad e & 7 (8 lanes = one 128-B line);
+  // the byte offset of its quad in chunk 0 (chunk ch adds the SGPR offset), OOB outside the image
+  int hoff[HIT];
+#pragma unroll
+  for (int i = 0; i < HIT; ++i) {
+    const int e = tid + NT * i, pos = e >> 3;
+    const int yy = y0 - D + pos / HWW, xx = x0 - D + pos % HWW;
+    const bool ok = pos < NPOS && yy >= 0 && yy < H && xx >= 0 && xx < W;
+    hoff[i] = ok ? ((yy * W + xx) * C + 4 * (e & 7)) * 4 : (int)OOB;
+  }
+  auto load_halo = [&](int ch, f32x4 (&hv)[HIT]) {
+    const int g = ch / NCC, cc = ch % NCC;
+    const int so = __builtin_amdgcn_readfirstlane((g * Cg + 32 * cc) * 4);
+#pragma unroll
+    for (int i = 0; i < HIT; ++i)
+      asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(hv[i]) : "v"(hoff[i]), "s"(xr), "s"(so) : "memory");
+  };
+  auto store_halo = [&](const f32x4 (&hv)[HIT]) {
+#pragma unroll
+    for (int i = 0; i < HIT; ++i) {
+      const int e = tid + NT * i, pos = e >> 3;
+      if (pos < NPOS) g3_put(sH, PE, pos, e & 7, hv[i]);
+    }
   };
   // one piece per wave: pieces 0..NPC-1 of the step's A fragments, waves past them a dummy copy
   auto issue_a = [&](int s, char *dst) {
@@ -105,10 +141,14 @@ __global__ __launch_bounds__(NT, 4) void conv3x3_g3_kernel(G3Args a) {
     asm volatile("global_load_lds_dwordx4 %0, off" :: "v"(src), "{m0}"(m0) : "memory");
   };
   // wait until at most CNT of this wave's vector-memory ops are in flight, then the workgroup
-  // barrier, in ONE asm statement; the B values about to be used pass through as operands
-  auto wait_bar = [&](auto cnt_c, f32x4 (&v)[2]) {
+  // barrier, in ONE asm statement (the halo values in flight pass through as operands, so no use
+  // is scheduled ahead of the wait)
+  auto wait_bar = [&](auto cnt_c, f32x4 (&hv)[HIT]) {
     constexpr int CNT = decltype(cnt_c)::value;
-    asm volatile("s_waitcnt vmcnt(%2)\n\ts_barrier" : "+v"(v[0]), "+v"(v[1]) : "n"(CNT) : "memory");
+    if constexpr (HIT == 4)
+      asm volatile("s_waitcnt vmcnt(%4)\n\ts_barrier" : "+v"(hv[0]), "+v"(hv[1]), "+v"(hv[2]), "+v"(hv[3]) : "n"(CNT) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%3)\n\ts_barrier" : "+v"(hv[0]), "+v"(hv[1]), "+v"(hv[2]) : "n"(CNT) : "memory");
   };
   auto slot = [&](int i) -> char * { return i == 0 ? sA0 : (i == 1 ? sA1 : sA2); };
 
@@ -117,29 +157,30 @@ __global__ __launch_bounds__(NT, 4) void conv3x3_g3_kernel(G3Args a) {
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int m = 0; m < NCB; ++m) acc[g][m] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 bv[3][2];
-  // steps s+1 and s+2 are in flight while step s computes: each step issues [A(s+2), B(s+2)]
-  // (3 ops) and then waits for everything but those three -- i.e. for step s+1's
+  // prologue: chunk 0's halo, A(0), A(1); everything landed, halo into LDS
+  f32x4 hv[HIT];
+  load_halo(0, hv);
   issue_a(0, sA0);
-  load_b(0, bv[0]);
   issue_a(1, sA1);
-  load_b(1, bv[1]);
-  wait_bar(std::integral_constant<int, 3>{}, bv[0]);
+  wait_bar(std::integral_constant<int, 0>{}, hv);
+  store_halo(hv);
+  __syncthreads();
+  // step s = (chunk s / 9, tap s % 9): issue A(s + 2) [and, at tap 0 of a chunk with a successor,
+  // the next chunk's halo after it], contract, then wait for A(s + 1) and barrier.  vmcnt counts
+  // in issue order, so A(s + 1) has landed when at most the ops issued after it remain: A(s + 2)
+  // (1) plus this step's halo loads (HIT) at tap 0 -- and at tap 1 the halo, now older than
+  // A(s + 2), must land too (two steps of cover).  At tap 8 the halo goes into LDS.
   for_steps([&](auto s_c) {
     constexpr int S = decltype(s_c)::value;
-    constexpr int GS = S / (9 * NCC);
-    if constexpr (S + 2 < NS) {
-      issue_a(S + 2, slot((S + 2) % 3));
-      load_b(S + 2, bv[(S + 2) % 3]);
-    }
-    float v8[8];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      v8[u] = bv[S % 3][0][u];
-      v8[4 + u] = bv[S % 3][1][u];
-    }
+    constexpr int CH = S / 9, K = S % 9, TI = K / 3, TJ = K % 3;
+    constexpr int GS = CH / NCC;
+    constexpr bool HALO_NEXT = K == 0 && CH + 1 < NCH;
+    if constexpr (S + 2 < NS) issue_a(S + 2, slot((S + 2) % 3));
+    if constexpr (HALO_NEXT) load_halo(CH + 1, hv);
+    const __bf16 *bp = sH + g3_swz((wave + TI * D) * HWW + jj + TJ * D, kr);
     bf16x8 B[3];
-    split8(v8, B);
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) B[pc] = *reinterpret_cast<const bf16x8 *>(bp + pc * PE);
     const char *ab = slot(S % 3) + lane * 16;
 #pragma unroll
     for (int m = 0; m < NCB; ++m) {
@@ -149,8 +190,12 @@ __global__ __launch_bounds__(NT, 4) void conv3x3_g3_kernel(G3Args a) {
       acc[GS][m] = mfma_split6(A, B, acc[GS][m]);
     }
     if constexpr (S + 1 < NS) {
-      constexpr int CNT = S + 2 < NS ? 3 : 0;
-      wait_bar(std::integral_constant<int, CNT>{}, bv[(S + 1) % 3]);
+      constexpr int CNT = (S + 2 < NS ? 1 : 0) + (HALO_NEXT ? HIT : 0);
+      wait_bar(std::integral_constant<int, CNT>{}, hv);
+      if constexpr (K == 8) {  // next chunk: every wave is done with this halo (the barrier)
+        store_halo(hv);
+        __syncthreads();
+      }
     }
   }, std::make_integer_sequence<int, NS>{});
 
@@ -234,17 +279,29 @@ int aanet_conv3x3_grouped_nhwc_f32(const float *x, const void *wsplit, const flo
   if (tiles > 0x7fffffffL) return AANET_EUNSUPPORTED;
   const dim3 grid((unsigned)tiles), blk(NT);
   hipStream_t st = as_hip(stream);
-  // the AANet offset convs: two 32-channel groups (scale 0) or one (single group)
+  // the AANet offset convs: two 32-channel groups (scale 0) or one (single group); dilation 1/2
+  auto launch = [&](auto g_c, auto ncc_c, auto ncb_c) -> bool {
+    constexpr int G = decltype(g_c)::value, NCC = decltype(ncc_c)::value, NCB = decltype(ncb_c)::value;
+    if (dil == 2)
+      hipLaunchKernelGGL((conv3x3_g3_kernel<G, NCC, NCB, 2>), grid, blk, 0, st, a);
+    else if (dil == 1)
+      hipLaunchKernelGGL((conv3x3_g3_kernel<G, NCC, NCB, 1>), grid, blk, 0, st, a);
+    else
+      return false;
+    return true;
+  };
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  bool ok = false;
   if (groups == 2 && ncc == 1 && ncb == 2)
-    hipLaunchKernelGGL((conv3x3_g3_kernel<2, 1, 2>), grid, blk, 0, st, a);
+    ok = launch(I2{}, I1{}, I2{});
   else if (groups == 2 && ncc == 1 && ncb == 1)
-    hipLaunchKernelGGL((conv3x3_g3_kernel<2, 1, 1>), grid, blk, 0, st, a);
+    ok = launch(I2{}, I1{}, I1{});
   else if (groups == 1 && ncc == 1 && ncb == 2)
-    hipLaunchKernelGGL((conv3x3_g3_kernel<1, 1, 2>), grid, blk, 0, st, a);
+    ok = launch(I1{}, I1{}, I2{});
   else if (groups == 1 && ncc == 2 && ncb == 2)
-    hipLaunchKernelGGL((conv3x3_g3_kernel<1, 2, 2>), grid, blk, 0, st, a);
-  else
-    return AANET_EUNSUPPORTED;
+    ok = launch(I1{}, I2{}, I2{});
+  if (!ok) return AANET_EUNSUPPORTED;
   return aanet_launch_status();
 }
 

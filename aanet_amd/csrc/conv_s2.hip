@@ -146,150 +146,11 @@ __device__ __forceinline__ void s2_epilogue(const S2Args &a, const f32x4 (&acc)[
     }
 }
 
-// NCH: input channels / 32 (1..4, the loop is unrolled over its 9 * NCH steps).  RING: steps in
-// the pipeline (step s computes while s+1 .. s+RING-1 load).
-template <int NCB, int NCH, int RING>
-__global__ __launch_bounds__(NT, 4) void conv3x3s2_kernel(S2Args a) {
-  constexpr int AB = NCB * 3 * 1024;  // this workgroup's A fragments of one (chunk, tap) step
-  // 1-KB weight DMA pieces per step: wave w issues pieces w, w + 8, ...: ND_HI of them for the
-  // first NPC % 8 waves, ND_LO for the others (each wave's s_waitcnt immediate picks its count)
-  constexpr int NPC = 3 * NCB, ND_LO = NPC / 8, ND_HI = (NPC + 7) / 8;
-  constexpr int NB = 8;  // B-operand dword loads per lane and step
-  constexpr int NS = 9 * NCH;
-  static_assert(RING == 2 || RING == 3, "pipeline depth");
-  // one __shared__ object per slot (see dcn_tile.hip for why separate objects)
-  __shared__ __attribute__((aligned(16))) char sA0[AB];
-  __shared__ __attribute__((aligned(16))) char sA1[AB];
-  __shared__ __attribute__((aligned(16))) char sA2[RING > 2 ? AB : 16];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int kr = lane >> 4, jj = lane & 15;
-  const int H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
-  const int tx = (Wo + TC - 1) / TC, ntiles = tx * ((Ho + TR - 1) / TR);
-  // XCD-aware bijective remap: each XCD walks a contiguous range of tiles (shared input rows)
-  const int nwg = gridDim.x, b0 = blockIdx.x;
-  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b0 & 7;
-  const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b0 >> 3);
-  const int n = bid / ntiles, tile = bid % ntiles;
-  const int cot = blockIdx.y, co_base = 16 * NCB * cot;  // this workgroup's output-channel tile
-  const bool nd_hi = wave < NPC % 8;                    // wave-uniform
-  const int y = (tile / tx) * TR + wave, x = (tile % tx) * TC + jj;
-  const bool pv = y < Ho && x < Wo;
-  const int HW = H * W;
-  const int C1 = a.C1, C2 = a.C - a.C1, nc1 = C1 / 32;
-  // buffer resources built by hand: the B loads are inline asm (see load_b)
-  const float *xb2 = a.x2 ? a.x2 + (long)n * C2 * HW : a.x;
-  const u32x4 xr = make_rsrc(a.x + (long)n * C1 * HW, C1 * HW * 4);
-  const u32x4 xr2 = make_rsrc(xb2, a.x2 ? C2 * HW * 4 : 0);
-  // lane base: channel 8kr of the chunk, input row 2y-1, column 2x-1 (tap (ti, tj) adds ti*W+tj)
-  const int yy0 = 2 * y - 1, xx0 = 2 * x - 1;
-  const int lbase = (8 * kr * HW + yy0 * W + xx0) * 4;
-  // bit k: tap k = (k / 3, k % 3) lies inside the image (a branch-free test in the loop: an
-  // exec-masked branch there makes the compiler wait for every load in flight at its join)
-  unsigned okmask = 0;
-#pragma unroll
-  for (int k = 0; k < 9; ++k)
-    okmask |= (pv && (unsigned)(yy0 + k / 3) < (unsigned)H && (unsigned)(xx0 + k % 3) < (unsigned)W) ? 1u << k : 0u;
-
-  // the eight channel values of this lane's B fragment at step s = (chunk s/9, tap s%9); out of
-  // the image: the out-of-range offset, whose buffer load returns 0 (zero padding).  Inline asm:
-  // with LDS-DMA loads in flight the compiler's waitcnt pass treats the vector-memory counter as
-  // unordered and waits for EVERY load before the first use of a B value (vmcnt(0)), which
-  // would cut the pipeline to one step.  The waits are explicit instead (wait_b): the values of
-  // step s+1 pass through the counted s_waitcnt at the end of step s as asm operands, so no use
-  // can be scheduled ahead of it.
-  auto load_b = [&](int s, float (&v)[8]) {
-    const int cc = s / 9, k = s - 9 * (s / 9), ti = k / 3, tj = k - 3 * (k / 3);
-    const unsigned keep = 0u - ((okmask >> k) & 1u);  // all ones inside the image
-    const unsigned off = ((unsigned)(lbase + (ti * W + tj) * 4) & keep) | (OOB & ~keep);
-    const bool second = cc >= nc1;
-    const int c0 = second ? cc - nc1 : cc;
-    u32x4 rs = second ? xr2 : xr;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) rs[q] = (unsigned)__builtin_amdgcn_readfirstlane((int)rs[q]);
-#pragma unroll
-    for (int u = 0; u < NB; ++u) {
-      const int so = __builtin_amdgcn_readfirstlane((32 * c0 + u) * HW * 4);
-      asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(v[u]) : "v"(off), "s"(rs), "s"(so) : "memory");
-    }
-  };
-  // this wave's loads issued before the last CNT steps' landed (CNT = the steps issued after the
-  // one awaited), then the workgroup barrier (every wave's DMA of that step landed) in the SAME
-  // asm statement: the bare s_barrier intrinsic does not order memory for the compiler, and an A
-  // read hoisted between the wait and the barrier would race with the other waves' DMAs.
-  // __syncthreads' fence is not used: it waits for every load in flight (vmcnt(0)).  The
-  // awaited step's B values pass through the asm as operands, so no use is scheduled before it.
-  // ONE asm statement for every wave (a branch between two would make the compiler copy the
-  // pending registers into common ones before it, reading them before they land): the count
-  // assumes ND_LO pieces per step, so the waves with ND_HI wait for one load more than needed.
-  auto wait_step = [&](auto cnt_c, float (&v)[8]) {
-    constexpr int CNT = decltype(cnt_c)::value;
-    asm volatile("s_waitcnt vmcnt(%8)\n\ts_barrier"
-                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
-                 : "n"(CNT * (NB + ND_LO)) : "memory");
-  };
-  // weight DMA, inline asm as well: the compiler then sees no vector-memory op in the loop and
-  // inserts no wait of its own (it cannot count LDS-DMA loads against ordinary loads, and waited
-  // for all of them before reading an A slot); every wait is explicit (wait_b)
-  auto issue_a = [&](int s, char *dst) {
-    const char *src = a.wsplit + ((long)s * a.ncbt + NCB * cot) * 3072 + lane * 16;
-#pragma unroll
-    for (int r = 0; r < ND_HI; ++r) {
-      const int pc = wave + 8 * r;
-      if (r == ND_LO && !nd_hi) break;  // wave-uniform
-      const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void *)(dst + pc * 1024));
-      asm volatile("global_load_lds_dwordx4 %0, off" :: "v"(src + pc * 1024), "{m0}"(m0) : "memory");
-    }
-  };
-
-  f32x4 acc[NCB];
-#pragma unroll
-  for (int m = 0; m < NCB; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // step s: issue step s+RING-1's weights and input (into the slot step s-1 used: every wave
-  // passed the barrier after reading it), contract step s, then wait for step s+1 (only the
-  // steps issued after it stay in flight) and barrier.
-  auto slot = [&](int i) -> char * { return i == 0 ? sA0 : (i == 1 ? sA1 : sA2); };
-  float v[RING][8];
-  for_steps([&](auto j_c) {
-    constexpr int J = decltype(j_c)::value;
-    if constexpr (J < RING - 1) {
-      issue_a(J, slot(J));
-      load_b(J, v[J]);
-    }
-  }, std::make_integer_sequence<int, RING>{});
-  wait_step(std::integral_constant<int, RING - 2>{}, v[0]);  // step 0 landed
-  for_steps([&](auto s_c) {
-    constexpr int S = decltype(s_c)::value;
-    constexpr int NX = S + RING - 1;  // the step issued now
-    if constexpr (NX < NS) {
-      issue_a(NX, slot(NX % RING));
-      load_b(NX, v[NX % RING]);
-    }
-    bf16x8 B[3];
-    split8(v[S % RING], B);
-    const char *ab = slot(S % RING) + lane * 16;
-#pragma unroll
-    for (int m = 0; m < NCB; ++m) {
-      bf16x8 A[3];
-#pragma unroll
-      for (int pc = 0; pc < 3; ++pc) A[pc] = *reinterpret_cast<const bf16x8 *>(ab + (m * 3 + pc) * 1024);
-      acc[m] = mfma_split6(A, B, acc[m]);
-    }
-    if constexpr (S + 1 < NS) {
-      constexpr int LAST = NX < NS ? NX : NS - 1;  // the newest step issued
-      wait_step(std::integral_constant<int, LAST - (S + 1)>{}, v[(S + 1) % RING]);
-    }
-  }, std::make_integer_sequence<int, NS>{});
-
-  s2_epilogue<NCB>(a, acc, n, y, x, kr, co_base, pv);
-}
-
 // ---- row form for the wide tiles (round 3) ------------------------------------------------
-// A counter pass of the form above at the C2 heads shape (tools/s2_pmc.sh): the matrix pipe busy
-// 37 % of the kernel, the texture unit 47 %, and the L1 sending 8.4x the input's bytes to L2:
-// every (channel, tap) is its own dword gather, so a lane's three taps of one input row are
+// A counter pass of the round-3 straight-line form (one dword gather per (channel, tap); removed
+// in round 4) at the C2 heads shape (tools/s2_pmc.sh): the matrix pipe busy 37 % of the kernel,
+// the texture unit 47 %, and the L1 sending 8.4x the input's bytes to L2: every (channel, tap)
+// was its own dword gather, so a lane's three taps of one input row are
 // three instructions that touch the same lines three steps apart, and with 16 waves per CU
 // streaming through a 32 KB L1 the lines are gone by the second touch.  (A rolled 64-VGPR
 // variant with twice the waves per SIMD was SLOWER, 102 vs 91 us: more waves, more misses.)
@@ -300,8 +161,8 @@ __global__ __launch_bounds__(NT, 4) void conv3x3s2_kernel(S2Args a) {
 // at NCB = 6, still two workgroups per CU); row r+1 is issued at the first tap of row r, so it
 // has the row's three steps to land.
 // Left border: the x = 0 lane loads columns 0..2 and shifts them (column -1 is padding); right
-// border (odd W): column 2x+1 = W is zeroed.  Same numerics as the form above (taps and chunks
-// in ascending order, the same split and piece products): bit-identical outputs.
+// border (odd W): column 2x+1 = W is zeroed.  Same numerics as the straight-line form (taps and
+// chunks in ascending order, the same split and piece products): bit-identical outputs.
 typedef float f32x3 __attribute__((ext_vector_type(3)));
 
 template <int NCB, int NCH>
@@ -360,8 +221,11 @@ __global__ __launch_bounds__(NT, 4) void conv3x3s2_rows_kernel(S2Args a) {
     }
   };
   // wait until this wave has at most CNT vector-memory ops in flight, then the workgroup barrier,
-  // in ONE asm statement (see conv3x3s2_kernel's wait_step); the row values about to be used
-  // pass through as operands so that no use is scheduled ahead of the wait
+  // in ONE asm statement: the bare s_barrier intrinsic does not order memory for the compiler (an
+  // A read hoisted between wait and barrier would race with the other waves' DMAs), and
+  // __syncthreads' fence would wait for every load in flight.  A branch between two such
+  // statements would make the compiler copy the pending registers before them.  The row values
+  // about to be used pass through as operands so that no use is scheduled ahead of the wait
   auto wait_bar = [&](auto cnt_c, f32x3 (&v)[8]) {
     constexpr int CNT = decltype(cnt_c)::value;
     asm volatile("s_waitcnt vmcnt(%8)\n\ts_barrier"
@@ -460,38 +324,13 @@ __global__ void conv3x3s2_pack_kernel(const float *__restrict__ w, bf16x8 *__res
   }
 }
 
-// Pipeline depth: three steps for the narrow tiles (their steps are short: a third step in
-// flight hides the load latency), two for the wide ones (whose LDS and registers it would cost
-// occupancy; A/B build: -DAANET_S2_WIDE_RING=3)
-#ifndef AANET_S2_WIDE_RING
-#define AANET_S2_WIDE_RING 2
-#endif
-int s2_rows_enabled() {
-  static const int on = [] {
-    const char *e = getenv("AANET_S2_ROWS");
-    return e ? atoi(e) : 1;
-  }();
-  return on;
-}
-
 template <int NCB>
 void launch_s2(int nch, dim3 grid, dim3 blk, hipStream_t st, const S2Args &a) {
-  // the row form (AANET_S2_ROWS=0: the straight-line form above; the narrow tiles measured
-  // 21 -> 16 us (branch-2 merged conv) and 14 -> 11 us (64 -> 16) alone, the step within noise)
-  if (s2_rows_enabled()) {
-    switch (nch) {
-      case 1: hipLaunchKernelGGL((conv3x3s2_rows_kernel<NCB, 1>), grid, blk, 0, st, a); return;
-      case 2: hipLaunchKernelGGL((conv3x3s2_rows_kernel<NCB, 2>), grid, blk, 0, st, a); return;
-      case 3: hipLaunchKernelGGL((conv3x3s2_rows_kernel<NCB, 3>), grid, blk, 0, st, a); return;
-      default: hipLaunchKernelGGL((conv3x3s2_rows_kernel<NCB, 4>), grid, blk, 0, st, a); return;
-    }
-  }
-  constexpr int R = NCB <= 2 ? 3 : AANET_S2_WIDE_RING;
   switch (nch) {  // the AANet pyramid: 32 / 64 / 96 input channels
-    case 1: hipLaunchKernelGGL((conv3x3s2_kernel<NCB, 1, R>), grid, blk, 0, st, a); break;
-    case 2: hipLaunchKernelGGL((conv3x3s2_kernel<NCB, 2, R>), grid, blk, 0, st, a); break;
-    case 3: hipLaunchKernelGGL((conv3x3s2_kernel<NCB, 3, R>), grid, blk, 0, st, a); break;
-    default: hipLaunchKernelGGL((conv3x3s2_kernel<NCB, 4, R>), grid, blk, 0, st, a); break;
+    case 1: hipLaunchKernelGGL((conv3x3s2_rows_kernel<NCB, 1>), grid, blk, 0, st, a); return;
+    case 2: hipLaunchKernelGGL((conv3x3s2_rows_kernel<NCB, 2>), grid, blk, 0, st, a); return;
+    case 3: hipLaunchKernelGGL((conv3x3s2_rows_kernel<NCB, 3>), grid, blk, 0, st, a); return;
+    default: hipLaunchKernelGGL((conv3x3s2_rows_kernel<NCB, 4>), grid, blk, 0, st, a); return;
   }
 }
 
@@ -516,6 +355,7 @@ int aanet_conv3x3s2_terms_f32(const float *x, const void *wsplit, const float *b
                               int c, int h, int w, int co, int co_a, float *out_a, int act_a,
                               float *out_b, int act_b, const aanet_s2_terms_t *terms,
                               aanet_stream_t stream) {
+  if (terms && terms->struct_size != sizeof(aanet_s2_terms_t)) return AANET_EABI;
   if (!x || !wsplit || n < 0 || h < 0 || w < 0 || co_a < 0 || co_a > co) return AANET_EINVAL;
   const int c2 = terms && terms->x2 ? terms->c2 : 0;
   if (c2 < 0 || (terms && terms->x2 == nullptr && terms->c2 != 0)) return AANET_EINVAL;

@@ -615,6 +615,11 @@ __global__ __launch_bounds__(256) void shift_volume_kernel(const float *__restri
 // (oc, d) plane receives YB*W contiguous floats (16-byte non-temporal stores): long contiguous
 // write streams run at 5.2 TB/s where one-row (1.2 KB) segments ran at 3.5 TB/s
 // (tools/shift_lab.hip, C5 [4,32,96,312], D=48).  HBM reads are exactly the two feature maps.
+// LDS layout (round 4): each row is stored as 4 residue planes, element x at (x & 3) * W/4 + x/4.
+// A thread writes output columns 4k..4k+3 and reads source element 4k + u - d: in the row-major
+// layout the 32 lanes of a ds_read_b32 hit words 4 apart (8 banks: a 4-way conflict on every
+// read, 5.3k conflict cycles per wave at C5); here consecutive lanes read consecutive words of one
+// residue plane ((u - d) & 3 is the same for the lanes of a d), conflict-free.
 template <bool CONCAT>
 __global__ __launch_bounds__(256) void shift_volume_band_kernel(const float *__restrict__ L,
                                                                 const float *__restrict__ R,
@@ -630,8 +635,14 @@ __global__ __launch_bounds__(256) void shift_volume_band_kernel(const float *__r
   const f32x4 *gl = reinterpret_cast<const f32x4 *>(L + ((long)bc * H + y0) * W);
   const f32x4 *gr = reinterpret_cast<const f32x4 *>(R + ((long)bc * H + y0) * W);
   for (int q = tid; q < S4; q += 256) {
-    reinterpret_cast<f32x4 *>(sL)[q] = __builtin_nontemporal_load(gl + q);
-    reinterpret_cast<f32x4 *>(sR)[q] = __builtin_nontemporal_load(gr + q);
+    const f32x4 vl = __builtin_nontemporal_load(gl + q), vr = __builtin_nontemporal_load(gr + q);
+    const int yy = q / W4, k = q - yy * W4;
+    float *dl = sL + yy * W + k, *dr = sR + yy * W + k;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      dl[u * W4] = vl[u];
+      dr[u * W4] = vr[u];
+    }
   }
   __syncthreads();
   const int OC = CONCAT ? 2 * C : C;
@@ -639,14 +650,15 @@ __global__ __launch_bounds__(256) void shift_volume_band_kernel(const float *__r
   float *o0 = out + (((long)b * OC + c) * D * H + y0) * W;               // oc = c
   float *o1 = CONCAT ? o0 + (long)C * D * HW : nullptr;                  // oc = C + c
   for (int e = tid; e < D * S4; e += 256) {
-    const int d = e / S4, r = e - d * S4, yy = r / W4, x = 4 * (r - yy * W4);
+    const int d = e / S4, r = e - d * S4, yy = r / W4, k = r - yy * W4, x = 4 * k;
     const float *l = sL + yy * W, *rr = sR + yy * W;
     f32x4 vl, vr;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const bool ok = x + u >= d;
-      vl[u] = ok ? l[x + u] : 0.f;
-      vr[u] = ok ? rr[x + u - d] : 0.f;
+      const int xs = x + u - d;  // source column of the right map
+      const bool ok = xs >= 0;
+      vl[u] = ok ? l[u * W4 + k] : 0.f;
+      vr[u] = ok ? rr[(xs & 3) * W4 + (xs >> 2)] : 0.f;
     }
     const long off = (long)d * HW + 4 * r;
     if (CONCAT) {

@@ -45,6 +45,6 @@ struct DcnTileArgs {
 // or a positive hipError_t.
 int dcn_tile_launch(const DcnTileArgs &a, hipStream_t stream);
 // 1 when the window kernel takes this shape (3x3, stride 1, pad = dil = 2, C = Co = Co2 = 64 or
-// 32, two deformable groups, W % 4 == 0) and AANET_DCN_WINDOW is not 0.
+// 32, two deformable groups, W % 4 == 0).
 int dcn_tile_supported(int c, int co, int co2, int kh, int kw, int stride, int pad, int dil,
                        int dg, int groups, int w);

@@ -646,19 +646,11 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
 
 }
 
-int window_enabled() {
-  static const int on = [] {
-    const char *e = getenv("AANET_DCN_WINDOW");
-    return e ? atoi(e) : 1;
-  }();
-  return on;
-}
-
 }  // namespace
 
 int dcn_tile_supported(int c, int co, int co2, int kh, int kw, int stride, int pad, int dil,
                        int dg, int groups, int w) {
-  return window_enabled() && (c == 64 || c == 32) && co == c && co2 == c && kh == 3 && kw == 3 &&
+  return (c == 64 || c == 32) && co == c && co2 == c && kh == 3 && kw == 3 &&
          stride == 1 && pad == dil && dil == 2 && dg == 2 && groups == 1 && w % 4 == 0;
 }
 

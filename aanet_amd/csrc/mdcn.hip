@@ -444,11 +444,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   // LDS slot to the threads that stage channels of that pixel and group (the VALU it saves is
   // matrix-pipe time).
   constexpr int PSLOT = GPC * PTT * 8;
-  // HALO 3 (3x3, stride 2, pad 1, NCHW input): a 4 x 16 output tile reads a 9 x 33 input halo,
-  // whose 32-channel piece planes (57 KB) exceed the two im2col buffers
-  constexpr int HALO3_FLOATS = HALO == 3 ? 9 * 33 * 32 * 3 / 2 : 0;
-  constexpr int SMEM = 2 * BUF > HALO3_FLOATS ? 2 * BUF : HALO3_FLOATS;
-  __shared__ __attribute__((aligned(16))) float smem[SMEM + (MODE ? 2 * PSLOT : 0)];
+  __shared__ __attribute__((aligned(16))) float smem[2 * BUF + (MODE ? 2 * PSLOT : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool pwave = __builtin_amdgcn_readfirstlane(wave) < GPC * PTT / 64;  // tid < GPC*PTT
@@ -456,10 +452,9 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   const int wc0 = __builtin_amdgcn_readfirstlane((wave / WP) * NCB);  // first co block of the wave
   const int wp0 = __builtin_amdgcn_readfirstlane((wave % WP) * NPB);  // first px block of the wave
   const long P = (long)a.Ho * a.Wo;
-  static_assert(!HALO || (MODE == 0 && PREC == 1 &&
-                          (HALO == 3 ? PTT == 64 && !(LAYOUT & 1) : PTT == 128 && (LAYOUT & 1)) && !(HALO == 3 && TAIL)),
+  static_assert(!HALO || (MODE == 0 && PREC == 1 && HALO <= 2 && PTT == 128 && (LAYOUT & 1)),
                 "halo configuration");
-  constexpr int TRH = HALO == 3 ? 4 : 8;  // output rows of a halo tile (16 columns)
+  constexpr int TRH = 8;  // output rows of a halo tile (16 columns)
   const int htx = HALO ? (a.Wo + 15) / 16 : 1;
   const int ntiles = HALO ? htx * ((a.Ho + TRH - 1) / TRH) : (int)((P + PTT - 1) / PTT);
   // XCD-aware remap of the pixel-tile index (bijective for any grid size)
@@ -878,38 +873,17 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   }
 
   if constexpr (HALO) {
-    // HALO 1/2: stride 1, dilation = padding = d; HALO 3: stride 2, dilation 1, padding 1
-    constexpr bool S2 = HALO == 3;
-    constexpr int d = S2 ? 1 : HALO;  // tap spacing in the halo
-    constexpr int hw = S2 ? 33 : 16 + 2 * d, npos = (S2 ? 9 : 8 + 2 * d) * hw;
-    const int hy = S2 ? 2 * hy0 - 1 : hy0 - d, hx = S2 ? 2 * hx0 - 1 : hx0 - d;
-    constexpr int HIT = S2 ? 1 : (npos * 8 + FNT - 1) / FNT;  // halo quads per thread (NHWC)
-    // NCHW (HALO 3): unit = (halo row, column quad, channel quad): 9 rows x 9 quads (input columns
-    // 2*hx0-4 .. 2*hx0+31, the first three unused) x 8 channel quads = 648 units, 2 per thread;
-    // a unit is 4 channel rows x 4 columns, stored as 4 positions of 4 channels (put_split)
-    constexpr int NU = 9 * 9 * 8, UIT = S2 ? (NU + FNT - 1) / FNT : 1;
-    f32x4 hv[HIT], hu[UIT][4];
-    auto load_halo_nchw = [&](int c0) {
-#pragma unroll
-      for (int i = 0; i < UIT; ++i) {
-        const int u = tid + FNT * i, cq = u / 81, rq = u % 81, row = rq / 9, qd = rq % 9;
-        const int yy = hy + row, xx = 2 * hx0 - 4 + 4 * qd;
-        const bool ok = u < NU && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;  // W % 4 == 0
-#pragma unroll
-        for (int ch = 0; ch < 4; ++ch) {
-          const int off = ok ? (((c0 + 4 * cq + ch) * a.H + yy) * a.W + xx) * 4 : img_bytes;
-          hu[i][ch] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
-        }
-      }
-    };
+    // stride 1, dilation = padding = d (the round-3 stride-2 NCHW form, HALO 3, was removed in
+    // round 4: faster alone, slower in the two-stream step)
+    constexpr int d = HALO;  // tap spacing in the halo
+    constexpr int hw = 16 + 2 * d, npos = (8 + 2 * d) * hw;
+    const int hy = hy0 - d, hx = hx0 - d;
+    constexpr int HIT = (npos * 8 + FNT - 1) / FNT;  // halo quads per thread (NHWC)
+    f32x4 hv[HIT];
     // 64-channel tiles recompute the halo quad offsets per chunk (a few VALU) rather than hold
     // them across the chunk loop: held, they were spilled to scratch and re-read every chunk
     // (76 B/lane at the 128-VGPR cap).  32-channel tiles have the registers to hold them.
     auto load_halo = [&](int c0) {
-      if constexpr (S2) {
-        load_halo_nchw(c0);
-        return;
-      }
       const int soff = __builtin_amdgcn_readfirstlane(c0 * 4);
       int t = tid;
       if constexpr (CO_T >= 64) asm volatile("" : "+v"(t));  // keep the arithmetic in the loop
@@ -952,7 +926,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       asm volatile("" : "+v"(col));  // recomputed per tap (not hoisted as 18 live addresses)
 #pragma unroll
       for (int b = 0; b < NPB; ++b) {
-        const int pos = S2 ? (2 * (wp0 + b) + ti) * hw + 2 * col + tj : (wp0 + b + ti * d) * hw + col + tj * d;
+        const int pos = (wp0 + b + ti * d) * hw + col + tj * d;
         const __bf16 *sH = reinterpret_cast<const __bf16 *>(smem) + swz(pos, kr);
         bf16x8 fb[3];
 #pragma unroll
@@ -961,39 +935,19 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
         for (int m = 0; m < NCB; ++m) acc[m][b] = mfma_split6(cur[m], fb, acc[m][b]);
       }
     };
-    // HALO 3 with 64-channel tiles: the next chunk's halo is not held in registers across the nine
-    // taps (32 VGPRs: they spilled at the 128 cap); its loads are issued just before the barrier
-    // that ends the previous chunk, so they overlap the slowest waves' last taps only
-    constexpr bool LATE = S2 && CO_T >= 64;
     auto stage = [&](int c0) {
-      if constexpr (LATE) load_halo(c0);
       __syncthreads();  // every wave is done with the previous chunk's halo
-      if constexpr (S2) {
-#pragma unroll
-        for (int i = 0; i < UIT; ++i) {
-          const int u = tid + FNT * i, cq = u / 81, rq = u % 81, row = rq / 9, qd = rq % 9;
-          if (u >= NU) continue;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {  // column 2*hx0-4 + 4qd + e -> halo column 4qd + e - 3
-            const int col = 4 * qd + e - 3;
-            if (col < 0) continue;
-            put_split(reinterpret_cast<__bf16 *>(smem), npos * 32, row * hw + col, cq,
-                      f32x4{hu[i][0][e], hu[i][1][e], hu[i][2][e], hu[i][3][e]});
-          }
-        }
-      } else {
 #pragma unroll
       for (int i = 0; i < HIT; ++i) {
         const int pos = (tid + FNT * i) >> 3;
         if (pos < npos) put_split(reinterpret_cast<__bf16 *>(smem), npos * 32, pos, tid & 7, hv[i]);
       }
-      }
       __syncthreads();
       const bool more = c0 + 32 < cend;
-      if (more && !LATE) load_halo(c0 + 32);
+      if (more) load_halo(c0 + 32);
       return more;
     };
-    if constexpr (!LATE) load_halo(cbeg);
+    load_halo(cbeg);
     load_ha(ha0, cbeg, 0);
     // nine taps per chunk: the A buffers alternate, so consecutive chunks start on opposite ones
     for (int c0 = cbeg; c0 < cend; c0 += 64) {
@@ -2320,31 +2274,6 @@ template <int MODE, int CO_T, int PTT, int FULL, int CFG>
 void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
   const dim3 blk(FNT);
   if constexpr (FULL && CFG == 0 && CO_T >= 32) {  // split-bf16 contraction (PREC 1)
-    static const int nosched = [] { const char *e = getenv("AANET_SPLIT_NOSCHED"); return e ? atoi(e) : 0; }();
-    if (a.split && packed && nosched && !(MODE == 1 && a.tail_w && a.layout == 1)) {  // A/B switch
-      if (a.tail_w) {
-        if (a.layout == 1)
-          hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 0, 1, 1, CFG, 1>), grid, blk, 0, st, a);
-        else
-          hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 0, 1, 0, CFG, 1>), grid, blk, 0, st, a);
-      } else if (a.layout == 1) {
-        hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 0, 1, 1, CFG, 1>), grid, blk, 0, st, a);
-      } else if (a.layout == 2) {
-        hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 0, 1, 2, CFG, 1>), grid, blk, 0, st, a);
-      } else {
-        hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 0, 0, 1, 0, CFG, 1>), grid, blk, 0, st, a);
-      }
-      return;
-    }
-    if constexpr (MODE == 0 && PTT == 64) {
-      if (a.split && packed && a.halo == 3) {  // 3x3 stride-2 halo-tile form (NCHW input)
-        if (a.layout == 2)
-          hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 64, 1, 0, 1, 1, 2, CFG, 1, 3>), grid, blk, 0, st, a);
-        else
-          hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 64, 1, 0, 1, 1, 0, CFG, 1, 3>), grid, blk, 0, st, a);
-        return;
-      }
-    }
     if constexpr (MODE == 0 && PTT == 128) {
       if (a.split && packed && a.halo == 1) {  // 3x3 stride-1 halo-tile form (NHWC input), HALO = dil
         if (a.dil == 1) {
@@ -2367,12 +2296,7 @@ void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
         return;
       }
     }
-    // AANET_SPLIT_DCN_TAIL=0: the deformable tail kernel with NHWC staging on the exact f32
-    // contraction (it ran so while its packed-fp32 corner blend was not reproducible, see the
-    // NHWC store_stage; A/B switch now)
-    static const int allow_racy = [] { const char *e = getenv("AANET_SPLIT_DCN_TAIL"); return e ? atoi(e) : 1; }();
-    const bool racy = MODE == 1 && a.tail_w && a.layout == 1 && !allow_racy;
-    if (a.split && packed && !racy) {
+    if (a.split && packed) {
       if (a.tail_w) {
         if (a.layout == 1)
           hipLaunchKernelGGL((conv_fwd_kernel<MODE, CO_T, PTT, 1, 1, 1, 1, 1, CFG, 1>), grid, blk, 0, st, a);
@@ -2461,14 +2385,9 @@ int launch_fwd(const MdcnArgs &a_in, int packed, hipStream_t st) {
   const int ncot = host_div_up(Cog, co_t);
   // 128-pixel tiles when they still give >= 2 workgroups per CU (the scale-1 convs of the C2
   // pyramid, 832 tiles: stride-2 64->64 exchange conv 93 -> 86 us), else 64
-  static const int ptt_min = [] { const char *e = getenv("AANET_PTT128_MIN_WG"); return e ? atoi(e) : 512; }();
-  int ptt = co_t == 16 || (long)a.N * host_div_up(P, 128) * a.groups * ncot >= ptt_min ? 128 : 64;
-  static const int ptt_env = [] { const char *e = getenv("AANET_PTT"); return e ? atoi(e) : 0; }();
-  if (ptt_env == 64 && co_t != 16) ptt = 64;  // A/B switches (tools/conv_microbench.py)
-  if (ptt_env == 128) ptt = 128;
+  int ptt = co_t == 16 || (long)a.N * host_div_up(P, 128) * a.groups * ncot >= 512 ? 128 : 64;
   if (full_cfg(a, MODE, co_t) == 1) ptt = 128;  // 16-channel chunks are staged 4 per thread
-  static const int nohalo = [] { const char *e = getenv("AANET_NO_HALO"); return e ? atoi(e) : 0; }();
-  a.halo = !nohalo && MODE == 0 && a.split && packed && (a.layout & 1) && a.kh == 3 && a.kw == 3 &&
+  a.halo = MODE == 0 && a.split && packed && (a.layout & 1) && a.kh == 3 && a.kw == 3 &&
            a.stride == 1 && a.pad == a.dil && a.dil <= 2 && co_t >= 32 && full_cfg(a, 0, co_t) == 0;
   if (a.halo) ptt = 128;
   // post stage (aanet_post_stage_t): the HALO 1 tail with the CSA epilogue, 64 -> 64 channels,
@@ -2476,19 +2395,7 @@ int launch_fwd(const MdcnArgs &a_in, int packed, hipStream_t st) {
   if (a.post && (MODE != 0 || !a.csa_out || !a.halo || a.dil != 1 || co_t != 64 || a.Co2 != 64 ||
                  a.post->disp || !a.post->out_nhwc || a.post->skip_outputs || !a.split || !packed))
     return AANET_EUNSUPPORTED;
-  // stride-2 halo form (the CSA down-sampling convs, aggregation.py:364-372): NCHW input.  Opt-in
-  // (AANET_HALO_S2=1): alone it is 9-16 % faster than the im2col form at the C2 scale-0 shapes,
-  // but in the two-stream eval schedule its 57 KB workgroups take LDS from the scale-0 chain's
-  // kernels and the step got 2 % slower
-  static const int halo2 = [] { const char *e = getenv("AANET_HALO_S2"); return e ? atoi(e) : 0; }();
-  if (!nohalo && halo2 && MODE == 0 && a.split && packed && !(a.layout & 1) && !a.tail_w &&
-      a.kh == 3 && a.kw == 3 && a.stride == 2 && a.pad == 1 && a.dil == 1 && co_t >= 32 &&
-      full_cfg(a, 0, co_t) == 0 && a.W % 4 == 0) {
-    a.halo = 3;
-    ptt = 64;
-  }
-  const int trh = a.halo == 3 ? 4 : 8;
-  dim3 grid((unsigned)(a.halo ? (long)a.N * host_div_up(a.Wo, 16) * host_div_up(a.Ho, trh)
+  dim3 grid((unsigned)(a.halo ? (long)a.N * host_div_up(a.Wo, 16) * host_div_up(a.Ho, 8)
                               : a.N * host_div_up(P, ptt)),
             (unsigned)(a.groups * ncot));
   if (ptt == 128) {
@@ -2645,7 +2552,9 @@ __global__ void pack_split_kernel(const float *__restrict__ w, bf16x8_t *__restr
 
 int set_csa(MdcnArgs &a, const aanet_csa_epilogue_t *csa) {
   if (!csa) return AANET_OK;
+  if (csa->struct_size != sizeof(aanet_csa_epilogue_t)) return AANET_EABI;
   a.post = csa->post;
+  if (a.post && a.post->struct_size != sizeof(aanet_post_stage_t)) return AANET_EABI;
   if (a.post && ((!a.post->out_nhwc && !a.post->disp) || !a.post->weight || a.post->act < 0 ||
                  a.post->act > 2))
     return AANET_EINVAL;

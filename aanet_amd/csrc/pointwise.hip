@@ -297,8 +297,7 @@ void launch_ci(const PwArgs &a, hipStream_t st) {
 
 int pw_conv_supported(int c, int co, int kh, int kw, int stride, int pad, int groups, long np,
                       int out_nhwc, int p) {
-  static const int on = [] { const char *e = getenv("AANET_PW"); return e ? atoi(e) : 1; }();
-  return on && kh == 1 && kw == 1 && stride == 1 && pad == 0 && groups == 1 && (c == 32 || c == 64) &&
+  return kh == 1 && kw == 1 && stride == 1 && pad == 0 && groups == 1 && (c == 32 || c == 64) &&
          co >= 1 && co <= 64 && np + 16 < 0x7fffffffL && (!out_nhwc || co % 4 == 0) && p >= 1;
 }
 

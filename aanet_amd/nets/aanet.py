@@ -20,6 +20,7 @@ from .feature import (FeaturePyramidNetwork, FeaturePyrmaid, GANetFeature, GCNet
                       PSMNetFeature, StereoNetFeature)
 from .refinement import HourglassRefinement, StereoDRNetRefinement, StereoNetRefinement
 from .resnet import AANetFeature
+from .._precision import fp32_convs
 
 _REFINEMENT = {'stereonet': StereoNetRefinement, 'stereodrnet': StereoDRNetRefinement,
                'hourglass': HourglassRefinement}
@@ -151,6 +152,7 @@ class AANet(FoldCacheMixin, nn.Module):
             pyramid.append(disparity)
         return pyramid
 
+    @fp32_convs
     def forward(self, left_img, right_img):
         """aanet.py:211-229 -> disparity pyramid, coarse to fine (hot-path disparities, then
         one per refinement stage)."""

@@ -18,6 +18,7 @@ import torch.nn as nn
 from .. import ops
 from ._fuse import FoldCacheMixin, conv_bn_act, folded, s2_conv_ok, s2_pack, s2_pack_k, use_fused
 from .deform import DeformSimpleBottleneck, SimpleBottleneck
+from .._precision import fp32_convs
 
 
 _SIDE_STREAMS = {}
@@ -33,8 +34,7 @@ def side_streams(device, n):
 
 
 def concurrent_scales():
-    """AANET_CONCURRENT_SCALES=0 runs the whole eval aggregation on one stream (A/B switch);
-    AANET_SIDE_STREAMS=1 puts every coarse scale on one shared side stream (round-2 schedule)."""
+    """AANET_CONCURRENT_SCALES=0 runs the whole eval aggregation on one stream (A/B switch)."""
     return os.environ.get("AANET_CONCURRENT_SCALES", "1") != "0"
 
 
@@ -54,24 +54,6 @@ def s2_sums():
     """AANET_S2_SUMS=0 keeps the coarse branches' CSA sums in aanet_csa_sum_f32 kernels instead of
     the stride-2 kernels' epilogues (A/B switch)."""
     return os.environ.get("AANET_S2_SUMS", "1") != "0"
-
-
-def num_side_streams(num_scales):
-    n = int(os.environ.get("AANET_SIDE_STREAMS", "0") or 0)
-    return max(1, min(n, num_scales - 1)) if n > 0 else num_scales - 1
-
-
-def split_heads():
-    """AANET_SPLIT_HEADS=1: the scale-0 heads launch split per output branch, each half on its
-    branch's side stream (A/B switch; the merged launch reads x0 once)."""
-    return os.environ.get("AANET_SPLIT_HEADS", "0") == "1"
-
-
-def early_conv1():
-    """AANET_EARLY_CONV1=1: a deformable module's conv1 (when no tail post stage computes it) runs
-    on its own side stream straight after the previous module's scale-0 tail, concurrently with
-    the heads launch, instead of after it on the main stream (A/B switch)."""
-    return os.environ.get("AANET_EARLY_CONV1", "0") == "1"
 
 
 def _record(stream):
@@ -227,22 +209,6 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
                               co_a, "leaky", "leaky", identity=x1.contiguous(),
                               up=t12.contiguous())
 
-    def _head1_sum(self, x0, x1, t12):
-        """Output branch 1 alone from the scale-0 block output (the branch-1 half of
-        _heads_sum1: one 64 -> 32 stride-2 conv with x1 and the resized up term in its epilogue)."""
-        l10 = self.fuse_layers[1][0]
-        pk = s2_pack(l10[0][0], [(l10[0][0], l10[0][1])])
-        co = l10[0][0].out_channels
-        return ops.conv3x3_s2(x0.contiguous(), pk[0], pk[1], co, co, "leaky", None,
-                              identity=x1.contiguous(), up=t12.contiguous())[0]
-
-    def _head2(self, x0):
-        """The first conv of the branch-2 chain alone (the other half of _heads_sum1)."""
-        l20 = self.fuse_layers[2][0]
-        pk = s2_pack(l20[0][0], [(l20[0][0], l20[0][1])])
-        co = l20[0][0].out_channels
-        return ops.conv3x3_s2(x0.contiguous(), pk[0], pk[1], co, co, "leaky", None)[0]
-
     def _branch2_sum(self, hb, x1, x2):
         """Output branch 2 as one stride-2 conv over [hb, x1] + x2 (see _s2_sums_ok)."""
         l20, l21 = self.fuse_layers[2][0], self.fuse_layers[2][1]
@@ -257,7 +223,7 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
             return self._down(heads[i], i, 0, start=1)
         return self._down(x[0], i, 0)
 
-    def _forward_eval(self, x, streams=None, keep=None, conv1_pre=None, post=None, marks=None):
+    def _forward_eval(self, x, streams=None, keep=None, conv1_pre=None, post=None):
         """Eval ISA + CSA.  The coarser scales run first, so that their exchange terms for output
         branch 0 exist when the scale-0 bottleneck runs: its tail kernel then writes both the
         block output and the cross-scale sum of branch 0 (aanet_csa_epilogue_t), which removes
@@ -333,15 +299,10 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
         if post is not None and post.get("result") is not None:
             keep.extend(v for v in post["result"].values() if v is not None)
         keep.append(x[0])
-        if marks is not None:
-            marks["tail"] = _record(main)  # block output and branch 0's sum are enqueued
         if "coarse" not in mark:  # the tail kernel did not take the block
             join()
         sums = self._s2_sums_ok(x)
-        split = sums and split_heads() and len(set(id(st) for st in streams[1:3])) == 2
-        if split:  # each branch's head on its own stream, straight after the tail (below)
-            heads = {}
-        elif sums:  # heads + branch 1's sum (x[1] and the up term exist: the join above)
+        if sums:  # heads + branch 1's sum (x[1] and the up term exist: the join above)
             out1, hb = self._heads_sum1(x[0], x[1], terms[(1, 2)])
             keep.extend((out1, hb))
             heads = {}
@@ -361,16 +322,6 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
             st = streams[i]
             with torch.cuda.stream(st):
                 st.wait_event(mark["coarse"])
-                if split:  # branch i's own head (and, i = 2, its merged sum) on its stream
-                    st.wait_event(b0_ev)
-                    if i == 1:
-                        out[i] = self._head1_sum(x[0], x[1], terms[(1, 2)])
-                    else:
-                        hb = self._head2(x[0])
-                        keep.append(hb)
-                        out[i] = self._branch2_sum(hb, x[1], x[2])
-                    keep.append(out[i])
-                    continue
                 if sums:
                     st.wait_event(b0_ev)
                     out[i] = out1 if i == 1 else self._branch2_sum(hb, x[1], x[2])
@@ -422,14 +373,14 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
             x_fused.append(ops.csa_sum([t.contiguous() for t in terms], act="leaky"))
         return x_fused
 
-    def forward(self, x, streams=None, keep=None, conv1_pre=None, post=None, marks=None):
+    @fp32_convs
+    def forward(self, x, streams=None, keep=None, conv1_pre=None, post=None):
         """aggregation.py:375-402.  streams / keep: the concurrent-scale schedule of
         AdaptiveAggregation (eval only, see _forward_eval); conv1_pre / post: the cross-module
-        pointwise fusions of AdaptiveAggregation (eval only); marks: receives the event recorded
-        on the current stream right after the scale-0 tail ("tail")."""
+        pointwise fusions of AdaptiveAggregation (eval only)."""
         assert len(self.branches) == len(x)
         if self.num_scales > 1 and use_fused(self, x[0]) and getattr(self, "aanet_fuse_csa", True):
-            return self._forward_eval(x, streams, keep, conv1_pre, post, marks)
+            return self._forward_eval(x, streams, keep, conv1_pre, post)
         if post is not None:
             post["result"] = None
         if streams is not None:  # reference op sequence: one stream
@@ -532,27 +483,7 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
         # the last module's block output and CSA sum feed nothing but final_conv: not stored
         return {"packed": pf, "bias": bf, "act": None, "disp": True, "skip_outputs": True}
 
-    def _early_conv1(self, i, x0, main, xs, tail_ev, keep):
-        """The next (deformable, one-block) fusion's scale-0 conv1 + BN1 + ReLU (NHWC) on the
-        side stream xs as soon as fusion i's tail has written x0, concurrently with fusion i's
-        heads launch on the main stream; the main stream waits for it before the next fusion's
-        offset conv.  None when the next fusion does not take it."""
-        if i + 1 >= self.num_fusions:
-            return None
-        nxt = self.fusions[i + 1]
-        if nxt.num_blocks != 1 or len(nxt.branches) == 0 or \
-                not isinstance(nxt.branches[0][0], DeformSimpleBottleneck):
-            return None
-        blk = nxt.branches[0][0]
-        if tuple(blk.conv1.weight.shape) != (64, 64, 1, 1):
-            return None
-        xs.wait_event(tail_ev)
-        with torch.cuda.stream(xs):
-            out = conv_bn_act(x0, blk.conv1, blk.bn1, "relu", out_nhwc=True)
-        main.wait_event(_record(xs))
-        keep.extend((x0, out))
-        return out
-
+    @fp32_convs
     def forward(self, cost_volume):
         """aggregation.py:452-464 (final 1x1 conv with bias on the HIP conv engine in eval)."""
         return self._run(cost_volume)[0]
@@ -565,16 +496,12 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
         cost-volume list is then None."""
         assert isinstance(cost_volume, list)
         fused = use_fused(self, cost_volume[0])
-        streams, xs = None, None
+        streams = None
         if fused and cost_volume[0].is_cuda and self.num_scales > 1 and concurrent_scales():
             dev = cost_volume[0].device
             main = torch.cuda.current_stream(dev)
-            nss = num_side_streams(self.num_scales)
-            ss = side_streams(dev, nss + (1 if early_conv1() else 0))
-            xs = ss[nss] if early_conv1() else None  # the early-conv1 stream
-            ss = ss[:nss]
-            # scale i >= 1 on side stream (i - 1) mod n
-            streams = [main] + [ss[(i - 1) % len(ss)] for i in range(1, self.num_scales)]
+            ss = side_streams(dev, self.num_scales - 1)
+            streams = [main] + ss  # scale i >= 1 on side stream i - 1
             for st in ss:
                 st.wait_stream(main)  # the cost volumes are written on the current stream
             keep = list(cost_volume)
@@ -583,10 +510,8 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
         for i in range(self.num_fusions):
             fusion = self.fusions[i]
             post = self._post_for(i, regress) if post_ok else None
-            marks = {}
             if streams is not None:
-                cost_volume = fusion(cost_volume, streams, keep, conv1_pre=pre, post=post,
-                                     marks=marks)
+                cost_volume = fusion(cost_volume, streams, keep, conv1_pre=pre, post=post)
             elif post_ok:
                 cost_volume = fusion(cost_volume, conv1_pre=pre, post=post)
             else:
@@ -595,13 +520,9 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
             pre = res["out"] if res is not None else None
             if res is not None and res.get("disp") is not None:
                 disp = res["disp"]
-            if pre is None and streams is not None and xs is not None and "tail" in marks:
-                pre = self._early_conv1(i, cost_volume[0], main, xs, marks["tail"], keep)
         if streams is not None:
             for st in ss:
                 main.wait_stream(st)
-            if xs is not None:
-                main.wait_stream(xs)
             del keep
         if disp is not None:
             return None, disp

@@ -9,6 +9,7 @@ come from the HIP concat / difference kernels (aanet_amd.nets.cost).
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+from .._precision import fp32_convs
 
 
 def conv3d(in_channels, out_channels, kernel_size=3, stride=1, dilation=1, groups=1):
@@ -57,6 +58,7 @@ class StereoNetAggregation(nn.Module):
                                                  for _ in range(4)])
         self.final_conv = nn.Conv3d(in_channels, 1, kernel_size=3, stride=1, padding=1, bias=True)
 
+    @fp32_convs
     def forward(self, cost_volume):
         assert cost_volume.dim() == 5  # [B, C, D, H, W]
         return self.final_conv(self.aggregation_layer(cost_volume)).squeeze(1)
@@ -77,6 +79,7 @@ class PSMNetBasicAggregation(nn.Module):
             setattr(self, name, nn.Sequential(conv1, relu(), conv1))
         self.classify = nn.Sequential(conv1, relu(), final_conv)
 
+    @fp32_convs
     def forward(self, cost):
         cost0 = self.dres0(cost)
         for name in ("dres1", "dres2", "dres3", "dres4"):
@@ -104,6 +107,7 @@ class PSMNetHourglass(nn.Module):
                                                       output_padding=1, stride=2, bias=False),
                                    nn.BatchNorm3d(inplanes))
 
+    @fp32_convs
     def forward(self, x, presqu, postsqu):
         pre = self.conv2(self.conv1(x))
         pre = F.relu(pre if postsqu is None else pre + postsqu, inplace=True)
@@ -130,6 +134,7 @@ class PSMNetHGAggregation(nn.Module):
                 convbn_3d(32, 32, 3, 1, 1), nn.ReLU(inplace=True),
                 nn.Conv3d(32, 1, kernel_size=3, padding=1, stride=1, bias=False)))
 
+    @fp32_convs
     def forward(self, cost):
         cost0 = self.dres0(cost)
         cost0 = self.dres1(cost0) + cost0
@@ -162,6 +167,7 @@ class GCNetAggregation(nn.Module):
         self.trans_conv5 = nn.ConvTranspose3d(32, 1, kernel_size=3, stride=2, padding=1, groups=1,
                                               dilation=1, bias=False)
 
+    @fp32_convs
     def forward(self, cost_volume):
         skip1 = self.conv1(cost_volume)
         a, skips = cost_volume, []

@@ -18,6 +18,7 @@ import torch.nn.functional as F
 from .. import ops
 from ._fuse import FoldCacheMixin, bn_affine, conv_bn_act, folded, offset_conv_eval, use_fused
 from .deform_conv import DeformConv, ModulatedDeformConv
+from .._precision import fp32_convs
 
 
 def conv3x3(in_planes, out_planes, stride=1, groups=1, dilation=1):
@@ -74,6 +75,7 @@ class DeformConv2d(FoldCacheMixin, nn.Module):
                                    oc.bias[i * cout:(i + 1) * cout], oc.stride, oc.padding,
                                    oc.dilation) for i in range(g)], 1)
 
+    @fp32_convs
     def forward(self, x):
         if self.modulation and use_fused(self, x):
             return self.forward_fused(x)
@@ -218,6 +220,7 @@ class DeformBottleneck(_BottleneckBase):
         self.downsample = downsample
         self.stride = stride
 
+    @fp32_convs
     def forward(self, x):
         if use_fused(self, x):
             return self._forward_fused(x, deform=True)
@@ -243,6 +246,7 @@ class SimpleBottleneck(_BottleneckBase):
         self.downsample = downsample
         self.stride = stride
 
+    @fp32_convs
     def forward(self, x):
         if use_fused(self, x):
             return self._forward_fused(x, deform=False)
@@ -271,6 +275,7 @@ class DeformSimpleBottleneck(_BottleneckBase):
         self.downsample = downsample
         self.stride = stride
 
+    @fp32_convs
     def forward(self, x):
         if use_fused(self, x):
             return self._forward_fused(x, deform=True)

@@ -13,6 +13,7 @@ import torch.nn.functional as F
 
 from ._fuse import FusedSequential, conv_bn_act, engine_conv, use_fused
 from .deform import DeformConv2d
+from .._precision import fp32_convs
 
 
 def _leaky():
@@ -72,6 +73,7 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
         self.stride = stride
 
+    @fp32_convs
     def forward(self, x):
         if use_fused(self, x) and isinstance(self.bn1, nn.BatchNorm2d):
             act = "leaky" if isinstance(self.relu, nn.LeakyReLU) else "relu"
@@ -95,6 +97,7 @@ class StereoNetFeature(nn.Module):
         self.residual_blocks = nn.Sequential(*[BasicBlock(32, 32) for _ in range(6)])
         self.final_conv = conv3x3(32, 32)  # no BN / ReLU on the last conv
 
+    @fp32_convs
     def forward(self, img):
         out = self.residual_blocks(self.downsample(img))
         if use_fused(self, out):
@@ -114,6 +117,7 @@ class PSMNetBasicBlock(nn.Module):
         self.downsample = downsample
         self.stride = stride
 
+    @fp32_convs
     def forward(self, x):
         if use_fused(self, x):
             out = self.conv1(x)
@@ -140,6 +144,7 @@ class FeaturePyrmaid(nn.Module):
         self.out1 = level(in_channel, in_channel * 2)
         self.out2 = level(in_channel * 2, in_channel * 4)
 
+    @fp32_convs
     def forward(self, x):
         out1 = self.out1(x)
         return [x, out1, self.out2(out1)]
@@ -163,6 +168,7 @@ class FeaturePyramidNetwork(nn.Module):
                 nn.init.xavier_uniform_(m.weight, gain=1)
                 nn.init.constant_(m.bias, 0)
 
+    @fp32_convs
     def forward(self, inputs):
         assert len(self.in_channels) == len(inputs)
         n = len(inputs)
@@ -216,6 +222,7 @@ class PSMNetFeature(nn.Module):
                                         nn.Conv2d(128, 32, kernel_size=1, padding=0, stride=1,
                                                   bias=False))
 
+    @fp32_convs
     def forward(self, x):
         out = self.layer1(self.firstconv(x))
         raw = self.layer2(out)
@@ -242,6 +249,7 @@ class BasicConv(nn.Module):
             self.bn = nn.BatchNorm2d(out_channels)
         self.conv = conv_t(in_channels, out_channels, bias=False, **kwargs)
 
+    @fp32_convs
     def forward(self, x):
         if use_fused(self, x) and engine_conv(self.conv):
             return conv_bn_act(x, self.conv, self.bn if self.use_bn else None,
@@ -272,6 +280,7 @@ class Conv2x(nn.Module):
             self.conv2 = BasicConv(cin, out_channels, False, is_3d, bn, relu, kernel_size=3,
                                    stride=1, padding=1)
 
+    @fp32_convs
     def forward(self, x, rem):
         x = self.conv1(x)
         assert x.size() == rem.size()
@@ -307,6 +316,7 @@ class GANetFeature(nn.Module):
         self.conv3b = Conv2x(64, 96, mdconv=feature_mdconv)
         self.conv4b = Conv2x(96, 128, mdconv=feature_mdconv)
 
+    @fp32_convs
     def forward(self, x):
         return _hourglass2(self, self.conv_start(x))
 
@@ -340,6 +350,7 @@ class GCNetFeature(nn.Module):
         self.conv2 = _psm_layer(self, PSMNetBasicBlock, 32, 8, 1, 1, 1)
         self.conv3 = conv3x3(32, 32)
 
+    @fp32_convs
     def forward(self, x):
         x = self.conv2(self.conv1(x))
         if use_fused(self, x):

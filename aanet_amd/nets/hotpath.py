@@ -14,6 +14,7 @@ from .aggregation import AdaptiveAggregation
 from .cost import CostVolume, CostVolumePyramid
 from ._fuse import FoldCacheMixin
 from .estimation import DisparityEstimation
+from .._precision import fp32_convs
 
 
 class AANetHotPath(FoldCacheMixin, nn.Module):
@@ -56,6 +57,7 @@ class AANetHotPath(FoldCacheMixin, nn.Module):
             return disparity_pyramid
         return [self.disparity_estimation(aggregation)]
 
+    @fp32_convs
     def forward(self, left_feature, right_feature):
         cost_volume = self.cost_volume_construction(left_feature, right_feature)
         aggregation, disp = self.aggregation._run(cost_volume, regress=self.regress_in_tail())

@@ -14,6 +14,7 @@ from ._fuse import FusedSequential, conv_bn_act, use_fused
 from .deform import DeformConv2d
 from .feature import BasicBlock, BasicConv, Conv2x, _hourglass2
 from .warp import disp_warp
+from .._precision import fp32_convs
 
 
 def conv2d(in_channels, out_channels, kernel_size=3, stride=1, dilation=1, groups=1):
@@ -77,6 +78,7 @@ class StereoNetRefinement(nn.Module):
         self.dilated_blocks = _dilated_stack()
         self.final_conv = nn.Conv2d(32, 1, 3, 1, 1)
 
+    @fp32_convs
     def forward(self, low_disp, left_img, right_img=None):
         disp = _upsampled_disp(low_disp, left_img, always_resize=True)
         out = self.dilated_blocks(self.conv(torch.cat((disp, left_img), dim=1)))
@@ -105,6 +107,7 @@ class StereoDRNetRefinement(_WarpErrorStem):
         self.dilated_blocks = _dilated_stack()
         self.final_conv = nn.Conv2d(32, 1, 3, 1, 1)
 
+    @fp32_convs
     def forward(self, low_disp, left_img, right_img):
         disp, x = self._stem(low_disp, left_img, right_img)
         return _residual_out(self, self.dilated_blocks(x), disp)
@@ -132,6 +135,7 @@ class HourglassRefinement(_WarpErrorStem):
         self.conv4b = Conv2x(96, 128, mdconv=True)
         self.final_conv = nn.Conv2d(32, 1, 3, 1, 1)
 
+    @fp32_convs
     def forward(self, low_disp, left_img, right_img):
         disp, x = self._stem(low_disp, left_img, right_img)
         return _residual_out(self, _hourglass2(self, self.conv_start(x)), disp)

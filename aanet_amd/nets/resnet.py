@@ -9,6 +9,7 @@ import torch.nn as nn
 
 from ._fuse import FusedSequential, conv_bn_act, use_fused
 from .deform import DeformBottleneck, _BottleneckBase
+from .._precision import fp32_convs
 
 
 def conv3x3(in_planes, out_planes, stride=1, groups=1, dilation=1):
@@ -43,6 +44,7 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
         self.stride = stride
 
+    @fp32_convs
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
         if use_fused(self, x) and isinstance(self.bn1, nn.BatchNorm2d):
@@ -74,6 +76,7 @@ class Bottleneck(_BottleneckBase):
         self.downsample = downsample
         self.stride = stride
 
+    @fp32_convs
     def forward(self, x):
         if use_fused(self, x):
             return self._forward_fused(x, deform=False)
@@ -134,6 +137,7 @@ class AANetFeature(nn.Module):
                          dilation=self.dilation, norm_layer=norm_layer) for _ in range(1, blocks)]
         return nn.Sequential(*layers)
 
+    @fp32_convs
     def forward(self, x):
         x = self.conv1(x)
         layer1 = self.layer1(x)

@@ -382,7 +382,7 @@ def timed_run(step, args, world):
     The graph replay is not always the faster schedule: ROCm's graph executor maps the captured
     multi-stream DAG onto its own queues, and on the eval aggregation it lost most of the
     concurrent-scale overlap (3.91-3.93 ms vs 3.76 ms eager on the same box,
-    tools/ab_schedules.sh).  So after capture untimed replays and eager steps are probed (5 alternating
+    the round-2 schedule A/B, in git history as tools/ab_schedules.sh).  So after capture untimed replays and eager steps are probed (5 alternating
     rounds of 5, best of each)
     and the faster one is timed (--graph / --no-graph force one); args.schedule records it."""
     for _ in range(args.warmup):

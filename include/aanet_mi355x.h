@@ -21,10 +21,17 @@ extern "C" {
 
 typedef struct ihipStream_t *aanet_stream_t; /* identical to hipStream_t */
 
+/* ABI version (aanet_version()).  4: every descriptor struct starts with `struct_size`
+ * (round 4; version 1 had none, and aanet_csa_epilogue_t grew a `post` member in round 3 without
+ * a way for the library to tell the two layouts apart). */
+#define AANET_ABI_VERSION 4
+
 enum {
   AANET_OK = 0,
   AANET_EINVAL = -1,      /* bad size / null pointer / inconsistent shape */
-  AANET_EUNSUPPORTED = -2 /* valid for the reference but outside what this build implements */
+  AANET_EUNSUPPORTED = -2, /* valid for the reference but outside what this build implements */
+  AANET_EABI = -3         /* a descriptor's struct_size is not this library's sizeof: the caller
+                             was built against another version of this header */
 };
 
 /* Activation layouts of the conv engine (the `layout` argument of the fused entry points).
@@ -54,7 +61,7 @@ enum {
   AANET_CONV_GENERIC_DCN = 32
 };
 
-int aanet_version(void);
+int aanet_version(void); /* AANET_ABI_VERSION of the library */
 const char *aanet_status_string(int status);
 
 /* ------------------------------------------------------------------ cost volumes ------- */
@@ -176,6 +183,7 @@ int aanet_conv2d_fused_f32(const float *x, const float *weight, const float *bia
  * may be NULL.  Tail kernels that cannot run it return AANET_EUNSUPPORTED (the caller then runs
  * the stage as separate kernels). */
 typedef struct {
+  size_t struct_size; /* sizeof(aanet_post_stage_t); AANET_EABI otherwise */
   const void *weight;
   const float *bias;
   int act;
@@ -186,6 +194,7 @@ typedef struct {
 } aanet_post_stage_t;
 
 typedef struct {
+  size_t struct_size; /* sizeof(aanet_csa_epilogue_t); AANET_EABI otherwise */
   float *out;
   int num_up;
   const float *up[3];
@@ -282,6 +291,7 @@ int aanet_conv3x3_grouped_nhwc_f32(const float *x, const void *wsplit, const flo
  * conv of the scale-0 chain and the 32->16 conv from scale 1).  identity: [n][co_a][ho][wo];
  * up: [n][co_a][up_h][up_w].  terms may be NULL (= aanet_conv3x3s2_f32). */
 typedef struct aanet_s2_terms {
+  size_t struct_size; /* sizeof(aanet_s2_terms_t); AANET_EABI otherwise */
   const float *x2;
   int c2;
   const float *identity;

@@ -31,7 +31,8 @@ def test_library_exports_every_header_symbol():
 
 def test_library_version_and_status_strings():
     L = _lib.lib()
-    assert L.aanet_version() == 1
+    assert L.aanet_version() == _lib.ABI_VERSION == 4
+    assert b"struct_size" in L.aanet_status_string(_lib.EABI)
     assert L.aanet_status_string(0) == b"ok"
     assert L.aanet_status_string(-1) == b"invalid argument"
     assert L.aanet_status_string(-2) == b"unsupported configuration"
@@ -47,6 +48,47 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
     assert L.aanet_mdcn_fwd_f32(*args) == -1
     with pytest.raises(_lib.AanetError):
         _lib.call("aanet_corr_volume_f32", None, None, None, 0, 1, 1, 1, 1, None)
+
+
+def test_descriptor_size_is_checked_without_a_gpu():
+    """Descriptor structs carry struct_size (ABI version 4): a caller built against another
+    header layout gets AANET_EABI before anything is read past the struct or launched (ADVICE r3:
+    a version-1 caller passed the smaller aanet_csa_epilogue_t and the library read `post` past
+    its end)."""
+    import ctypes as C
+    L = _lib.lib()
+    d = _lib.CsaEpilogue()
+    assert d.struct_size == C.sizeof(_lib.CsaEpilogue)
+    assert _lib.PostStage().struct_size == C.sizeof(_lib.PostStage)
+    assert _lib.S2Terms(None, 0).struct_size == C.sizeof(_lib.S2Terms)
+    dummy = C.c_void_p(16)  # never dereferenced: the descriptor check comes first
+    args = lambda desc: ([None] * 5 + [0, dummy, None, None, 0, 64, None, 1, 64, 8, 8, 64, 3, 3, 1, 1, 1]  # noqa: E731
+                         + [C.byref(desc), 1, None])
+    d.struct_size -= 8  # the version-1 layout had no `post` pointer
+    assert L.aanet_conv2d_pw_f32(*args(d)) == _lib.EABI
+    d.struct_size += 8
+    p = _lib.PostStage()
+    p.struct_size = 8
+    d.post = C.pointer(p)
+    assert L.aanet_conv2d_pw_f32(*args(d)) == _lib.EABI
+    t = _lib.S2Terms(None, 0)
+    t.struct_size = 0
+    assert L.aanet_conv3x3s2_terms_f32(None, None, None, 1, 32, 8, 8, 16, 16, None, 0, None, 0,
+                                       C.byref(t), None) == _lib.EABI
+
+
+def test_import_leaves_global_torch_flags_alone():
+    """importing the package no longer turns TF32 off process-wide; the package's module
+    forwards switch it off for their own MIOpen convs and restore it."""
+    import subprocess
+    import sys
+    code = ("import torch; a = torch.backends.cudnn.allow_tf32; import aanet_amd; "
+            "from aanet_amd._precision import fp32_convs; "
+            "seen = []; f = fp32_convs(lambda: seen.append(torch.backends.cudnn.allow_tf32)); f(); "
+            "print(a, torch.backends.cudnn.allow_tf32, seen[0])")
+    out = subprocess.run([sys.executable, "-c", code], cwd=REPO, capture_output=True, text=True,
+                         timeout=120).stdout.split()
+    assert out == ["True", "True", "False"], out
 
 
 def test_ops_fail_loudly_on_cpu_tensors():

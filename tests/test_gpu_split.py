@@ -35,7 +35,7 @@ def _errs(got, ref64, scale64):
     (2, 64, 24, 52, 64, 3, 1, 1, 1, 1, False),    # same, NCHW staging
     (2, 64, 24, 52, 54, 3, 1, 2, 2, 2, True),     # offset_conv: grouped, dilated, Cog = 27
     (2, 64, 24, 52, 64, 1, 1, 0, 1, 1, False),    # conv1 / conv3
-    (2, 64, 24, 52, 32, 3, 2, 1, 1, 1, False),    # CSA strided 3x3 (HALO 3 under AANET_HALO_S2=1)
+    (2, 64, 24, 52, 32, 3, 2, 1, 1, 1, False),    # CSA strided 3x3
     (2, 64, 25, 36, 64, 3, 2, 1, 1, 1, False),    # stride 2, 64-ch tile, ragged rows / columns
     (1, 32, 16, 40, 32, 3, 2, 1, 1, 1, False),    # stride 2, one input chunk
     (1, 128, 12, 40, 96, 3, 1, 1, 1, 1, False),   # Co > 64: two output tiles
@@ -175,9 +175,9 @@ def test_halo_conv_nhwc_output_vs_torch():
     assert (got.cpu() - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item())
 
 
-def test_halo_stride2_nhwc_output_vs_torch():
-    """Stride-2 halo form (NCHW input, HALO 3) with a channels-last output, bias, BN affine and
-    LeakyReLU: the CSA down-sampling exchange conv of aggregation.py:364-372."""
+def test_stride2_nhwc_output_vs_torch():
+    """Stride-2 engine conv (NCHW input, im2col form) with a channels-last output, bias, BN affine
+    and LeakyReLU: the CSA down-sampling exchange conv of aggregation.py:364-372."""
     gen = torch.Generator().manual_seed(10)
     x = torch.randn(2, 64, 21, 44, generator=gen)
     w = torch.randn(64, 64, 3, 3, generator=gen) / 24
@@ -190,42 +190,6 @@ def test_halo_stride2_nhwc_output_vs_torch():
                            post_shift=sh.to(DEV), packed_weight=ops.pack_weight_split(wd), out_nhwc=True)
     assert got.shape == ref.shape and got.is_contiguous(memory_format=torch.channels_last)
     assert (got.cpu() - ref).abs().max().item() <= 2e-5 * (1 + ref.abs().max().item())
-
-
-_S2_SCRIPT = """
-import torch, torch.nn.functional as F
-from aanet_amd import ops
-g = torch.Generator().manual_seed(12)
-for (N, C, H, W, Co, onhwc) in [(2, 64, 24, 52, 32, False), (2, 64, 25, 36, 64, True),
-                                (1, 32, 16, 40, 32, False), (1, 64, 128, 416, 64, True)]:
-    x = torch.randn(N, C, H, W, generator=g)
-    w = torch.randn(Co, C, 3, 3, generator=g) / (3 * C ** 0.5)
-    b = torch.randn(Co, generator=g)
-    ref = F.leaky_relu(F.conv2d(x.double(), w.double(), b.double(), 2, 1), 0.2)
-    wd = w.cuda()
-    got = ops.conv2d_fused(x.cuda(), wd, b.cuda(), 2, 1, 1, 1, "leaky",
-                           packed_weight=ops.pack_weight_split(wd), out_nhwc=onhwc)
-    again = ops.conv2d_fused(x.cuda(), wd, b.cuda(), 2, 1, 1, 1, "leaky",
-                             packed_weight=ops.pack_weight_split(wd), out_nhwc=onhwc)
-    assert torch.equal(got, again)
-    err = (got.cpu().double() - ref).abs().max().item()
-    assert err <= 2e-5 * (1 + ref.abs().max().item()), (N, C, H, W, Co, err)
-print("s2 halo ok")
-"""
-
-
-def test_halo_stride2_form_opt_in():
-    """The opt-in stride-2 halo form (AANET_HALO_S2=1, read once per process: run in a child
-    process) against torch fp64 over ragged tiles, one and two input chunks, 32/64-channel tiles,
-    NCHW and channels-last outputs and the C2 scale-0 shape, and run to run."""
-    import os
-    import subprocess
-    import sys
-    env = dict(os.environ, AANET_HALO_S2="1")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", _S2_SCRIPT], env=env, cwd=root, capture_output=True,
-                       text=True, timeout=110)
-    assert r.returncode == 0 and "s2 halo ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
 def test_fused_paths_bit_reproducible():
