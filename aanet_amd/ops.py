@@ -566,16 +566,20 @@ def resize_bilinear(x, size):
     return ResizeBilinearFunction.apply(x, size)
 
 
+DCN_BWD_ALGOS = {"auto": 0, "global": 1, "window": 2}  # AANET_DCN_BWD_* (include/aanet_mi355x.h)
+
+
 def mdcn_backward(x, offset, mask, weight, grad_out, with_bias, stride, padding, dilation, groups,
-                  deformable_groups, deterministic=None, nchw_scatter=False):
+                  deformable_groups, deterministic=None, nchw_scatter=False, algo="auto"):
     """deform_conv_cuda.cpp:571-685 -> (gX, gOffset, gMask, gW, gB or None).
 
-    Default: aanet_mdcn_bwd_ws_f32 (grad_x float atomics into an NHWC workspace, then
-    transposed); nchw_scatter=True: the workspace-free aanet_mdcn_bwd_f32.
+    Default: aanet_mdcn_bwd_algo_f32 with the caller-owned workspace; algo "auto" takes the
+    atomic-free window form of grad_x where it applies (stride 1, 8/16/32 channels per deformable
+    group), "window" / "global" force one form (AANET_EUNSUPPORTED if the window form does not
+    apply).  nchw_scatter=True: the workspace-free aanet_mdcn_bwd_f32 (global atomics in NCHW).
 
     deterministic (default: torch.are_deterministic_algorithms_enabled()): the bit-reproducible
-    form (aanet_mdcn_bwd_det_f32: fixed-point grad_x accumulation, ordered grad_W reduction)
-    instead of float atomics."""
+    form (fixed-point grad_x accumulation, ordered grad_W reduction) instead of float atomics."""
     require_gpu(x, offset, mask, weight, grad_out,
                 names=("input", "offset", "mask", "weight", "grad_output"))
     N, C, H, W = x.shape
@@ -585,30 +589,23 @@ def mdcn_backward(x, offset, mask, weight, grad_out, with_bias, stride, padding,
     gb = x.new_zeros((Co,)) if with_bias else None
     if deterministic is None:
         deterministic = torch.are_deterministic_algorithms_enabled()
-    if deterministic:
-        nbytes = _lib.lib().aanet_mdcn_bwd_det_workspace_size(N, C, H, W, Co, kh, kw, stride,
-                                                               padding, dilation, groups,
-                                                               deformable_groups)
-        if nbytes == 0:
-            raise ValueError("aanet_mdcn_bwd_det_workspace_size: invalid shape")
-        ws = torch.empty((nbytes,), device=x.device, dtype=torch.uint8)
-        call("aanet_mdcn_bwd_det_f32", ptr(x), ptr(offset), ptr(mask), ptr(weight), ptr(grad_out),
-             ptr(gx), ptr(goff), ptr(gm), ptr(gw), ptr(gb), N, C, H, W, Co, kh, kw, stride,
-             padding, dilation, groups, deformable_groups, ptr(ws), nbytes, stream_of(x))
-        return gx, goff, gm, gw, gb
-    if nchw_scatter:  # the workspace-free entry point (grad_x atomics in NCHW)
+    if algo not in DCN_BWD_ALGOS:
+        raise ValueError(f"mdcn_backward: algo must be one of {sorted(DCN_BWD_ALGOS)}")
+    if nchw_scatter and not deterministic:  # the workspace-free entry point (grad_x atomics in NCHW)
         call("aanet_mdcn_bwd_f32", ptr(x), ptr(offset), ptr(mask), ptr(weight), ptr(grad_out),
              ptr(gx), ptr(goff), ptr(gm), ptr(gw), ptr(gb), N, C, H, W, Co, kh, kw, stride, padding,
              dilation, groups, deformable_groups, stream_of(x))
         return gx, goff, gm, gw, gb
-    nbytes = _lib.lib().aanet_mdcn_bwd_ws_workspace_size(N, C, H, W, Co, kh, kw, stride, padding,
-                                                         dilation, groups, deformable_groups)
+    size_fn = "aanet_mdcn_bwd_det_workspace_size" if deterministic else "aanet_mdcn_bwd_ws_workspace_size"
+    nbytes = getattr(_lib.lib(), size_fn)(N, C, H, W, Co, kh, kw, stride, padding, dilation, groups,
+                                          deformable_groups)
     if nbytes == 0:
-        raise ValueError("aanet_mdcn_bwd_ws_workspace_size: invalid shape")
+        raise ValueError(f"{size_fn}: invalid shape")
     ws = torch.empty((nbytes,), device=x.device, dtype=torch.uint8)
-    call("aanet_mdcn_bwd_ws_f32", ptr(x), ptr(offset), ptr(mask), ptr(weight), ptr(grad_out),
+    call("aanet_mdcn_bwd_algo_f32", ptr(x), ptr(offset), ptr(mask), ptr(weight), ptr(grad_out),
          ptr(gx), ptr(goff), ptr(gm), ptr(gw), ptr(gb), N, C, H, W, Co, kh, kw, stride, padding,
-         dilation, groups, deformable_groups, ptr(ws), nbytes, stream_of(x))
+         dilation, groups, deformable_groups, int(bool(deterministic)), DCN_BWD_ALGOS[algo],
+         ptr(ws), nbytes, stream_of(x))
     return gx, goff, gm, gw, gb
 
 

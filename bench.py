@@ -231,12 +231,13 @@ def kernel_rooflines(model, left, right, batch, iters):
     flops = 2.0 * B * H * W * (w2.shape[0] * w2.shape[1] * 9 + w3.shape[0] * w3.shape[1])
     res["conv3x3_pw_s0"] = dict(bound="mfma", ms=ms, algo=flops, unit="TFLOP/s",
                                 achieved=flops / ms / 1e9, peak=conv_peak())
-    # the offset_conv of the scale-0 deformable block (3x3, dilation 2, 2 groups, 64 -> 54, the
-    # conv engine's halo form on the channels-last conv1 output)
+    # the offset_conv of the scale-0 deformable block (3x3, dilation 2, 2 groups, 64 -> 54, on the
+    # channels-last conv1 output), on the path the step takes (nets/_fuse.offset_conv_eval)
+    from aanet_amd.nets._fuse import offset_conv_eval
     oc = blk.conv2.offset_conv
     with torch.no_grad():
         x1 = conv_bn_act(vol, blk.conv1, blk.bn1, "relu", out_nhwc=True)
-        ms = time_events(lambda: conv_bn_act(x1, oc), iters, stream)
+        ms = time_events(lambda: offset_conv_eval(x1, oc), iters, stream)
     flops = 2.0 * B * H * W * oc.out_channels * (oc.in_channels // oc.groups) * 9
     res["offset_conv_s0"] = dict(bound="mfma", ms=ms, algo=flops, unit="TFLOP/s",
                                  achieved=flops / ms / 1e9, peak=conv_peak())
@@ -646,11 +647,13 @@ def dcn_sweep_main(args, device, rank):
                                         deterministic=False)
         bwd_det = lambda: ops.mdcn_backward(x, off, mask, w, go, False, stride, pad, dil, 1, dg,  # noqa: E731
                                             deterministic=True)
+        bwd_glob = lambda: ops.mdcn_backward(x, off, mask, w, go, False, stride, pad, dil, 1, dg,  # noqa: E731
+                                             deterministic=False, algo="global")
         flops = 2.0 * B * Ho * Wo * C * C * k * k
-        ms_f, ms_b, ms_d = (time_events(f, iters, stream) for f in (fwd, bwd, bwd_det))
+        ms_f, ms_b, ms_d, ms_g = (time_events(f, iters, stream) for f in (fwd, bwd, bwd_det, bwd_glob))
         line = {"bench": "dcn_sweep (C4)", "shape": name, "input": [B, C, H, W], "stride": stride,
                 "deformable_groups": dg, "dilation": dil, "fwd_us": ms_f * 1e3, "bwd_us": ms_b * 1e3,
-                "bwd_det_us": ms_d * 1e3,
+                "bwd_det_us": ms_d * 1e3, "bwd_global_atomic_us": ms_g * 1e3,
                 "fwd_tflops": flops / ms_f / 1e9, "bwd_tflops": 2 * flops / ms_b / 1e9,
                 "fwd_frac_f32_mfma": flops / ms_f / 1e9 / FP32_MFMA_PEAK_TF,
                 "bwd_frac_f32_mfma": 2 * flops / ms_b / 1e9 / FP32_MFMA_PEAK_TF,

@@ -347,6 +347,25 @@ int aanet_mdcn_bwd_det_f32(const float *x, const float *offset, const float *mas
                            int stride, int pad, int dil, int groups, int dg, void *workspace,
                            size_t workspace_bytes, aanet_stream_t stream);
 
+/* The same backward with the grad_x algorithm chosen explicitly (the _ws / _det entry points use
+ * AANET_DCN_BWD_AUTO).  deterministic: 0 = float atomics (workspace of
+ * aanet_mdcn_bwd_ws_workspace_size bytes), 1 = fixed point (aanet_mdcn_bwd_det_workspace_size). */
+enum {
+  AANET_DCN_BWD_AUTO = 0,   /* the window form where it applies, else the global-atomic form */
+  AANET_DCN_BWD_GLOBAL = 1, /* one global atomic per (pixel, tap, corner, channel) contribution,
+                               the reference's col2im pattern (kernel.cu:635-693) */
+  AANET_DCN_BWD_WINDOW = 2  /* stride 1, 8/16/32 channels per deformable group: each 8x8 output
+                               tile sums its contributions in an LDS window without atomics and
+                               adds the window once (AANET_EUNSUPPORTED for other shapes) */
+};
+int aanet_mdcn_bwd_algo_f32(const float *x, const float *offset, const float *mask,
+                            const float *weight, const float *grad_out, float *grad_x,
+                            float *grad_offset, float *grad_mask, float *grad_weight,
+                            float *grad_bias, int n, int c, int h, int w, int co, int kh, int kw,
+                            int stride, int pad, int dil, int groups, int dg, int deterministic,
+                            int algo, void *workspace, size_t workspace_bytes,
+                            aanet_stream_t stream);
+
 /* Weight (and bias) gradient of an ordinary convolution -- the wgrad of every nn.Conv2d of the
  * ISA/CSA blocks in training (nets/deform.py:6-14, 70-72; nets/aggregation.py:354-370, 447),
  * which the reference leaves to cuDNN.  x [n, c, h, w]; grad_out [n, co, ho, wo] (NCHW);

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from aanet_amd import ops
+from aanet_amd import _lib, ops
 from oracle import oracle
 
 pytestmark = pytest.mark.gpu
@@ -289,20 +289,24 @@ def test_deterministic_mode_reaches_shim_and_torch_ops():
 
 
 @pytest.mark.parametrize("case", BWD_CASES)
-@pytest.mark.parametrize("window", ["2", "0"])
-def test_mdcn_backward_window_form_vs_oracle(case, window, monkeypatch):
-    """The LDS-window grad_x form (mdcn_bwd_data_win_kernel, stride 1, <= 32 channels per
-    deformable group) with float atomics (AANET_DCN_BWD_WINDOW=2; by default it runs only for the
-    deterministic form) and the global-atomic form it replaces (=0), against the oracle, with
-    offsets large enough that some corners fall outside the window."""
-    monkeypatch.setenv("AANET_DCN_BWD_WINDOW", window)
+@pytest.mark.parametrize("algo", ["window", "global"])
+def test_mdcn_backward_window_form_vs_oracle(case, algo):
+    """The window grad_x form (mdcn_bwd_data_win_kernel: stride 1, 8/16/32 channels per
+    deformable group, owner-computes LDS window sums) and the global-atomic form, each in float
+    and fixed-point mode, against the oracle, with offsets large enough that some corners fall
+    outside the window.  Shapes the window form does not take report AANET_EUNSUPPORTED."""
     N, C, H, W, Co, k, s, p, d, dg = case
     x, off, msk, w, b = make_case(9, N, C, H, W, Co, k, s, p, d, dg, off_scale=2.5)
     Ho, Wo = off.shape[2:]
     go = np.random.default_rng(10).standard_normal((N, Co, Ho, Wo)).astype(np.float32)
     for det in (False, True):
-        got = ops.mdcn_backward(g2t(x), g2t(off), g2t(msk), g2t(w), g2t(go), True, s, p, d, 1, dg,
-                                deterministic=det)
+        try:
+            got = ops.mdcn_backward(g2t(x), g2t(off), g2t(msk), g2t(w), g2t(go), True, s, p, d, 1,
+                                    dg, deterministic=det, algo=algo)
+        except _lib.AanetError as e:
+            assert algo == "window" and e.status == _lib.EUNSUPPORTED and \
+                (s != 1 or C // dg not in (8, 16, 32)), (case, e)
+            return
         ref = oracle.mdcn_backward(x, off, msk, w, go, True, s, p, d, 1, dg)
         for name, gt, r in zip(("grad_input", "grad_offset", "grad_mask", "grad_weight", "grad_bias"), got, ref):
             err = np.abs(t2n(gt) - r)
@@ -310,21 +314,44 @@ def test_mdcn_backward_window_form_vs_oracle(case, window, monkeypatch):
             assert err.max() <= 1e-4 * scale + 1e-6, f"{name} det={det}: max err {err.max():.3g}"
 
 
-@pytest.mark.parametrize("form", ["atomic", "window", "deterministic"])
-def test_mdcn_backward_c4_agg_s0_vs_oracle(form, monkeypatch):
+@pytest.mark.parametrize("form", ["atomic", "window", "deterministic", "deterministic_global"])
+def test_mdcn_backward_c4_agg_s0_vs_oracle(form):
     """SURVEY C4 at the aggregation's scale-0 shape: one image of 64 channels at 128x416,
-    dg 2, 3x3, dil 2 (the C2 bottleneck DCN), against the oracle, for the float-atomic
-    (NHWC workspace scatter), LDS-window float (AANET_DCN_BWD_WINDOW=2) and fixed-point
-    deterministic forms.  Grids ~100x those of BWD_CASES (deform_conv_cuda_kernel.cu:635-767)."""
+    dg 2, 3x3, dil 2 (the C2 bottleneck DCN), against the oracle, for the global float-atomic
+    (NHWC workspace scatter), window (the default) and fixed-point deterministic (window and
+    global) forms.  Grids ~100x those of BWD_CASES (deform_conv_cuda_kernel.cu:635-767)."""
     N, C, H, W, Co, k, s, p, d, dg = 1, 64, 128, 416, 64, 3, 1, 2, 2, 2
     x, off, msk, w, b = make_case(11, N, C, H, W, Co, k, s, p, d, dg, off_scale=0.7)
     go = np.random.default_rng(12).standard_normal((N, Co, H, W)).astype(np.float32)
-    if form == "window":
-        monkeypatch.setenv("AANET_DCN_BWD_WINDOW", "2")
+    algo = {"atomic": "global", "window": "window", "deterministic": "auto",
+            "deterministic_global": "global"}[form]
     got = ops.mdcn_backward(g2t(x), g2t(off), g2t(msk), g2t(w), g2t(go), True, s, p, d, 1, dg,
-                            deterministic=form == "deterministic")
+                            deterministic=form.startswith("deterministic"), algo=algo)
     ref = oracle.mdcn_backward(x, off, msk, w, go, True, s, p, d, 1, dg)
     for name, gt, r in zip(("grad_input", "grad_offset", "grad_mask", "grad_weight", "grad_bias"), got, ref):
         err = np.abs(t2n(gt) - r)
         scale = np.abs(r).max() + 1e-12
         assert err.max() <= 1e-4 * scale + 1e-6, f"{form} {name}: max err {err.max():.3g} (scale {scale:.3g})"
+
+
+def test_mdcn_backward_window_deterministic_bit_reproducible():
+    """The window form in fixed-point mode (the default deterministic path at the aggregation
+    shapes): its window sums run in a fixed order (table entries in ascending pixel order, no LDS
+    atomics), the global fallback and the flush add int64 fixed-point values, so two runs give
+    identical bits -- with offsets large enough that both the window and the fallback paths run,
+    and with clustered offsets that fill the per-position tables past their capacity."""
+    N, C, H, W, Co, k, s, p, d, dg = 2, 64, 40, 96, 64, 3, 1, 2, 2, 2
+    x, off, msk, w, b = make_case(21, N, C, H, W, Co, k, s, p, d, dg, off_scale=1.5)
+    go = np.random.default_rng(22).standard_normal((N, Co, H, W)).astype(np.float32)
+    # clustered offsets in one corner of the image: many pixels share a table position
+    off[:, :, :8, :8] = -np.arange(8, dtype=np.float32)[None, None, None, :] * 0.999
+    args = (g2t(x), g2t(off), g2t(msk), g2t(w), g2t(go), True, s, p, d, 1, dg)
+    a = ops.mdcn_backward(*args, deterministic=True, algo="window")
+    b2 = ops.mdcn_backward(*args, deterministic=True, algo="window")
+    for u, v in zip(a, b2):
+        assert torch.equal(u, v)
+    ref = oracle.mdcn_backward(x, off, msk, w, go, True, s, p, d, 1, dg)
+    for name, gt, r in zip(("grad_input", "grad_offset", "grad_mask", "grad_weight", "grad_bias"), a, ref):
+        err = np.abs(t2n(gt) - r)
+        scale = np.abs(r).max() + 1e-12
+        assert err.max() <= 1e-4 * scale + 1e-6, f"{name}: max err {err.max():.3g}"
