@@ -50,23 +50,6 @@ typedef __attribute__((address_space(3))) void lds_void;
 #ifndef DCN_UNROLL
 #define DCN_UNROLL 0
 #endif
-// A/B switches of round 4 (compile-time, tools/build_variant.sh):
-//   DCN_NT: single-use streams (offsets, mask, identity, outputs) with the non-temporal policy, so
-//     they do not evict the x lines that the neighbouring tiles' windows re-read from L2
-//   DCN_NOOK: corner weights without the per-corner image-bounds masks (in-window samples read
-//     zero-padded window positions, so an out-of-image corner contributes 0 either way)
-#ifndef DCN_NT
-#define DCN_NT 0
-#endif
-//   DCN_LB: waves per SIMD the register budget is sized for (4: 128 VGPRs, two workgroups per CU;
-//     2: 256 VGPRs, one workgroup per CU)
-#ifndef DCN_LB
-#define DCN_LB 4
-#endif
-#ifndef DCN_NOOK
-#define DCN_NOOK 0
-#endif
-constexpr int NTPOL = DCN_NT ? 2 : 0;  // buffer-load cache policy: nt
 
 constexpr int NT = 512;          // 8 waves, one tile row each
 constexpr int TR = 8, TC = 16;   // tile: 8 rows x 16 columns of output pixels
@@ -134,16 +117,6 @@ __device__ __forceinline__ TapState tap_state(float oh, float ow, float ml, int 
   const float lh = h - (float)hl, lw = w - (float)wl;
   const float hh = 1.f - lh, hw = 1.f - lw;
   TapState s;
-#if DCN_NOOK
-  // the kernel.cu:478-493 corner bounds need no masks here: an in-window sample reads its
-  // out-of-image corners as the window's zero padding (0 * w = w * 0), and the global fallback
-  // below re-checks them; an invalid sample (valid == 0) gets all-zero weights
-  const float mv = valid ? m : 0.f;
-  s.w0 = hh * hw * mv;
-  s.w1 = hh * lw * mv;
-  s.w2 = lh * hw * mv;
-  s.w3 = lh * lw * mv;
-#else
   const bool ok1 = valid && hl >= 0 && wl >= 0;
   const bool ok2 = valid && hl >= 0 && wl + 1 <= W - 1;
   const bool ok3 = valid && hl + 1 <= H - 1 && wl >= 0;
@@ -152,7 +125,6 @@ __device__ __forceinline__ TapState tap_state(float oh, float ow, float ml, int 
   s.w1 = (ok2 ? hh * lw : 0.f) * m;
   s.w2 = (ok3 ? lh * hw : 0.f) * m;
   s.w3 = (ok4 ? lh * lw : 0.f) * m;
-#endif
   const int rh = hl - wy0, rw = wl - wx0;
   const bool inwin = (unsigned)rh <= (unsigned)(WR - 2) && (unsigned)rw <= (unsigned)(WC - 2);
   // an invalid sample has four zero weights: any in-window position will do
@@ -164,7 +136,7 @@ __device__ __forceinline__ TapState tap_state(float oh, float ow, float ml, int 
 // A chunk is one tap of a 32-channel K slice ("phase"): with CG = 32 a phase is one group, with
 // CG = 16 it holds both groups (lane groups kr = 0, 1 carry group 0's channels, kr = 2, 3 group 1's).
 template <int DIL, int CG, bool POST>
-__global__ __launch_bounds__(NT, DCN_LB) void dcn_tile_kernel(DcnTileArgs a) {
+__global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   constexpr int CT = 2 * CG;             // channels = Co = Co2
   constexpr int NPH = CT / 32;           // phases
   constexpr int NCH = NPH * K;           // chunks
@@ -254,9 +226,9 @@ __global__ __launch_bounds__(NT, DCN_LB) void dcn_tile_kernel(DcnTileArgs a) {
     const int o_h = (int)__umul24((unsigned)(gr * 2 * K + 2 * t), P4) + p4;
     const int o_w = o_h + (int)P4;
     const int o_m = (int)__umul24((unsigned)(gr * K + t), P4) + p4;
-    poh = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, o_h, 0, NTPOL));
-    pow_ = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, o_w, 0, NTPOL));
-    pml = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mskr, o_m, 0, NTPOL));
+    poh = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, o_h, 0, 0));
+    pow_ = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, o_w, 0, 0));
+    pml = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(mskr, o_m, 0, 0));
   };
   TapState ps;  // this lane's state for (tap, group) pt(kr) of the current pass
   auto compute_pass = [&](int t0) {
@@ -437,11 +409,7 @@ __global__ __launch_bounds__(NT, DCN_LB) void dcn_tile_kernel(DcnTileArgs a) {
     eo[i] = ((long)(n * Co2 + co2) * H + yy) * W + xx;
     if (!eok[i]) continue;
     eb[i] = a.tail_b ? a.tail_b[co2] : 0.f;
-#if DCN_NT
-    if (res) er[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(a.residual + eo[i]));
-#else
     if (res) er[i] = *reinterpret_cast<const f32x4 *>(a.residual + eo[i]);
-#endif
   }
 
   // ---- tail: BN2 + act -> conv3 (pointwise, split-bf16) ----------------------------------------
@@ -566,13 +534,7 @@ __global__ __launch_bounds__(NT, DCN_LB) void dcn_tile_kernel(DcnTileArgs a) {
       if (res) t += er[i][u];
       v[u] = act_f(t, a.tail_act);
     }
-    if (!post || !a.post_skip) {
-#if DCN_NT
-      __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(a.out + eo[i]));
-#else
-      *reinterpret_cast<f32x4 *>(a.out + eo[i]) = v;
-#endif
-    }
+    if (!post || !a.post_skip) *reinterpret_cast<f32x4 *>(a.out + eo[i]) = v;
     if (csa) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -584,13 +546,7 @@ __global__ __launch_bounds__(NT, DCN_LB) void dcn_tile_kernel(DcnTileArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) v[u] = act_f(v[u], a.csa_act);
-      if (!post || !a.post_skip) {
-#if DCN_NT
-        __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(a.csa_out + eo[i]));
-#else
-        *reinterpret_cast<f32x4 *>(a.csa_out + eo[i]) = v;
-#endif
-      }
+      if (!post || !a.post_skip) *reinterpret_cast<f32x4 *>(a.csa_out + eo[i]) = v;
     }
     if (post)  // the branch output back into the item's own slot: the post stage's B operand
       *reinterpret_cast<f32x4 *>(sO + (e >> 5) * OP + (qi >> 2) * 16 + 4 * (qi & 3)) = v;

@@ -1013,7 +1013,10 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     // 2 + kr / 2 of the upper -- and the pieces go to LDS as ds_write_b128 under swz_tail.  The
     // round-3 form wrote each half with ds_write_b64 (16 rows at one quad per lane group: 4-way
     // bank conflicts, 144 conflict cycles per wave; MI355X_MICROARCH.md §LDS lane groups).
-    constexpr bool PAIRED = SPL && NCB == 2;
+#ifndef AANET_TAIL_PAIRED  // A/B build switch (tools/build_variant.sh): 0 = the round-3 b64 staging
+#define AANET_TAIL_PAIRED 1
+#endif
+    constexpr bool PAIRED = AANET_TAIL_PAIRED && SPL && NCB == 2;
     if constexpr (PAIRED) {
       float *sC = smem + (wc0 >> 1) * BUF;
       const bool odd = (kr & 1) != 0;
@@ -1712,28 +1715,21 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_nhwc_kernel(MdcnArgs a, cons
   }
 }
 
-// Window form of mdcn_bwd_data_nhwc_kernel (stride 1, 8/16/32 channels per deformable group): the
-// workgroup owns an 8 x 8 output tile and sums its grad_x corner contributions for one deformable
-// group in an LDS copy of the tile's input window (rows/cols [origin, origin + WR/WC), the corners
-// of every offset in [-R, R)), then adds the window to the global accumulator once: one global
-// atomic per window element instead of one per (pixel, tap, corner, channel) -- 9 x 4 x 64 /
-// (WR x WC) times fewer.
-// Round 4: the window is summed WITHOUT atomics.  LDS float atomics ran at ~180 cycles per wave
-// instruction per CU here (the round-3 form of this kernel spent 4.5 of its 7.3 ms in them).  Per
-// tap, each pixel whose 2x2 corner block lies in the window enters its top-left window position
-// in a small table (an LDS integer slot counter, CAP slots per position; a pixel that finds its
-// position full takes the global-atomic path like a pixel outside the window).  Then each window
-// element is updated by exactly one lane ("owner computes"): lane (position q, channel c) reads
-// the table entries of the four positions whose corner block covers q (q, q - 1, q - WC,
-// q - WC - 1) and adds weight x colg for each -- a plain read-modify-write.  The colg chunk is
-// kept transposed ([pixel][channel], pitch KC + 1) so those reads are conflict-free.
-// DET: the entries of a table position are taken in ascending pixel order, taps and corners in a
-// fixed order, so the float window sum is reproducible; the flush converts it to the fixed-point
-// int64 accumulator (and the global fallback adds fixed-point contributions), whose integer sum
-// does not depend on the order in which the atomics land.
-// dynamic LDS: sG [Co][GP], sWt [KC][WTP], sCgT [PT][KC + 1], sS [PT][16], window float
-// [WR*WC][cpg], counts int [2][WR*WC], table uchar [2][WR*WC][CAP]
-constexpr int WIN_CAP = 4;
+// Round 4 tried an atomic-free "owner computes" form of this kernel (per-tap tables of the pixels
+// whose corner block starts at each window position; each window element updated by one lane):
+// bit-reproducible, but slower -- agg_s0 backward 7.84 ms float / 8.20 ms fixed point, against
+// 4.57 ms for the global-atomic form and 6.0 ms for this LDS-atomic window form: the owner loop is
+// a chain of dependent LDS reads (count -> table -> per-entry state) per window position and tap,
+// at two workgroups (8 waves) per CU.  It is in the git history (round 4).
+// Window form of mdcn_bwd_data_nhwc_kernel (stride 1, <= 32 channels per deformable group): the
+// workgroup owns an 8 x 8 output tile and accumulates its grad_x corner contributions for one
+// deformable group in an LDS copy of the tile's input window (rows/cols [origin, origin + WR/WC),
+// the corners of every offset in [-R, R)) with LDS atomics, then adds the window to the global
+// NHWC accumulator once: one global atomic per window element instead of one per (pixel, tap,
+// corner, channel) -- 9 x 4 x 64 / (WR x WC) times fewer.  Corners outside the window take the
+// global atomic directly.  DET: the same integer fixed-point contributions as the atomic form,
+// summed in int64 (LDS and global), so the result stays independent of the order.
+// dynamic LDS: sG [Co][GP], sWt [KC][WTP], sCg [KC][CP], sS [PT][16], window [WR*WC][cpg]
 template <int DET>
 __global__ __launch_bounds__(NT) void mdcn_bwd_data_win_kernel(MdcnArgs a, const float *__restrict__ xh,
                                                                const float *__restrict__ wT,
@@ -1745,48 +1741,42 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_win_kernel(MdcnArgs a, const
                                                                const double *__restrict__ det_scale,
                                                                int WR, int WCc, int R) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  constexpr int CPT = KC + 1;
   const int Co = a.Co;
-  const int K = a.kh * a.kw, cpg = a.C / a.dg, C = a.C;
-  const int NPOS = WR * WCc;
   float *sG = sm;                       // [Co][GP]      gOut tile
   float *sWt = sG + Co * GP;            // [KC][WTP]     W^T chunk
-  float *sCgT = sWt + KC * WTP;         // [PT][CPT]     colg chunk, transposed
-  float *sS = sCgT + PT * CPT;          // [PT][16]      per-pixel corners, weights, mask, window pos
-  float *sAcc = sS + PT * 16;           // [NPOS][cpg]   window accumulator
-  int *sCnt = reinterpret_cast<int *>(sAcc + NPOS * cpg);                  // [2][NPOS]
-  unsigned char *sTab = reinterpret_cast<unsigned char *>(sCnt + 2 * NPOS);  // [2][NPOS][CAP]
+  float *sCg = sWt + KC * WTP;          // [KC][CP]      colg chunk
+  float *sS = sCg + KC * CP;            // [PT][16]      per-pixel corners, weights, mask, window pos
+  void *sAcc = sS + PT * 16;            // [WR*WC][cpg]  float or int64 window accumulator
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long P = (long)a.Ho * a.Wo;
   const int ttx = (a.Wo + 7) / 8, tpi = ttx * ((a.Ho + 7) / 8);
   const int n = blockIdx.x / tpi, tile = blockIdx.x % tpi, g = blockIdx.y;
   const int ty0 = (tile / ttx) * 8, tx0 = (tile % ttx) * 8;
+  const int K = a.kh * a.kw, cpg = a.C / a.dg, C = a.C;
   const long HW = (long)a.H * a.W;
   const double scale = DET ? *det_scale : 1.0;
   const float *xn = xh + (long)n * HW * C;
   const int wy0 = ty0 - a.pad - R, wx0 = tx0 - a.pad - R;  // window origin (stride 1)
+  const int nwin = WR * WCc * cpg;
   auto pix = [&](int pl) -> long {  // linear output pixel of tile pixel pl, or -1
     const int y = ty0 + (pl >> 3), x = tx0 + (pl & 7);
     return (y < a.Ho && x < a.Wo) ? (long)y * a.Wo + x : -1;
   };
-  for (int e = tid; e < NPOS * cpg; e += NT) sAcc[e] = 0.f;
-  for (int e = tid; e < NPOS; e += NT) sCnt[e] = 0;  // table 0 (tap 0)
+  for (int e = tid; e < nwin; e += NT) {
+    if (DET)
+      reinterpret_cast<long long *>(sAcc)[e] = 0;
+    else
+      reinterpret_cast<float *>(sAcc)[e] = 0.f;
+  }
   for (int e = tid; e < Co * PT; e += NT) {
     const int co = e / PT, pl = e % PT;
     const long pp = pix(pl);
     sG[co * GP + pl] = pp >= 0 ? gout[((long)n * Co + co) * P + pp] : 0.f;
   }
-  __syncthreads();
   const int kr = lane >> 4, jj = lane & 15;
   const int q = tid & 7;  // channel quad of the gradient role; pixels (tid >> 3) + 32 it
-  // owner role: LP lanes (one per channel) per window position, 64 / LP positions per wave
-  const int LP = cpg <= 8 ? 8 : (cpg <= 16 ? 16 : 32);
-  const int ocl = lane % LP, oq0 = wave * (64 / LP) + lane / LP, ostep = (NT / 64) * (64 / LP);
   for (int k = 0; k < K; ++k) {
-    const int tb = k & 1;
-    if (k) __syncthreads();  // every wave is done with tap k-1 (sS, the table of tap k-1)
-    // the next tap's table: its last readers (tap k-1's owners) passed the barrier above
-    for (int e = tid; e < NPOS; e += NT) sCnt[(tb ^ 1) * NPOS + e] = 0;
+    if (k) __syncthreads();  // every wave is done scattering tap k-1 (it reads sS)
     if (wave == 0) {  // published for the chunk loop (its first barrier orders it)
 #pragma clang fp contract(off)
       const long p = pix(lane);
@@ -1802,26 +1792,18 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_win_kernel(MdcnArgs a, const
       qq[3] = __builtin_bit_cast(float, on && (s.ok & 8) ? s.i4 : -1);
       qq[4] = hh * hw, qq[5] = hh * s.lw, qq[6] = s.lh * hw, qq[7] = s.lh * s.lw;
       qq[8] = s.m, qq[9] = s.lh, qq[10] = s.lw, qq[11] = on ? 1.f : 0.f;
-      // window position of the 2x2 corner block (top-left) entered in the tap's table, or -1:
-      // global atomics (outside the window, or the position's CAP slots are taken)
+      // window position of the 2x2 corner block (top-left), or -1: global atomics
       int wpos = -1;
       if (on) {
         const int rh = s.hl - wy0, rw = s.wl - wx0;
-        if ((unsigned)rh <= (unsigned)(WR - 2) && (unsigned)rw <= (unsigned)(WCc - 2)) {
-          const int t = tb * NPOS + rh * WCc + rw;
-          const int slot = atomicAdd(sCnt + t, 1);
-          if (slot < WIN_CAP) {
-            sTab[t * WIN_CAP + slot] = (unsigned char)lane;
-            wpos = rh * WCc + rw;
-          }
-        }
+        if ((unsigned)rh <= (unsigned)(WR - 2) && (unsigned)rw <= (unsigned)(WCc - 2)) wpos = rh * WCc + rw;
       }
       qq[12] = __builtin_bit_cast(float, wpos);
     }
     float gm[2] = {0.f, 0.f}, goh[2] = {0.f, 0.f}, gow[2] = {0.f, 0.f};
     for (int c0 = g * cpg; c0 < (g + 1) * cpg; c0 += KC) {
       const int rows = min(KC, (g + 1) * cpg - c0);
-      __syncthreads();  // previous chunk's sCgT / sWt readers are done; sS and the table are written
+      __syncthreads();  // previous chunk's sCg / sWt readers are done
       for (int e = tid; e < KC * Co; e += NT) {
         const int co = e % Co, cl = e / Co;
         sWt[cl * WTP + co] = cl < rows ? wT[((long)k * C + c0 + cl) * Co + co] : 0.f;
@@ -1839,7 +1821,7 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_win_kernel(MdcnArgs a, const
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sCgT[(16 * wave + jj) * CPT + 16 * cb + 4 * kr + r] = cacc[cb][r];
+        for (int r = 0; r < 4; ++r) sCg[(16 * cb + 4 * kr + r) * CP + 16 * wave + jj] = cacc[cb][r];
       __syncthreads();
       // offset / mask partials: (pixel, channel quad)
       if (4 * q < rows) {
@@ -1862,7 +1844,7 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_win_kernel(MdcnArgs a, const
           const f32x4 v4 = i4 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i4 * C + cq) : z;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const float cg = sCgT[px * CPT + 4 * q + u];
+            const float cg = sCg[(4 * q + u) * CP + px];
             const float val = hh * hw * v1[u] + hh * lw * v2[u] + lh * hw * v3[u] + lh * lw * v4[u];
             gm[it] += cg * val;
             const float wh = -hw * v1[u] - lw * v2[u] + hw * v3[u] + lw * v4[u];
@@ -1873,11 +1855,12 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_win_kernel(MdcnArgs a, const
           }
         }
       }
-      // grad_x, pixels off the window path: global atomics; lanes 0-31 channel cl of pixel
-      // 16w + 2t, lanes 32-63 of pixel 16w + 2t + 1
-      {
-        const int cl = lane & 31;
+      // grad_x: lanes 0-31 channel cl of pixel 16w + 2t, lanes 32-63 of pixel 16w + 2t + 1; the
+      // window channel index is c0 + cl - g*cpg (< cpg <= 32: one chunk per group)
+      const int cl = lane & 31;
+      if (cl < rows && a.dbg_noatom != 1) {
         const long cbase = (long)n * HW * C + c0 + cl;
+        const int wc = c0 + cl - g * cpg;
         auto gadd = [&](int i, float v) {
           if (DET)
             atomicAdd(reinterpret_cast<unsigned long long *>(gxi + cbase + (long)i * C),
@@ -1885,59 +1868,36 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_win_kernel(MdcnArgs a, const
           else
             atomicAdd(gx + cbase + (long)i * C, v);
         };
+        auto wadd = [&](int wp, float v) {
+          if (DET)
+            atomicAdd(reinterpret_cast<unsigned long long *>(sAcc) + (long)wp * cpg + wc,
+                      (unsigned long long)__double2ll_rn((double)v * scale));
+          else
+            atomicAdd(reinterpret_cast<float *>(sAcc) + wp * cpg + wc, v);
+        };
+#pragma unroll 2
         for (int t = 0; t < 8; ++t) {
 #pragma clang fp contract(off)
           const int px = 16 * wave + 2 * t + (lane >> 5);
           const float *qq = sS + px * 16;
-          const float q12 = qq[12];
-          if (cl >= rows || __builtin_bit_cast(int, q12) >= 0) continue;
           const f32x4 qi = *reinterpret_cast<const f32x4 *>(qq);
           const f32x4 qw = *reinterpret_cast<const f32x4 *>(qq + 4);
-          const float top = sCgT[px * CPT + cl] * qq[8];
-          const float qi0 = qi[0], qi1 = qi[1], qi2 = qi[2], qi3 = qi[3];
+          const float top = sCg[cl * CP + px] * qq[8];
+          const float qi0 = qi[0], qi1 = qi[1], qi2 = qi[2], qi3 = qi[3], q12 = qq[12];
           const int i1 = __builtin_bit_cast(int, qi0), i2 = __builtin_bit_cast(int, qi1);
           const int i3 = __builtin_bit_cast(int, qi2), i4 = __builtin_bit_cast(int, qi3);
-          if (i1 >= 0) gadd(i1, qw[0] * top);
-          if (i2 >= 0) gadd(i2, qw[1] * top);
-          if (i3 >= 0) gadd(i3, qw[2] * top);
-          if (i4 >= 0) gadd(i4, qw[3] * top);
-        }
-      }
-      // grad_x, window path: owner computes (the window channel index is c0 + ocl - g*cpg; one
-      // chunk per group)
-      if (ocl < rows) {
-        const int wc = c0 + ocl - g * cpg;
-        const int *cnt = sCnt + tb * NPOS;
-        const unsigned *tab = reinterpret_cast<const unsigned *>(sTab) + tb * NPOS;  // CAP = 4 bytes
-        for (int qp = oq0; qp < NPOS; qp += ostep) {
-#pragma clang fp contract(off)
-          const int qy = qp / WCc, qx = qp - qy * WCc;
-          float acc = sAcc[qp * cpg + wc];
-#pragma unroll
-          for (int d = 0; d < 4; ++d) {  // corner d of the block whose top-left is src
-            const int dy = d >> 1, dx = d & 1;
-            if (qy < dy || qx < dx) continue;
-            const int src = qp - dy * WCc - dx;
-            const int nc = min(cnt[src], WIN_CAP);
-            if (nc == 0) continue;
-            unsigned ent = tab[src];
-            if (nc < 4) ent |= 0xffffffffu << (8 * nc);  // unused slots: pixel 255, sorted last
-            if (DET) {  // ascending pixel order: a fixed summation order
-              unsigned b[4] = {ent & 0xff, (ent >> 8) & 0xff, (ent >> 16) & 0xff, ent >> 24};
-#define WSWAP(i, j) { const unsigned lo = min(b[i], b[j]), hi = max(b[i], b[j]); b[i] = lo; b[j] = hi; }
-              WSWAP(0, 1) WSWAP(2, 3) WSWAP(0, 2) WSWAP(1, 3) WSWAP(1, 2)
-#undef WSWAP
-              ent = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
-            }
-            for (int e = 0; e < nc; ++e) {
-              const int px = (ent >> (8 * e)) & 0xff;
-              const float *qq = sS + px * 16;
-              const float qid = qq[d];
-              if (__builtin_bit_cast(int, qid) < 0) continue;  // corner outside the image
-              acc += qq[4 + d] * (sCgT[px * CPT + ocl] * qq[8]);
-            }
+          const int wp = __builtin_bit_cast(int, q12);
+          if (wp >= 0) {  // corners outside the image have index -1 (skipped), as below
+            if (i1 >= 0) wadd(wp, qw[0] * top);
+            if (i2 >= 0) wadd(wp + 1, qw[1] * top);
+            if (i3 >= 0) wadd(wp + WCc, qw[2] * top);
+            if (i4 >= 0) wadd(wp + WCc + 1, qw[3] * top);
+          } else {
+            if (i1 >= 0) gadd(i1, qw[0] * top);
+            if (i2 >= 0) gadd(i2, qw[1] * top);
+            if (i3 >= 0) gadd(i3, qw[2] * top);
+            if (i4 >= 0) gadd(i4, qw[3] * top);
           }
-          sAcc[qp * cpg + wc] = acc;
         }
       }
     }
@@ -1963,18 +1923,18 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_win_kernel(MdcnArgs a, const
   if (a.dbg_noatom) return;
   // add the window to the global accumulator: consecutive threads take consecutive channels of a
   // position (one 128-byte line per 32 lanes); untouched (zero) elements are skipped
-  for (int e = tid; e < NPOS * cpg; e += NT) {
+  for (int e = tid; e < nwin; e += NT) {
     const int pos = e / cpg, wc = e - pos * cpg;
     const int gy = wy0 + pos / WCc, gxp = wx0 + pos % WCc;
     if (gy < 0 || gy >= a.H || gxp < 0 || gxp >= a.W) continue;
     const long o = ((long)n * HW + (long)gy * a.W + gxp) * C + g * cpg + wc;
-    const float v = sAcc[e];
-    if (v == 0.f) continue;
-    if (DET)
-      atomicAdd(reinterpret_cast<unsigned long long *>(gxi + o),
-                (unsigned long long)__double2ll_rn((double)v * scale));
-    else
-      atomicAdd(gx + o, v);
+    if (DET) {
+      const long long v = reinterpret_cast<long long *>(sAcc)[e];
+      if (v) atomicAdd(reinterpret_cast<unsigned long long *>(gxi + o), (unsigned long long)v);
+    } else {
+      const float v = reinterpret_cast<float *>(sAcc)[e];
+      if (v != 0.f) atomicAdd(gx + o, v);
+    }
   }
 }
 
@@ -3073,14 +3033,16 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
 #endif
     const int cpg = c / dg, R = 2;
     const int WR = 8 + (kh - 1) * dil + 2 * R, WCw = 8 + (kw - 1) * dil + 2 * R;
-    const size_t smem3 = sizeof(float) * ((size_t)co * GP + (size_t)KC * WTP + (size_t)PT * (KC + 1) +
-                                          (size_t)PT * 16 + (size_t)WR * WCw * cpg) +
-                         (size_t)2 * WR * WCw * (4 + WIN_CAP);
-    // window form (stride 1, 8/16/32 channels per deformable group; owner-computes window sums,
-    // see mdcn_bwd_data_win_kernel), else the global-atomic form; algo forces one (tests)
-    const bool win_ok = stride == 1 && (cpg == 8 || cpg == 16 || cpg == 32) && smem3 <= 160 * 1024;
+    const size_t smem3 = sizeof(float) * ((size_t)co * GP + (size_t)KC * WTP + (size_t)KC * CP + (size_t)PT * 16) +
+                         (size_t)WR * WCw * cpg * (det ? 8 : 4);
+    // window form (stride 1, <= 32 channels per deformable group): grad_x summed per 8x8 tile in
+    // LDS.  AUTO takes it for the deterministic form only: there it is 11-22 % faster (int64 LDS
+    // atomics replace int64 global ones); with float atomics the global-atomic kernel is faster
+    // (agg_s0 4.6 vs 7.3 ms: the 75 KB of LDS halve the waves that hide the per-tap gather
+    // latency).  algo forces one form (tests).
+    const bool win_ok = stride == 1 && cpg <= KC && smem3 <= 160 * 1024;
     if (algo == AANET_DCN_BWD_WINDOW && !win_ok) return AANET_EUNSUPPORTED;
-    if (win_ok && algo != AANET_DCN_BWD_GLOBAL) {
+    if (win_ok && (algo == AANET_DCN_BWD_WINDOW || (algo == AANET_DCN_BWD_AUTO && det))) {
       static const bool win_attr = [] {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_win_kernel<0>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);

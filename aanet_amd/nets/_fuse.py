@@ -159,9 +159,10 @@ def offset_conv_pack(conv):
     """(pre-split fragments, bias) of a deformable offset_conv for ops.conv3x3_grouped_nhwc,
     cached on the conv and keyed by its folded weights; None when the conv is outside the kernel
     (3x3, stride 1, padding = dilation, 32k channels per group, <= 32 outputs per group).
-    Opt-in (AANET_OFFSET_KERNEL=1): in the C2 step it measured slower than the conv engine's
-    halo form (3.57 vs 3.44 ms, same call), so the engine stays the default."""
-    if os.environ.get("AANET_OFFSET_KERNEL", "0") != "1" or type(conv) is not nn.Conv2d or \
+    Round 4: the kernel is the halo form owning every group of its tile (conv_g3.hip): 94-95 vs
+    102-103 us for the engine's halo form at C2 scale 0, step 3.636 vs 3.662 ms (same call,
+    DESIGN.md 3), so it is the default; the round-3 direct form was slower than the engine."""
+    if type(conv) is not nn.Conv2d or \
             not engine_conv(conv) or _int(conv.kernel_size) != 3 or _int(conv.stride) != 1 or \
             _int(conv.padding) != _int(conv.dilation) or \
             (conv.in_channels // conv.groups) % 32 or (conv.out_channels // conv.groups) > 32:
@@ -195,9 +196,8 @@ def offset_conv_eval(x, conv):
 
 
 def s2_conv_ok(conv):
-    """A conv of the CSA down chains that ops.conv3x3_s2 takes (3x3, stride 2, pad 1, plain);
-    AANET_S2_KERNEL=0 keeps them on the conv engine (A/B switch)."""
-    return os.environ.get("AANET_S2_KERNEL", "1") != "0" and type(conv) is nn.Conv2d and engine_conv(conv) and _int(conv.kernel_size) == 3 and \
+    """A conv of the CSA down chains that ops.conv3x3_s2 takes (3x3, stride 2, pad 1, plain)."""
+    return type(conv) is nn.Conv2d and engine_conv(conv) and _int(conv.kernel_size) == 3 and \
         _int(conv.stride) == 2 and _int(conv.padding) == 1 and _int(conv.dilation) == 1 and \
         conv.groups == 1 and conv.in_channels % 32 == 0 and conv.out_channels % 16 == 0 and \
         conv.out_channels <= 96

@@ -57,11 +57,11 @@ def test_conv3x3_grouped_nhwc_vs_fp64(case):
     assert torch.equal(again, got)  # no atomics, fixed order
 
 
-def test_offset_conv_eval_uses_kernel_and_matches_engine(monkeypatch):
-    """DeformSimpleBottleneck's eval offset_conv (nets/_fuse.offset_conv_eval, opt-in) takes the
-    grouped kernel for the scale-0 shape and agrees with the conv engine's form (the default path) within the split contraction's error."""
+def test_offset_conv_eval_uses_kernel_and_matches_engine():
+    """DeformSimpleBottleneck's eval offset_conv (nets/_fuse.offset_conv_eval) takes the grouped
+    halo kernel for the scale-0 shape and agrees with the conv engine's form within the split
+    contraction's error."""
     from aanet_amd.nets import _fuse
-    monkeypatch.setenv("AANET_OFFSET_KERNEL", "1")  # opt-in path (read per call)
     torch.manual_seed(0)
     blk = nets.DeformSimpleBottleneck(64, 64, mdconv_dilation=2, deformable_groups=2).to(DEV).eval()
     oc = blk.conv2.offset_conv

@@ -23,12 +23,12 @@ for r in 1 2; do
   done
 done
 # DCN tail variants (tools/build_variant.sh: DCN_NOOK, DCN_NT): parity, then same-call timing
-for V in nook nt ntnook lb2 prio; do
+for V in nook nt ntnook lb2 prio pf pfnook; do
   AANET_MI355X_LIB=aanet_amd/libaanet_mi355x_$V.so $T 300 python -u -m pytest tests/test_gpu_dcn_tile.py tests/test_gpu_split.py -m gpu -q -rf --timeout 120 --timeout-method thread > gpurun_out/r04d_tests_$V.log 2>&1
   rc2=$?; echo "== $V tests"; tail -2 gpurun_out/r04d_tests_$V.log; [ $rc2 -le 1 ] || exit $rc2
 done
 for r in 1 2 3; do
-  for V in base nook nt ntnook lb2 prio; do
+  for V in base nook nt ntnook lb2 prio pf pfnook; do
     L=aanet_amd/libaanet_mi355x_$V.so; [ $V = base ] && L=aanet_amd/libaanet_mi355x.so
     echo "== $V round $r"; AANET_MI355X_LIB=$L $T 120 python tools/dcn_tile_bench.py 30 0.5 || exit 9
   done
