@@ -135,6 +135,12 @@ __device__ __forceinline__ TapState tap_state(float oh, float ow, float ml, int 
 // CG = channels per deformable group (two groups): 32 (scale 0: C = 64) or 16 (scale 1: C = 32).
 // A chunk is one tap of a 32-channel K slice ("phase"): with CG = 32 a phase is one group, with
 // CG = 16 it holds both groups (lane groups kr = 0, 1 carry group 0's channels, kr = 2, 3 group 1's).
+// Tile order inside an XCD's contiguous range: row-major (0) or column-major (1, vertical
+// neighbours -- which share half their window rows -- run next to each other).
+#ifndef DCN_COLMAJOR
+#define DCN_COLMAJOR 0
+#endif
+
 template <int DIL, int CG, bool POST>
 __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   constexpr int CT = 2 * CG;             // channels = Co = Co2
@@ -166,7 +172,12 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b0 & 7;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b0 >> 3);
   const int n = bid / ntiles, tile = bid % ntiles;
+#if DCN_COLMAJOR
+  const int ty = (H + TR - 1) / TR;
+  const int y0 = (tile % ty) * TR, x0 = (tile / ty) * TC;
+#else
   const int y0 = (tile / tx) * TR, x0 = (tile % tx) * TC;
+#endif
   const int wy0 = y0 - MG, wx0 = x0 - MG;
   const int py = y0 + wave, px = x0 + jj;  // this lane's output pixel
   const bool pv = py < H && px < W;
@@ -338,6 +349,9 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   // front of it; issued after the DMA, that wait exposed the DMA's whole L2 latency every chunk.
   float pf_win = 0.f, pf_res = 0.f;
   auto step = [&](int c, const char *cur, char *nxt) {
+#if DCN_UNROLL
+    __builtin_amdgcn_sched_barrier(0);  // unrolled: no code motion across chunk boundaries
+#endif
     const int g = c >= K ? 1 : 0, k = c - K * g, t0 = k - k % TPP;
     TapState s;
     if (k == 0) {  // group start: its window (loaded in the chunk before) and pass-0 states
@@ -571,8 +585,14 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
     const int bid2 = (xc2 < r82 ? xc2 * (q82 + 1) : r82 * (q82 + 1) + (xc2 - r82) * q82) + (bb >> 3);
     const int t2 = bid2 % nt2;
     pn = bid2 / nt2;
+#if DCN_COLMAJOR
+    const int ty2 = (H + TR - 1) / TR;
+    ppy = (t2 % ty2) * TR + pwave;
+    ppx = (t2 / ty2) * TC + pjj;
+#else
     ppy = (t2 / tx2) * TR + pwave;
     ppx = (t2 % tx2) * TC + pjj;
+#endif
   }
   const bool ppv = ppy < H && ppx < W;
   bf16x8 B3[2][3];

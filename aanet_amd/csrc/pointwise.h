@@ -15,8 +15,7 @@ struct PwArgs {
   int N, C, P, Co, in_nhwc, out_nhwc;
 };
 
-// 1 when pw_conv_launch takes the shape (np = N*P pixels, p = P pixels per image) and AANET_PW
-// is not 0.
+// 1 when pw_conv_launch takes the shape (np = N*P pixels, p = P pixels per image).
 int pw_conv_supported(int c, int co, int kh, int kw, int stride, int pad, int groups, long np,
                       int out_nhwc, int p);
 int pw_conv_launch(const PwArgs &a, hipStream_t stream);

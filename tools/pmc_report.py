@@ -11,7 +11,9 @@ from collections import defaultdict
 root = sys.argv[1]
 subs = sys.argv[2:] or [""]
 vals = defaultdict(lambda: defaultdict(list))
-for f in sorted(glob.glob(os.path.join(root, "pass*", "**", "*counter_collection.csv"), recursive=True)):
+files = sorted(glob.glob(os.path.join(root, "pass*", "**", "*counter_collection.csv"), recursive=True)) or \
+    sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True))
+for f in files:
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
         key = next((s for s in subs if s in name), None)

@@ -25,8 +25,8 @@ KMAP = {"corr_volume_s0": r"corr_reg_kernel<5, 8, 2>", "disp_regress_s0": r"disp
         # MODE, CO_T, PTT, PACKED, TAIL, SCHED, FULL, LAYOUT, CFG, PREC (1: split-bf16), HALO (= dil),
         # POST (0: no post stage)
         "conv3x3_pw_s0": r"conv_fwd_kernel<0, 64, 128, 1, 1, 1, 1, 1, 0, 1, 1, 0>",
-        # the scale-0 offset_conv (halo form, HALO = dilation 2, split-bf16)
-        "offset_conv_s0": r"conv_fwd_kernel<0, 32, 128, 1, 0, 1, 1, 1, 0, 1, 2, 0>",
+        # the scale-0 offset_conv (conv_g3.hip halo kernel: G=2 groups in one WG, NCC=1, NCB=2, dil 2)
+        "offset_conv_s0": r"conv3x3_g3_kernel<2, 1, 2, 2>",
         # the scale-0 heads launch of the CSA exchange (conv_s2.hip row form, 6 co blocks, 2 chunks)
         "s2_heads_s0": r"conv3x3s2_rows_kernel<6, 2>",
         # the C5 concat volume (shift_volume_band_kernel, concat form)
