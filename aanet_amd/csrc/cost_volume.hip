@@ -612,9 +612,9 @@ __global__ __launch_bounds__(256) void shift_volume_kernel(const float *__restri
 // Band form (W % 4 == 0): one workgroup per band of YB consecutive source rows y of one (b, c).
 // The band's left and right rows are read once into LDS, then the workgroup writes all D shifted
 // copies: concat oc = c (left, x >= d) and oc = C + c (right at x - d); difference oc = c.  Each
-// (oc, d) plane receives YB*W contiguous floats (16-byte non-temporal stores): long contiguous
-// write streams run at 5.2 TB/s where one-row (1.2 KB) segments ran at 3.5 TB/s
-// (tools/shift_lab.hip, C5 [4,32,96,312], D=48).  HBM reads are exactly the two feature maps.
+// (oc, d) plane receives YB*W contiguous floats (16-byte stores): long contiguous write streams
+// run at 5.2 TB/s where one-row (1.2 KB) segments ran at 3.5 TB/s (tools/shift_lab.hip, C5
+// [4,32,96,312], D=48).  HBM reads are exactly the two feature maps.
 // LDS layout (round 4): each row is stored as 4 residue planes, element x at (x & 3) * W/4 + x/4.
 // A thread writes output columns 4k..4k+3 and reads source element 4k + u - d: in the row-major
 // layout the 32 lanes of a ds_read_b32 hit words 4 apart (8 banks: a 4-way conflict on every
@@ -649,28 +649,55 @@ __global__ __launch_bounds__(256) void shift_volume_band_kernel(const float *__r
   const long HW = (long)H * W;
   float *o0 = out + (((long)b * OC + c) * D * H + y0) * W;               // oc = c
   float *o1 = CONCAT ? o0 + (long)C * D * HW : nullptr;                  // oc = C + c
-  for (int e = tid; e < D * S4; e += 256) {
-    const int d = e / S4, r = e - d * S4, yy = r / W4, k = r - yy * W4, x = 4 * k;
-    const float *l = sL + yy * W, *rr = sR + yy * W;
-    f32x4 vl, vr;
+  // Thread slots r = tid + 256 i (i < MAXSLOT: S4 <= 2048, band_rows): the row / column of a slot
+  // and its left values are fixed for the whole d loop; per (d, slot) the right values sit at
+  // residue-plane offsets that are the same for every lane ((u - d) & 3 and (u - d) >> 2), so the
+  // loop body is 4 LDS reads, 8 selects and 2 stores (the d-major order keeps each plane's 8-row
+  // segment a contiguous write stream).  Plain stores: a pure 1 MB-per-workgroup store stream ran
+  // at 5.65-5.73 TB/s plain vs 5.27-5.36 TB/s non-temporal (tools/write_ceiling.hip), and this
+  // kernel at 277-280 vs 288-289 us (C5).
+  constexpr int MAXSLOT = 8;
+  int rb[MAXSLOT], x4[MAXSLOT];
+  f32x4 lv[MAXSLOT];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int xs = x + u - d;  // source column of the right map
-      const bool ok = xs >= 0;
-      vl[u] = ok ? l[u * W4 + k] : 0.f;
-      vr[u] = ok ? rr[(xs & 3) * W4 + (xs >> 2)] : 0.f;
-    }
-    const long off = (long)d * HW + 4 * r;
-    if (CONCAT) {
-      __builtin_nontemporal_store(vl, reinterpret_cast<f32x4 *>(o0 + off));
-      __builtin_nontemporal_store(vr, reinterpret_cast<f32x4 *>(o1 + off));
-    } else {
-      __builtin_nontemporal_store(vl - vr, reinterpret_cast<f32x4 *>(o0 + off));
+  for (int i = 0; i < MAXSLOT; ++i) {
+    const int r = tid + 256 * i, rr = r < S4 ? r : 0;
+    const int yy = rr / W4, k = rr - yy * W4;
+    rb[i] = yy * W + k;
+    x4[i] = r < S4 ? 4 * k : -0x40000000;  // slots past the band never store
+#pragma unroll
+    for (int u = 0; u < 4; ++u) lv[i][u] = sL[yy * W + u * W4 + k];
+  }
+  for (int d = 0; d < D; ++d) {
+    int ro[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ro[u] = __builtin_amdgcn_readfirstlane(((u - d) & 3) * W4 + ((u - d) >> 2));
+    float *p0 = o0 + (long)d * HW;
+    float *p1 = CONCAT ? o1 + (long)d * HW : nullptr;
+#pragma unroll
+    for (int i = 0; i < MAXSLOT; ++i) {
+      if (256 * i >= S4) break;  // uniform
+      if (x4[i] < -0x20000000) continue;
+      f32x4 vl, vr;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = x4[i] + u >= d;
+        vl[u] = ok ? lv[i][u] : 0.f;
+        vr[u] = ok ? sR[rb[i] + ro[u]] : 0.f;
+      }
+      const long off = 4L * (tid + 256 * i);
+      if (CONCAT) {
+        *reinterpret_cast<f32x4 *>(p0 + off) = vl;
+        *reinterpret_cast<f32x4 *>(p1 + off) = vr;
+      } else {
+        *reinterpret_cast<f32x4 *>(p0 + off) = vl - vr;
+      }
     }
   }
 }
 
-// rows per band: 8, fewer when the band's two LDS rows would exceed 64 KB
+// rows per band: 8, fewer when the band's two LDS rows would exceed 64 KB (so S4 = rows * W / 4
+// <= 2048: the band kernel's 8 thread slots)
 int band_rows(int w) {
   int yb = 8;
   while (yb > 1 && 2L * yb * w * 4 > 64 * 1024) yb >>= 1;

@@ -21,6 +21,7 @@ CASES = [
     (1, 32, 12, 20, 27, 1, 2),    # one group of 32
     (1, 64, 9, 17, 32, 1, 2),     # one group, two chunks
     (3, 64, 5, 4, 54, 2, 2),      # image smaller than the dilated stencil
+    (1, 32, 11, 19, 32, 1, 1),    # one group of 32, 32 outputs (full co blocks), dilation 1
 ]
 
 
