@@ -41,16 +41,6 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 
-#ifndef DCN_PFWAIT
-#define DCN_PFWAIT 0
-#endif
-#ifndef DCN_PRIO
-#define DCN_PRIO 0
-#endif
-#ifndef DCN_UNROLL
-#define DCN_UNROLL 0
-#endif
-
 constexpr int NT = 512;          // 8 waves, one tile row each
 constexpr int TR = 8, TC = 16;   // tile: 8 rows x 16 columns of output pixels
 constexpr int RW = 2;            // window margin beyond the taps: offsets in [-RW, RW) stay inside
@@ -135,12 +125,6 @@ __device__ __forceinline__ TapState tap_state(float oh, float ow, float ml, int 
 // CG = channels per deformable group (two groups): 32 (scale 0: C = 64) or 16 (scale 1: C = 32).
 // A chunk is one tap of a 32-channel K slice ("phase"): with CG = 32 a phase is one group, with
 // CG = 16 it holds both groups (lane groups kr = 0, 1 carry group 0's channels, kr = 2, 3 group 1's).
-// Tile order inside an XCD's contiguous range: row-major (0) or column-major (1, vertical
-// neighbours -- which share half their window rows -- run next to each other).
-#ifndef DCN_COLMAJOR
-#define DCN_COLMAJOR 0
-#endif
-
 template <int DIL, int CG, bool POST>
 __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   constexpr int CT = 2 * CG;             // channels = Co = Co2
@@ -172,12 +156,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b0 & 7;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b0 >> 3);
   const int n = bid / ntiles, tile = bid % ntiles;
-#if DCN_COLMAJOR
-  const int ty = (H + TR - 1) / TR;
-  const int y0 = (tile % ty) * TR, x0 = (tile / ty) * TC;
-#else
   const int y0 = (tile / tx) * TR, x0 = (tile % tx) * TC;
-#endif
   const int wy0 = y0 - MG, wx0 = x0 - MG;
   const int py = y0 + wave, px = x0 + jj;  // this lane's output pixel
   const bool pv = py < H && px < W;
@@ -349,9 +328,6 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   // front of it; issued after the DMA, that wait exposed the DMA's whole L2 latency every chunk.
   float pf_win = 0.f, pf_res = 0.f;
   auto step = [&](int c, const char *cur, char *nxt) {
-#if DCN_UNROLL
-    __builtin_amdgcn_sched_barrier(0);  // unrolled: no code motion across chunk boundaries
-#endif
     const int g = c >= K ? 1 : 0, k = c - K * g, t0 = k - k % TPP;
     TapState s;
     if (k == 0) {  // group start: its window (loaded in the chunk before) and pass-0 states
@@ -379,27 +355,13 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       pf_res = a.residual[((long)(n * a.Co2 + co2) * H + yy) * W + x0];
     }
     tap(g, k, cur, s, NPH == 2 && c == K - 1);
-#if DCN_PFWAIT
-    // the warm-up load (issued after the DMA, so the youngest) is left in flight for a chunk
-    const bool pf = (NPH == 2 && c == 3 && wave * 64 < WR * WC) || (c == NCH - 6 && a.residual);
-    if (pf)
-      asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else
-#endif
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of A(c+1) landed ...
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of A(c+1) landed ...
     if (!(a.dbg & 8)) __syncthreads();                 // ... and every other wave's
   };
   load_window(0);
   issue_a(0, sA0);
   load_pass(0, 0);
-#if DCN_PRIO
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // MI355X_MICROARCH.md item 4: the younger half
-#endif
-#if DCN_UNROLL
-#pragma unroll
-#else
 #pragma unroll 1
-#endif
   for (int c = 0; c < NCH - 1; c += 2) {
     step(c, sA0, sA1);
     step(c + 1, sA1, sA0);
@@ -585,14 +547,8 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
     const int bid2 = (xc2 < r82 ? xc2 * (q82 + 1) : r82 * (q82 + 1) + (xc2 - r82) * q82) + (bb >> 3);
     const int t2 = bid2 % nt2;
     pn = bid2 / nt2;
-#if DCN_COLMAJOR
-    const int ty2 = (H + TR - 1) / TR;
-    ppy = (t2 % ty2) * TR + pwave;
-    ppx = (t2 / ty2) * TC + pjj;
-#else
     ppy = (t2 / tx2) * TR + pwave;
     ppx = (t2 % tx2) * TC + pjj;
-#endif
   }
   const bool ppv = ppy < H && ppx < W;
   bf16x8 B3[2][3];

@@ -574,9 +574,10 @@ def mdcn_backward(x, offset, mask, weight, grad_out, with_bias, stride, padding,
     """deform_conv_cuda.cpp:571-685 -> (gX, gOffset, gMask, gW, gB or None).
 
     Default: aanet_mdcn_bwd_algo_f32 with the caller-owned workspace; algo "auto" takes the
-    LDS-window form of grad_x for the deterministic backward where it applies (stride 1, <= 32
-    channels per deformable group) and the global-atomic form otherwise; "window" / "global"
-    force one form (AANET_EUNSUPPORTED if the window form does not apply).  nchw_scatter=True: the workspace-free aanet_mdcn_bwd_f32 (global atomics in NCHW).
+    LDS-window form of grad_x where it applies (stride 1, <= 32 channels per deformable group,
+    channel counts divisible by 4; int64 fixed-point window in both modes) and the global-atomic
+    form otherwise; "window" / "global" force one form (AANET_EUNSUPPORTED if the window form
+    does not apply).  nchw_scatter=True: the workspace-free aanet_mdcn_bwd_f32 (global atomics in NCHW).
 
     deterministic (default: torch.are_deterministic_algorithms_enabled()): the bit-reproducible
     form (fixed-point grad_x accumulation, ordered grad_W reduction) instead of float atomics."""

@@ -351,13 +351,15 @@ int aanet_mdcn_bwd_det_f32(const float *x, const float *offset, const float *mas
  * AANET_DCN_BWD_AUTO).  deterministic: 0 = float atomics (workspace of
  * aanet_mdcn_bwd_ws_workspace_size bytes), 1 = fixed point (aanet_mdcn_bwd_det_workspace_size). */
 enum {
-  AANET_DCN_BWD_AUTO = 0,   /* deterministic: the window form where it applies; float: global */
+  AANET_DCN_BWD_AUTO = 0,   /* the window form where it applies, else global (both modes) */
   AANET_DCN_BWD_GLOBAL = 1, /* one global atomic per (pixel, tap, corner, channel) contribution,
                                the reference's col2im pattern (kernel.cu:635-693), into an NHWC
                                accumulator */
-  AANET_DCN_BWD_WINDOW = 2  /* stride 1, <= 32 channels per deformable group: each 8x8 output
-                               tile sums its contributions in an LDS window (LDS atomics) and
-                               adds the window once (AANET_EUNSUPPORTED for other shapes) */
+  AANET_DCN_BWD_WINDOW = 2  /* stride 1, <= 32 channels per deformable group, channel counts
+                               divisible by 4: each (8x8 output tile, 16-channel slice) sums its
+                               contributions in an int64 fixed-point LDS window and adds the
+                               window once -- float atomics (deterministic = 0) or int64 ones
+                               (AANET_EUNSUPPORTED for other shapes) */
 };
 int aanet_mdcn_bwd_algo_f32(const float *x, const float *offset, const float *mask,
                             const float *weight, const float *grad_out, float *grad_x,

@@ -292,8 +292,9 @@ def test_deterministic_mode_reaches_shim_and_torch_ops():
 @pytest.mark.parametrize("algo", ["window", "global"])
 def test_mdcn_backward_window_form_vs_oracle(case, algo):
     """The LDS-window grad_x form (mdcn_bwd_data_win_kernel: stride 1, <= 32 channels per
-    deformable group) and the global-atomic form, each in float and fixed-point mode, against the
-    oracle, with offsets large enough that some corners fall outside the window.  Shapes the
+    deformable group, channel counts that allow channels-last reads; int64 fixed-point window,
+    16-channel slices) and the global-atomic form, each in float and fixed-point mode, against
+    the oracle, with offsets large enough that some corners fall outside the window.  Shapes the
     window form does not take report AANET_EUNSUPPORTED."""
     N, C, H, W, Co, k, s, p, d, dg = case
     x, off, msk, w, b = make_case(9, N, C, H, W, Co, k, s, p, d, dg, off_scale=2.5)
@@ -305,7 +306,7 @@ def test_mdcn_backward_window_form_vs_oracle(case, algo):
                                     dg, deterministic=det, algo=algo)
         except _lib.AanetError as e:
             assert algo == "window" and e.status == _lib.EUNSUPPORTED and \
-                (s != 1 or C // dg > 32), (case, e)
+                (s != 1 or C // dg > 32 or C % 4 or (C // dg) % 4), (case, e)
             return
         ref = oracle.mdcn_backward(x, off, msk, w, go, True, s, p, d, 1, dg)
         for name, gt, r in zip(("grad_input", "grad_offset", "grad_mask", "grad_weight", "grad_bias"), got, ref):
@@ -318,8 +319,8 @@ def test_mdcn_backward_window_form_vs_oracle(case, algo):
 def test_mdcn_backward_c4_agg_s0_vs_oracle(form):
     """SURVEY C4 at the aggregation's scale-0 shape: one image of 64 channels at 128x416,
     dg 2, 3x3, dil 2 (the C2 bottleneck DCN), against the oracle, for the global float-atomic
-    (NHWC workspace scatter), window (the default) and fixed-point deterministic (window and
-    global) forms.  Grids ~100x those of BWD_CASES (deform_conv_cuda_kernel.cu:635-767)."""
+    (NHWC workspace scatter), window (the default in both modes: int64 fixed-point LDS window)
+    and fixed-point deterministic (window and global) forms.  Grids ~100x those of BWD_CASES (deform_conv_cuda_kernel.cu:635-767)."""
     N, C, H, W, Co, k, s, p, d, dg = 1, 64, 128, 416, 64, 3, 1, 2, 2, 2
     x, off, msk, w, b = make_case(11, N, C, H, W, Co, k, s, p, d, dg, off_scale=0.7)
     go = np.random.default_rng(12).standard_normal((N, Co, H, W)).astype(np.float32)
