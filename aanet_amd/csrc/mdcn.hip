@@ -1715,13 +1715,13 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_nhwc_kernel(MdcnArgs a, cons
   }
 }
 
-// Window form of mdcn_bwd_data_nhwc_kernel (stride 1, <= 32 channels per deformable group).  The
-// workgroup owns an 8 x 8 output tile, one deformable group and a 16-channel slice of it
-// (blockIdx.y = g * NH + slice), and sums its grad_x corner contributions in an LDS copy of the
-// tile's input window (rows/cols [origin, origin + WR/WC): the corners of every offset in
-// [-R, R)), then adds the window to the global accumulator once -- one global add per window
-// element instead of one per (pixel, tap, corner, channel).  Corners outside the window take a
-// global atomic directly.
+// Window form of mdcn_bwd_data_nhwc_kernel (stride 1, <= 32 channels per deformable group,
+// K <= 9 taps, <= 64 output channels).  The workgroup owns an 8 x 8 output tile and one deformable group, and walks the
+// group's channels in 16-channel slices: per slice it sums the grad_x corner contributions in an
+// LDS copy of the tile's input window (rows/cols [origin, origin + WR/WC): the corners of every
+// offset in [-R, R)), then adds the window to the global accumulator once -- one global add per
+// window element instead of one per (pixel, tap, corner, channel).  Corners outside the window
+// take a global atomic directly.
 // The window is INT64 FIXED POINT in both modes (scale 2^(38 - ceil(log2 bound)), computed on
 // the device by det_scale_kernel): an LDS ds_add_u64 costs ~26 cycles per wave-instruction per CU
 // against ~196 for ds_add_f32 (tools/lds_rmw_lab.hip, profiles/r04_lds_scatter_probe.txt), and
@@ -1729,16 +1729,21 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_nhwc_kernel(MdcnArgs a, cons
 // (two workgroups per CU).  DET: the window and the out-of-window corners go to the int64 global
 // accumulator (bit-reproducible); otherwise the window is converted once to float and added with
 // float atomics (its per-tile sums are exact to 2^-38 of the bound before that one rounding).
-// grad_offset / grad_mask: each slice adds its partial channel sum to the zeroed outputs when
-// there are two slices (two addends onto 0: the same float in either order), else stores it.
+// grad_offset / grad_mask: the first slice's per-(tap, pixel) channel sums wait in LDS (sP) and
+// the last slice adds its own and stores the result -- no atomics, fixed order.
+// Taps are software-pipelined: the raw offsets / mask of the next tap (wave 0, lane = pixel) and
+// this thread's elements of the next tap's W^T slice are loaded into registers one tap ahead.
 // Round 4 also tried an atomic-free "owner computes" form (per-tap tables of the pixels whose
 // corner block starts at each window position): bit-reproducible, but slower -- agg_s0 backward
 // 7.84 ms float / 8.20 ms fixed point: the owner loop is a chain of dependent LDS reads per window
 // position and tap.  It is in the git history (round 4).
-// dynamic LDS: sG [Co][GP], sWt [16][WTP], sCg [16][CP], sS [PT][16], window [WR*WC][16] int64
-constexpr int WHC = 16;  // channels per window workgroup
+// dynamic LDS: sG [Co][GP], sWt [16][WTP], sCg [16][CP], sS [PT][16], sP [3][9][PT],
+// window [WR*WC][16] int64
+constexpr int WHC = 16;  // channels per window slice
+constexpr int WKMAX = 9; // taps the sP partial buffer holds
+constexpr int WCOMAX = 64;  // output channels (the W^T slice is prefetched in registers)
 template <int DET>
-__global__ __launch_bounds__(NT) void mdcn_bwd_data_win_kernel(MdcnArgs a, const float *__restrict__ xh,
+__global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, const float *__restrict__ xh,
                                                                const float *__restrict__ wT,
                                                                const float *__restrict__ gout,
                                                                float *__restrict__ gx,
@@ -1753,17 +1758,18 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_win_kernel(MdcnArgs a, const
   float *sWt = sG + Co * GP;            // [16][WTP]     W^T slice
   float *sCg = sWt + WHC * WTP;         // [16][CP]      colg slice
   float *sS = sCg + WHC * CP;           // [PT][16]      per-pixel corners, weights, mask, window pos
-  long long *sAcc = reinterpret_cast<long long *>(sS + PT * 16);  // [WR*WC][16]
+  float *sP = sS + PT * 16;             // [3][WKMAX][PT] first slice's grad_offset / mask sums
+  long long *sAcc = reinterpret_cast<long long *>(sP + 3 * WKMAX * PT);  // [WR*WC][16]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long P = (long)a.Ho * a.Wo;
   const int ttx = (a.Wo + 7) / 8, tpi = ttx * ((a.Ho + 7) / 8);
   const int K = a.kh * a.kw, cpg = a.C / a.dg, C = a.C;
   const int NH = (cpg + WHC - 1) / WHC;
-  const int n = blockIdx.x / tpi, tile = blockIdx.x % tpi, g = blockIdx.y / NH, sl = blockIdx.y % NH;
+  const int n = blockIdx.x / tpi, tile = blockIdx.x % tpi, g = blockIdx.y;
   const int ty0 = (tile / ttx) * 8, tx0 = (tile % ttx) * 8;
-  const int cb0 = g * cpg + sl * WHC, rows = min(WHC, (g + 1) * cpg - cb0);
   const long HW = (long)a.H * a.W;
   const double scale = *det_scale;
+  const double inv = 1.0 / scale;
   const float *xn = xh + (long)n * HW * C;
   const int wy0 = ty0 - a.pad - R, wx0 = tx0 - a.pad - R;  // window origin (stride 1)
   const int nwin = WR * WCc * WHC;
@@ -1771,7 +1777,6 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_win_kernel(MdcnArgs a, const
     const int y = ty0 + (pl >> 3), x = tx0 + (pl & 7);
     return (y < a.Ho && x < a.Wo) ? (long)y * a.Wo + x : -1;
   };
-  for (int e = tid; e < nwin; e += NT) sAcc[e] = 0;
   for (int e = tid; e < Co * PT; e += NT) {
     const int co = e / PT, pl = e % PT;
     const long pp = pix(pl);
@@ -1779,173 +1784,187 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_win_kernel(MdcnArgs a, const
   }
   const int kr = lane >> 4, jj = lane & 15;
   const int q = tid & 3, qpx = tid >> 2;  // gradient role: channel quad q of pixel qpx
-  // Software pipeline over taps: the raw offsets / mask of tap k+1 (wave 0, lane = pixel) and this
-  // thread's elements of tap k+1's W^T slice are loaded into registers during tap k, so no tap
-  // waits for a global round trip before its sampling state and colg exist.
   const long sp = pix(lane);
   const int sy = sp >= 0 ? (int)(sp / a.Wo) : 0, sx = sp >= 0 ? (int)(sp % a.Wo) : 0;
   const float *offg = a.offset + (long)n * a.off_bs + (long)g * 2 * K * P + (sp >= 0 ? sp : 0);
-  constexpr int WPT = WHC * 256 / NT;  // W^T slice elements per thread (Co <= 256)
+  constexpr int WPT = WHC * WCOMAX / NT;  // W^T slice elements per thread
   float roh = 0.f, row = 0.f, rm = 0.f, rw[WPT];
-  auto prefetch = [&](int kk) {
+  auto prefetch = [&](int kk, int c0) {  // tap kk's offsets / mask and W^T rows c0 .. c0+15
     if (wave == 0) {
       roh = offg[(long)(2 * kk) * P];
       row = offg[(long)(2 * kk + 1) * P];
       rm = a.mask[(long)n * a.mask_bs + ((long)g * K + kk) * P + (sp >= 0 ? sp : 0)];
     }
+    const int nr = min(WHC, (g + 1) * cpg - c0);
 #pragma unroll
     for (int j = 0; j < WPT; ++j) {
       const int e = tid + NT * j, co = e % Co, cl = e / Co;
-      rw[j] = (e < WHC * Co && cl < rows) ? wT[((long)kk * C + cb0 + cl) * Co + co] : 0.f;
+      rw[j] = (e < WHC * Co && cl < nr) ? wT[((long)kk * C + c0 + cl) * Co + co] : 0.f;
     }
   };
-  prefetch(0);
-  for (int k = 0; k < K; ++k) {
-    __syncthreads();  // every wave is done with tap k-1 (sS, sWt, sCg); at k = 0: sG, sAcc
-    if (wave == 0) {
+  prefetch(0, g * cpg);
+  for (int sl = 0; sl < NH; ++sl) {
+    const int cb0 = g * cpg + sl * WHC, rows = min(WHC, (g + 1) * cpg - cb0);
+    const bool last = sl == NH - 1;
+    for (int e = tid; e < nwin; e += NT) sAcc[e] = 0;  // ordered by the first tap's barrier
+    for (int k = 0; k < K; ++k) {
+      __syncthreads();  // every wave is done with tap k-1 (sS, sWt, sCg) and the last flush
+      if (wave == 0) {
 #pragma clang fp contract(off)
-      const bool pvalid = sp >= 0;
-      const int i = k / a.kw, j = k % a.kw;
-      const float m = a.mask_logits ? a.mask_scale * (1.f / (1.f + expf(-rm))) : rm;  // deform.py:86-89
-      Samp s;
-      make_samp(s, (float)(sy * a.stride - a.pad + i * a.dil) + roh,
-                (float)(sx * a.stride - a.pad + j * a.dil) + row, a.H, a.W, m);
-      const bool on = pvalid && s.valid;
-      const float hh = 1.f - s.lh, hw = 1.f - s.lw;
-      float *qq = sS + lane * 16;
-      qq[0] = __builtin_bit_cast(float, on && (s.ok & 1) ? s.i1 : -1);
-      qq[1] = __builtin_bit_cast(float, on && (s.ok & 2) ? s.i2 : -1);
-      qq[2] = __builtin_bit_cast(float, on && (s.ok & 4) ? s.i3 : -1);
-      qq[3] = __builtin_bit_cast(float, on && (s.ok & 8) ? s.i4 : -1);
-      qq[4] = hh * hw, qq[5] = hh * s.lw, qq[6] = s.lh * hw, qq[7] = s.lh * s.lw;
-      qq[8] = s.m, qq[9] = s.lh, qq[10] = s.lw, qq[11] = on ? 1.f : 0.f;
-      // window position of the 2x2 corner block (top-left), or -1: global atomics
-      int wpos = -1;
-      if (on) {
-        const int rh = s.hl - wy0, rw_ = s.wl - wx0;
-        if ((unsigned)rh <= (unsigned)(WR - 2) && (unsigned)rw_ <= (unsigned)(WCc - 2)) wpos = rh * WCc + rw_;
+        const bool pvalid = sp >= 0;
+        const int i = k / a.kw, j = k % a.kw;
+        const float m = a.mask_logits ? a.mask_scale * (1.f / (1.f + expf(-rm))) : rm;  // deform.py:86-89
+        Samp s;
+        make_samp(s, (float)(sy * a.stride - a.pad + i * a.dil) + roh,
+                  (float)(sx * a.stride - a.pad + j * a.dil) + row, a.H, a.W, m);
+        const bool on = pvalid && s.valid;
+        const float hh = 1.f - s.lh, hw = 1.f - s.lw;
+        float *qq = sS + lane * 16;
+        qq[0] = __builtin_bit_cast(float, on && (s.ok & 1) ? s.i1 : -1);
+        qq[1] = __builtin_bit_cast(float, on && (s.ok & 2) ? s.i2 : -1);
+        qq[2] = __builtin_bit_cast(float, on && (s.ok & 4) ? s.i3 : -1);
+        qq[3] = __builtin_bit_cast(float, on && (s.ok & 8) ? s.i4 : -1);
+        qq[4] = hh * hw, qq[5] = hh * s.lw, qq[6] = s.lh * hw, qq[7] = s.lh * s.lw;
+        qq[8] = s.m, qq[9] = s.lh, qq[10] = s.lw, qq[11] = on ? 1.f : 0.f;
+        // window position of the 2x2 corner block (top-left), or -1: global atomics
+        int wpos = -1;
+        if (on) {
+          const int rh = s.hl - wy0, rw_ = s.wl - wx0;
+          if ((unsigned)rh <= (unsigned)(WR - 2) && (unsigned)rw_ <= (unsigned)(WCc - 2)) wpos = rh * WCc + rw_;
+        }
+        qq[12] = __builtin_bit_cast(float, wpos);
       }
-      qq[12] = __builtin_bit_cast(float, wpos);
-    }
 #pragma unroll
-    for (int j = 0; j < WPT; ++j) {
-      const int e = tid + NT * j, co = e % Co, cl = e / Co;
-      if (e < WHC * Co) sWt[cl * WTP + co] = rw[j];
-    }
-    if (k + 1 < K) prefetch(k + 1);
-    __syncthreads();
-    // corner quads of the offset / mask partials (pixel qpx, channel quad q), issued before the
-    // colg MFMAs so their latency overlaps them
-    const float *qq = sS + qpx * 16;
-    const f32x4 qi = *reinterpret_cast<const f32x4 *>(qq);
-    const float qi0 = qi[0], qi1 = qi[1], qi2 = qi[2], qi3 = qi[3];
-    const int i1 = __builtin_bit_cast(int, qi0), i2 = __builtin_bit_cast(int, qi1);
-    const int i3 = __builtin_bit_cast(int, qi2), i4 = __builtin_bit_cast(int, qi3);
-    const bool qon = 4 * q < rows;
-    const int cq = cb0 + 4 * q;
-    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-    const f32x4 v1 = qon && i1 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i1 * C + cq) : z;
-    const f32x4 v2 = qon && i2 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i2 * C + cq) : z;
-    const f32x4 v3 = qon && i3 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i3 * C + cq) : z;
-    const f32x4 v4 = qon && i4 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i4 * C + cq) : z;
-    f32x4 cacc = {0.f, 0.f, 0.f, 0.f};
-    for (int ks = 0; ks < Co / 4; ++ks) {
-      const float bv = sG[(4 * ks + kr) * GP + 16 * wave + jj];
-      const float av = sWt[jj * WTP + 4 * ks + kr];
-      cacc = mfma16x16x4(av, bv, cacc);
-    }
+      for (int j = 0; j < WPT; ++j) {
+        const int e = tid + NT * j, co = e % Co, cl = e / Co;
+        if (e < WHC * Co) sWt[cl * WTP + co] = rw[j];
+      }
+      if (k + 1 < K)
+        prefetch(k + 1, cb0);
+      else if (!last)
+        prefetch(0, cb0 + WHC);
+      __syncthreads();
+      // corner quads of the offset / mask partials (pixel qpx, channel quad q), issued before the
+      // colg MFMAs so their latency overlaps them
+      const float *qq = sS + qpx * 16;
+      const f32x4 qi = *reinterpret_cast<const f32x4 *>(qq);
+      const float qi0 = qi[0], qi1 = qi[1], qi2 = qi[2], qi3 = qi[3];
+      const int i1 = __builtin_bit_cast(int, qi0), i2 = __builtin_bit_cast(int, qi1);
+      const int i3 = __builtin_bit_cast(int, qi2), i4 = __builtin_bit_cast(int, qi3);
+      const bool qon = 4 * q < rows;
+      const int cq = cb0 + 4 * q;
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 v1 = qon && i1 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i1 * C + cq) : z;
+      const f32x4 v2 = qon && i2 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i2 * C + cq) : z;
+      const f32x4 v3 = qon && i3 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i3 * C + cq) : z;
+      const f32x4 v4 = qon && i4 >= 0 ? *reinterpret_cast<const f32x4 *>(xn + (long)i4 * C + cq) : z;
+      f32x4 cacc = {0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < Co / 4; ++ks) {
+        const float bv = sG[(4 * ks + kr) * GP + 16 * wave + jj];
+        const float av = sWt[jj * WTP + 4 * ks + kr];
+        cacc = mfma16x16x4(av, bv, cacc);
+      }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) sCg[(4 * kr + r) * CP + 16 * wave + jj] = cacc[r];
-    __syncthreads();
-    float gm = 0.f, goh = 0.f, gow = 0.f;
-    if (qon) {
+      for (int r = 0; r < 4; ++r) sCg[(4 * kr + r) * CP + 16 * wave + jj] = cacc[r];
+      __syncthreads();
+      float gm = 0.f, goh = 0.f, gow = 0.f;
+      if (qon) {
 #pragma clang fp contract(off)
-      const float m = qq[8], lh = qq[9], lw = qq[10];
-      const float hh = 1.f - lh, hw = 1.f - lw;
+        const float m = qq[8], lh = qq[9], lw = qq[10];
+        const float hh = 1.f - lh, hw = 1.f - lw;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float cg = sCg[(4 * q + u) * CP + qpx];
-        const float val = hh * hw * v1[u] + hh * lw * v2[u] + lh * hw * v3[u] + lh * lw * v4[u];
-        gm += cg * val;
-        const float wh = -hw * v1[u] - lw * v2[u] + hw * v3[u] + lw * v4[u];
-        const float ww = -hh * v1[u] + hh * v2[u] - lh * v3[u] + lh * v4[u];
-        const float top = cg * m;
-        goh += wh * top;
-        gow += ww * top;
+        for (int u = 0; u < 4; ++u) {
+          const float cg = sCg[(4 * q + u) * CP + qpx];
+          const float val = hh * hw * v1[u] + hh * lw * v2[u] + lh * hw * v3[u] + lh * lw * v4[u];
+          gm += cg * val;
+          const float wh = -hw * v1[u] - lw * v2[u] + hw * v3[u] + lw * v4[u];
+          const float ww = -hh * v1[u] + hh * v2[u] - lh * v3[u] + lh * v4[u];
+          const float top = cg * m;
+          goh += wh * top;
+          gow += ww * top;
+        }
       }
-    }
-    // grad_x: lane (pixel 16 w + 4 t + lane / 16, channel lane % 16)
-    const int cl = lane & 15;
-    if (cl < rows && a.dbg_noatom != 1) {
-      const long cbase = (long)n * HW * C + cb0 + cl;
+      // grad_x: lane (pixel 16 w + 4 t + lane / 16, channel lane % 16)
+      const int cl = lane & 15;
+      if (cl < rows && a.dbg_noatom != 1) {
+        const long cbase = (long)n * HW * C + cb0 + cl;
 #pragma unroll 2
-      for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < 4; ++t) {
 #pragma clang fp contract(off)
-        const int px = 16 * wave + 4 * t + (lane >> 4);
-        const float *qq = sS + px * 16;
-        const f32x4 qi = *reinterpret_cast<const f32x4 *>(qq);
-        const f32x4 qw = *reinterpret_cast<const f32x4 *>(qq + 4);
-        const float top = sCg[cl * CP + px] * qq[8];
-        const float qi0 = qi[0], qi1 = qi[1], qi2 = qi[2], qi3 = qi[3], q12 = qq[12];
-        const int i1 = __builtin_bit_cast(int, qi0), i2 = __builtin_bit_cast(int, qi1);
-        const int i3 = __builtin_bit_cast(int, qi2), i4 = __builtin_bit_cast(int, qi3);
-        const int wp = __builtin_bit_cast(int, q12);
-        if (wp >= 0) {  // corners outside the image have index -1 (skipped), as below
-          unsigned long long *w0 = reinterpret_cast<unsigned long long *>(sAcc) + (long)wp * WHC + cl;
-          if (i1 >= 0) atomicAdd(w0, (unsigned long long)__double2ll_rn((double)(qw[0] * top) * scale));
-          if (i2 >= 0) atomicAdd(w0 + WHC, (unsigned long long)__double2ll_rn((double)(qw[1] * top) * scale));
-          if (i3 >= 0) atomicAdd(w0 + WCc * WHC, (unsigned long long)__double2ll_rn((double)(qw[2] * top) * scale));
-          if (i4 >= 0) atomicAdd(w0 + (WCc + 1) * WHC, (unsigned long long)__double2ll_rn((double)(qw[3] * top) * scale));
+          const int px = 16 * wave + 4 * t + (lane >> 4);
+          const float *qp = sS + px * 16;
+          const f32x4 pi = *reinterpret_cast<const f32x4 *>(qp);
+          const f32x4 qw = *reinterpret_cast<const f32x4 *>(qp + 4);
+          const float top = sCg[cl * CP + px] * qp[8];
+          const float pi0 = pi[0], pi1 = pi[1], pi2 = pi[2], pi3 = pi[3], q12 = qp[12];
+          const int j1 = __builtin_bit_cast(int, pi0), j2 = __builtin_bit_cast(int, pi1);
+          const int j3 = __builtin_bit_cast(int, pi2), j4 = __builtin_bit_cast(int, pi3);
+          const int wp = __builtin_bit_cast(int, q12);
+          if (wp >= 0) {  // corners outside the image have index -1 (skipped), as below
+            unsigned long long *w0 = reinterpret_cast<unsigned long long *>(sAcc) + (long)wp * WHC + cl;
+            if (j1 >= 0) atomicAdd(w0, (unsigned long long)__double2ll_rn((double)(qw[0] * top) * scale));
+            if (j2 >= 0) atomicAdd(w0 + WHC, (unsigned long long)__double2ll_rn((double)(qw[1] * top) * scale));
+            if (j3 >= 0) atomicAdd(w0 + WCc * WHC, (unsigned long long)__double2ll_rn((double)(qw[2] * top) * scale));
+            if (j4 >= 0) atomicAdd(w0 + (WCc + 1) * WHC, (unsigned long long)__double2ll_rn((double)(qw[3] * top) * scale));
+          } else {
+            auto gadd = [&](int i, float v) {
+              if (DET)
+                atomicAdd(reinterpret_cast<unsigned long long *>(gxi + cbase + (long)i * C),
+                          (unsigned long long)__double2ll_rn((double)v * scale));
+              else
+                atomicAdd(gx + cbase + (long)i * C, v);
+            };
+            if (j1 >= 0) gadd(j1, qw[0] * top);
+            if (j2 >= 0) gadd(j2, qw[1] * top);
+            if (j3 >= 0) gadd(j3, qw[2] * top);
+            if (j4 >= 0) gadd(j4, qw[3] * top);
+          }
+        }
+      }
+      // reduce the 4 channel quads of each pixel (lanes 4j .. 4j+3), fixed order; the first
+      // slice parks its sums in sP, the last adds them (slice order) and stores
+#pragma unroll
+      for (int msk = 1; msk < 4; msk <<= 1) {
+        gm += __shfl_xor(gm, msk);
+        goh += __shfl_xor(goh, msk);
+        gow += __shfl_xor(gow, msk);
+      }
+      if (q == 0) {
+        float *pp = sP + k * PT + qpx;
+        if (sl > 0) {
+          goh = pp[0] + goh;
+          gow = pp[WKMAX * PT] + gow;
+          gm = pp[2 * WKMAX * PT] + gm;
+        }
+        if (!last) {
+          pp[0] = goh, pp[WKMAX * PT] = gow, pp[2 * WKMAX * PT] = gm;
         } else {
-          auto gadd = [&](int i, float v) {
-            if (DET)
-              atomicAdd(reinterpret_cast<unsigned long long *>(gxi + cbase + (long)i * C),
-                        (unsigned long long)__double2ll_rn((double)v * scale));
-            else
-              atomicAdd(gx + cbase + (long)i * C, v);
-          };
-          if (i1 >= 0) gadd(i1, qw[0] * top);
-          if (i2 >= 0) gadd(i2, qw[1] * top);
-          if (i3 >= 0) gadd(i3, qw[2] * top);
-          if (i4 >= 0) gadd(i4, qw[3] * top);
+          const long p = pix(qpx);
+          if (p >= 0) {
+            const long ob = (long)n * a.dg * 2 * K * P + (long)g * 2 * K * P;
+            goff[ob + (long)(2 * k) * P + p] = goh;
+            goff[ob + (long)(2 * k + 1) * P + p] = gow;
+            gmask[(long)n * a.dg * K * P + ((long)g * K + k) * P + p] = gm;
+          }
         }
       }
     }
-    // reduce the 4 channel quads of each pixel (lanes 4j .. 4j+3), fixed order
-#pragma unroll
-    for (int msk = 1; msk < 4; msk <<= 1) {
-      gm += __shfl_xor(gm, msk);
-      goh += __shfl_xor(goh, msk);
-      gow += __shfl_xor(gow, msk);
+    __syncthreads();  // the slice's window is complete
+    if (a.dbg_noatom) continue;
+    // add the window to the global accumulator: consecutive threads take consecutive channels of a
+    // position (16 lanes = one 64-byte (float) / 128-byte (int64) segment); zero elements skipped
+    for (int e = tid; e < nwin; e += NT) {
+      const int pos = e / WHC, wc = e - pos * WHC;
+      const int gy = wy0 + pos / WCc, gxp = wx0 + pos % WCc;
+      if (wc >= rows || gy < 0 || gy >= a.H || gxp < 0 || gxp >= a.W) continue;
+      const long o = ((long)n * HW + (long)gy * a.W + gxp) * C + cb0 + wc;
+      const long long v = sAcc[e];
+      if (!v) continue;
+      if (DET)
+        atomicAdd(reinterpret_cast<unsigned long long *>(gxi + o), (unsigned long long)v);
+      else
+        atomicAdd(gx + o, (float)((double)v * inv));
     }
-    const long p = pix(qpx);
-    if (q == 0 && p >= 0) {
-      const long ob = (long)n * a.dg * 2 * K * P + (long)g * 2 * K * P;
-      float *po = goff + ob + (long)(2 * k) * P + p, *pw = goff + ob + (long)(2 * k + 1) * P + p;
-      float *pm = gmask + (long)n * a.dg * K * P + ((long)g * K + k) * P + p;
-      if (NH == 1) {
-        *po = goh, *pw = gow, *pm = gm;
-      } else {
-        atomicAdd(po, goh), atomicAdd(pw, gow), atomicAdd(pm, gm);
-      }
-    }
-  }
-  __syncthreads();  // the window is complete
-  if (a.dbg_noatom) return;
-  // add the window to the global accumulator: consecutive threads take consecutive channels of a
-  // position (16 lanes = one 64-byte (float) / 128-byte (int64) segment); zero elements skipped
-  const double inv = 1.0 / scale;
-  for (int e = tid; e < nwin; e += NT) {
-    const int pos = e / WHC, wc = e - pos * WHC;
-    const int gy = wy0 + pos / WCc, gxp = wx0 + pos % WCc;
-    if (wc >= rows || gy < 0 || gy >= a.H || gxp < 0 || gxp >= a.W) continue;
-    const long o = ((long)n * HW + (long)gy * a.W + gxp) * C + cb0 + wc;
-    const long long v = sAcc[e];
-    if (!v) continue;
-    if (DET)
-      atomicAdd(reinterpret_cast<unsigned long long *>(gxi + o), (unsigned long long)v);
-    else
-      atomicAdd(gx + o, (float)((double)v * inv));
   }
 }
 
@@ -2986,14 +3005,16 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
   }
   const bool nr = nhs && bwd_nhwc_reads(a);  // channels-last reads too
   const int GP = round_pitch(PT, 16), WTP = round_pitch(co, 2);
-  // window form of grad_x (stride 1, <= 32 channels per deformable group, channels-last reads):
-  // 8x8 tile x 16-channel slice per workgroup, int64 fixed-point LDS window (see the kernel).
+  // window form of grad_x (stride 1, <= 32 channels per deformable group, channels-last reads,
+  // <= 9 taps, <= 64 output channels): 8x8 tile per workgroup in 16-channel slices, int64
+  // fixed-point LDS window.
   // AUTO takes it in both modes; GLOBAL / WINDOW force one form (tests, A/B).
   const int cpg = c / dg, R = 2;
   const int WR = 8 + (kh - 1) * dil + 2 * R, WCw = 8 + (kw - 1) * dil + 2 * R;
-  const size_t smem3 = sizeof(float) * ((size_t)co * GP + (size_t)WHC * WTP + (size_t)WHC * CP + (size_t)PT * 16) +
+  const size_t smem3 = sizeof(float) * ((size_t)co * GP + (size_t)WHC * WTP + (size_t)WHC * CP + (size_t)PT * 16 +
+                                       (size_t)3 * WKMAX * PT) +
                        (size_t)WR * WCw * WHC * 8;
-  const bool win_ok = nr && stride == 1 && cpg <= 2 * WHC && smem3 <= 160 * 1024;
+  const bool win_ok = nr && stride == 1 && cpg <= 2 * WHC && K <= WKMAX && co <= WCOMAX && smem3 <= 160 * 1024;
   if (algo == AANET_DCN_BWD_WINDOW && !win_ok) return AANET_EUNSUPPORTED;
   const bool use_win = win_ok && (algo == AANET_DCN_BWD_WINDOW || algo == AANET_DCN_BWD_AUTO);
   float *xh = nhs ? reinterpret_cast<float *>(wb + L.xh) : nullptr;
@@ -3021,11 +3042,6 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
     hipLaunchKernelGGL(det_absmax_kernel, dim3(host_div_up(nm, 1024) > 512 ? 512 : host_div_up(nm, 1024)),
                        dim3(256), 0, st, mask, nm, bounds + 2);
     hipLaunchKernelGGL(det_scale_kernel, dim3(1), dim3(1), 0, st, bounds, scale);
-  }
-  if (use_win && cpg > WHC) {  // two channel slices add their grad_offset / grad_mask partials
-    e = hipMemsetAsync(grad_offset, 0, sizeof(float) * (size_t)n * dg * 2 * K * P, st);
-    if (e == hipSuccess) e = hipMemsetAsync(grad_mask, 0, sizeof(float) * (size_t)n * dg * K * P, st);
-    if (e != hipSuccess) return (int)e;
   }
   const size_t smem = sizeof(float) * ((size_t)co * GP + (size_t)KC * WTP + (size_t)KC * CP + 3 * 4 * 64 +
                                       (size_t)PT * 12);
@@ -3067,8 +3083,7 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
     a.dbg_noatom = 0;
 #endif
     if (use_win) {
-      const int nsl = (cpg + WHC - 1) / WHC;
-      const dim3 gwin((unsigned)(n * host_div_up(a.Wo, 8) * host_div_up(a.Ho, 8)), (unsigned)(dg * nsl));
+      const dim3 gwin((unsigned)(n * host_div_up(a.Wo, 8) * host_div_up(a.Ho, 8)), (unsigned)dg);
       if (det)
         hipLaunchKernelGGL(mdcn_bwd_data_win_kernel<1>, gwin, dim3(NT), smem3, st, a, xh, wt, grad_out,
                            grad_x, grad_offset, grad_mask, GP, WTP, gxi, scale, WR, WCw, R);
