@@ -1737,12 +1737,20 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_nhwc_kernel(MdcnArgs a, cons
 // corner block starts at each window position): bit-reproducible, but slower -- agg_s0 backward
 // 7.84 ms float / 8.20 ms fixed point: the owner loop is a chain of dependent LDS reads per window
 // position and tap.  It is in the git history (round 4).
+// FUSEW (float mode): the weight gradient of the tile rides along -- the sampled column values
+// (the forward's (w1 v1 + w2 v2 + w3 v3 + w4 v4) * mask, from the corner quads the offset / mask
+// partials load anyway) go to LDS, one 16x16x4 f32 MFMA run per (tap, slice) forms the tile's
+// [64 co][16 c] product with the staged gOut tile, and it is added with float atomics into a
+// [K][Co][C] accumulator (64-byte segments; transposed into grad_weight afterwards).  The
+// deterministic mode keeps mdcn_bwd_weight_kernel: the same partials as int64 fixed-point atomics
+// (8-byte adds) took agg_s0 from 3.60 to 3.96 ms.  This
+// replaces mdcn_bwd_weight_kernel, whose 18 chunks each re-read gOut and re-gathered the corners.
 // dynamic LDS: sG [Co][GP], sWt [16][WTP], sCg [16][CP], sS [PT][16], sP [3][9][PT],
-// window [WR*WC][16] int64
+// [FUSEW: sCol [16][CP]], window [WR*WC][16] int64
 constexpr int WHC = 16;  // channels per window slice
 constexpr int WKMAX = 9; // taps the sP partial buffer holds
 constexpr int WCOMAX = 64;  // output channels (the W^T slice is prefetched in registers)
-template <int DET>
+template <int DET, int FUSEW = 0>
 __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, const float *__restrict__ xh,
                                                                const float *__restrict__ wT,
                                                                const float *__restrict__ gout,
@@ -1751,7 +1759,8 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
                                                                float *__restrict__ gmask, int GP,
                                                                int WTP, long long *__restrict__ gxi,
                                                                const double *__restrict__ det_scale,
-                                                               int WR, int WCc, int R) {
+                                                               int WR, int WCc, int R,
+                                                               float *__restrict__ gwT = nullptr) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int Co = a.Co;
   float *sG = sm;                       // [Co][GP]      gOut tile
@@ -1759,7 +1768,8 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
   float *sCg = sWt + WHC * WTP;         // [16][CP]      colg slice
   float *sS = sCg + WHC * CP;           // [PT][16]      per-pixel corners, weights, mask, window pos
   float *sP = sS + PT * 16;             // [3][WKMAX][PT] first slice's grad_offset / mask sums
-  long long *sAcc = reinterpret_cast<long long *>(sP + 3 * WKMAX * PT);  // [WR*WC][16]
+  float *sCol = sP + 3 * WKMAX * PT;    // [16][CP]      sampled columns (FUSEW)
+  long long *sAcc = reinterpret_cast<long long *>(sCol + (FUSEW ? WHC * CP : 0));  // [WR*WC][16]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long P = (long)a.Ho * a.Wo;
   const int ttx = (a.Wo + 7) / 8, tpi = ttx * ((a.Ho + 7) / 8);
@@ -1866,7 +1876,33 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) sCg[(4 * kr + r) * CP + 16 * wave + jj] = cacc[r];
+      if constexpr (FUSEW) {
+#pragma clang fp contract(off)
+        // the forward's sampled value (samp_val order) times the mask; zeros past the slice
+        const f32x4 wq = *reinterpret_cast<const f32x4 *>(qq + 4);
+        const float mq = qq[8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          sCol[(4 * q + u) * CP + qpx] = (wq[0] * v1[u] + wq[1] * v2[u] + wq[2] * v3[u] + wq[3] * v4[u]) * mq;
+      }
       __syncthreads();
+      if constexpr (FUSEW) {
+        // this tile's weight-gradient block: wave w = output channels 16w..16w+15, the slice's 16
+        // channels, K = the tile's 64 pixels; one float atomic per element into gwT[k][co][c]
+        f32x4 wacc = {0.f, 0.f, 0.f, 0.f};
+        for (int ks = 0; ks < PT / 4; ++ks) {
+          const float av = sG[(16 * wave + jj) * GP + 4 * ks + kr];
+          const float bv = sCol[jj * CP + 4 * ks + kr];
+          wacc = mfma16x16x4(av, bv, wacc);
+        }
+        if (jj < rows) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int co = 16 * wave + 4 * kr + r;
+            if (co < Co) atomicAdd(gwT + ((long)k * Co + co) * C + cb0 + jj, wacc[r]);
+          }
+        }
+      }
       float gm = 0.f, goh = 0.f, gow = 0.f;
       if (qon) {
 #pragma clang fp contract(off)
@@ -1965,6 +2001,16 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
       else
         atomicAdd(gx + o, (float)((double)v * inv));
     }
+  }
+}
+
+// grad_weight [Co][C][K] += gwT [K][Co][C] (the fused window form's accumulator)
+__global__ __launch_bounds__(256) void gw_kcoc_add_kernel(const float *__restrict__ gwT,
+                                                          float *__restrict__ gw, int Co, int C, int K) {
+  const long nw = (long)Co * C * K;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < nw; e += (long)gridDim.x * 256) {
+    const int k = (int)(e % K), c = (int)((e / K) % C), co = (int)(e / ((long)K * C));
+    gw[e] += gwT[((long)k * Co + co) * C + c];
   }
 }
 
@@ -2938,7 +2984,7 @@ BwdPlan bwd_plan(const MdcnArgs &a) {
 
 // Deterministic-backward workspace: [grad_x as int64][weight partials][bounds, scale]
 struct DetLayout {
-  size_t gxi, part, bounds, scale, xh, wt, total;
+  size_t gxi, part, bounds, scale, xh, wt, gw, total;
 };
 
 DetLayout det_layout(const MdcnArgs &a, const BwdPlan &pl) {
@@ -2968,7 +3014,8 @@ DetLayout ws_layout(const MdcnArgs &a) {
   L.wt = up(L.xh + nx * 4);
   L.bounds = up(L.wt + nw * 4);
   L.scale = L.bounds + 16;
-  L.total = up(L.scale + 8);
+  L.gw = up(L.scale + 8);  // [K][Co][C] weight-gradient accumulator of the fused window form
+  L.total = up(L.gw + nw * 4);
   return L;
 }
 
@@ -3011,8 +3058,9 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
   // AUTO takes it in both modes; GLOBAL / WINDOW force one form (tests, A/B).
   const int cpg = c / dg, R = 2;
   const int WR = 8 + (kh - 1) * dil + 2 * R, WCw = 8 + (kw - 1) * dil + 2 * R;
+  const bool fusew = !det;  // float mode: the weight gradient rides in the window kernel
   const size_t smem3 = sizeof(float) * ((size_t)co * GP + (size_t)WHC * WTP + (size_t)WHC * CP + (size_t)PT * 16 +
-                                       (size_t)3 * WKMAX * PT) +
+                                       (size_t)3 * WKMAX * PT + (fusew ? (size_t)WHC * CP : 0)) +
                        (size_t)WR * WCw * WHC * 8;
   const bool win_ok = nr && stride == 1 && cpg <= 2 * WHC && K <= WKMAX && co <= WCOMAX && smem3 <= 160 * 1024;
   if (algo == AANET_DCN_BWD_WINDOW && !win_ok) return AANET_EUNSUPPORTED;
@@ -3059,9 +3107,9 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_nhwc_kernel<1>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_win_kernel<0>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_win_kernel<1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_win_kernel<0, 1>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
@@ -3084,13 +3132,20 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
 #endif
     if (use_win) {
       const dim3 gwin((unsigned)(n * host_div_up(a.Wo, 8) * host_div_up(a.Ho, 8)), (unsigned)dg);
-      if (det)
+      if (det) {
         hipLaunchKernelGGL(mdcn_bwd_data_win_kernel<1>, gwin, dim3(NT), smem3, st, a, xh, wt, grad_out,
                            grad_x, grad_offset, grad_mask, GP, WTP, gxi, scale, WR, WCw, R);
-      else
-        hipLaunchKernelGGL(mdcn_bwd_data_win_kernel<0>, gwin, dim3(NT), smem3, st, a, xh, wt, grad_out,
+      } else {
+        float *gwT = reinterpret_cast<float *>(wb + L.gw);
+        const long nw = (long)co * c * K;
+        e = hipMemsetAsync(gwT, 0, sizeof(float) * (size_t)nw, st);
+        if (e != hipSuccess) return (int)e;
+        hipLaunchKernelGGL((mdcn_bwd_data_win_kernel<0, 1>), gwin, dim3(NT), smem3, st, a, xh, wt, grad_out,
                            reinterpret_cast<float *>(wb + L.gxi), grad_offset, grad_mask, GP, WTP,
-                           nullptr, scale, WR, WCw, R);
+                           nullptr, scale, WR, WCw, R, gwT);
+        hipLaunchKernelGGL(gw_kcoc_add_kernel, dim3(host_div_up(nw, 256) > 1024 ? 1024 : host_div_up(nw, 256)),
+                           dim3(256), 0, st, gwT, grad_weight, co, c, K);
+      }
     } else if (det)
       hipLaunchKernelGGL(mdcn_bwd_data_nhwc_kernel<1>, gdata, dim3(NT), smem2, st, a, xh, wt, grad_out,
                          grad_x, grad_offset, grad_mask, GP, WTP, gxi, scale);
@@ -3121,7 +3176,9 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
     if (rc) return rc;
   }
   const dim3 gw3(pl.nchunks, (unsigned)pl.nsplit, host_div_up(co, 64));
-  if (nr && det)
+  if (use_win && fusew)
+    ;  // the window kernel added the weight gradient
+  else if (nr && det)
     hipLaunchKernelGGL((mdcn_bwd_weight_kernel<1, 1>), gw3, dim3(NT), 0, st, a, grad_out, grad_weight,
                        pl.npieces, pl.range, part, xh);
   else if (nr)

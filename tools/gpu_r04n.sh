@@ -14,4 +14,14 @@ for l in open('gpurun_out/r04n_sweep.jsonl'):
     d=json.loads(l)
     if 'shape' in d: print(d['shape'], 'fwd %.0f bwd %.0f det %.0f global %.0f us' % (d['fwd_us'], d['bwd_us'], d['bwd_det_us'], d['bwd_global_atomic_us']))
 "
+
+if [ -n "${TRAIN:-}" ]; then
+  timeout -k 10 300 python bench.py --train --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/r04n_train.json 2>gpurun_out/r04n_train.err || exit 13
+  timeout -k 10 300 python bench.py --train --deterministic --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/r04n_train_det.json 2>gpurun_out/r04n_train_det.err || exit 14
+  python -c "
+import json
+for f in ('gpurun_out/r04n_train.json', 'gpurun_out/r04n_train_det.json'):
+    d = json.loads(open(f).read().strip().splitlines()[-1]); print(f, round(d['ms_per_step'], 3), 'ms', round(d['value'], 1), 'pairs/s')
+"
+fi
 exit $rc

@@ -5,7 +5,7 @@ set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 mkdir -p gpurun_out
-for D in 0 1 2; do
+for D in 0 1 2; do :;
   AANET_MI355X_LIB=aanet_amd/libaanet_mi355x_dbg.so AANET_DCN_BWD_DBG=$D timeout -k 10 200 python bench.py --dcn-sweep --dcn-shapes agg_s0 --kernel-iters 10 > gpurun_out/r04o_$D.jsonl 2>/dev/null || exit 7
   python -c "
 import json
