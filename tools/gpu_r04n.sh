@@ -5,7 +5,7 @@ set -u
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 400 python -u -m pytest tests/test_gpu_mdcn.py tests/test_gpu_train.py -m gpu -q -rf --timeout 120 --timeout-method thread > gpurun_out/r04n_tests.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_mdcn.py tests/test_gpu_train.py tests/test_gpu_engine_conv.py -m gpu -q -rf --timeout 120 --timeout-method thread > gpurun_out/r04n_tests.log 2>&1
 rc=$?; tail -6 gpurun_out/r04n_tests.log; [ $rc -le 1 ] || exit $rc
 timeout -k 10 200 python bench.py --dcn-sweep --kernel-iters 10 > gpurun_out/r04n_sweep.jsonl 2> gpurun_out/r04n_sweep.err || exit 7
 python -c "
