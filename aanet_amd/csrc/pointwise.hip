@@ -254,6 +254,108 @@ __global__ __launch_bounds__(256) void pw_conv_nchw_kernel(PwArgs a) {
   }
 }
 
+// NCHW input, split once (CI = 64, CB = 2 or 4: 64-pixel blocks).  pw_conv_nchw_kernel splits every
+// staged value in each of the CB * SUB = 4 waves that read it (3,494 VALU per wave at C2 conv1,
+// 4x the needed split work).  Here the staging thread splits its values once and stores the three
+// bf16 pieces as [piece][pixel][channel] planes (128-byte pixel rows at CI = 64), 16-byte chunk q
+// of pixel px at chunk q ^ (px & (NQ - 1)): the staging writes (8 lanes = 8 pixels of one
+// chunk) and the fragment reads (16 lanes = 16 pixels, lane groups kr and kr + 1) are both
+// conflict-free.  A lane's B fragment is then three ds_read_b128.  Staging: thread = (pixel
+// t % 64, 8-channel groups (t / 64) + 4i), eight dword loads per group (lanes = consecutive
+// pixels: 256-byte wave loads), next block's loads in flight during the current block's MFMAs.
+// Measured at C2 scale 0 (64 -> 64, same call): 43.8-44.2 vs 40.3-41.3 us alone (48 KB of LDS:
+// three workgroups per CU instead of four, 4x the load instructions), but the bench step
+// 3.369-3.387 vs 3.385-3.407 ms -- its VALU no longer competes with the concurrent kernels.
+template <int CI, int CB, int ONH>
+__global__ __launch_bounds__(256) void pw_conv_nchw_s_kernel(PwArgs a) {
+  constexpr int NCC = CI / 32;
+  constexpr int BP = 64;                    // pixels per block
+  constexpr int SUB = 4 / CB, SW = BP / SUB;  // pixel sub-blocks per block, pixels per sub-block
+  constexpr int NQ = CI / 8;                // 16-byte chunks (8 channels) per pixel row
+  constexpr int GPT = NQ / 4;               // 8-channel groups per staging thread
+  constexpr int PL = BP * CI;               // bf16 per piece plane
+  __shared__ __attribute__((aligned(16))) __bf16 sB[2][3 * PL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int jj = lane & 15, kr = lane >> 4;
+  const int cb = wave % CB, sub = wave / CB;
+  const int T = a.N * a.P, P = a.P, Co = a.Co;
+  const int nblk = (T + BP - 1) / BP;
+  const int per = (nblk + gridDim.x - 1) / gridDim.x;
+  const int b0 = blockIdx.x * per, b1 = min(nblk, b0 + per);
+  if (b0 >= b1) return;  // workgroup-uniform
+
+  const bf16x8 *fr = static_cast<const bf16x8 *>(a.wsplit);
+  bf16x8 A[NCC][3];
+#pragma unroll
+  for (int cc = 0; cc < NCC; ++cc)
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) A[cc][pc] = fr[((cc * 4 + cb) * 3 + pc) * 64 + lane];
+  float eb[1][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int co = 16 * cb + 4 * kr + r;
+    eb[0][r] = (a.bias && co < Co) ? a.bias[co] : 0.f;
+  }
+
+  const int spx = tid & 63, sg = tid >> 6;  // staging: pixel, first 8-channel group
+  float rv[GPT][8];
+  auto load = [&](int b) {
+    const int t = b * BP + spx;
+    const bool ok = t < T;
+    const int n = ok ? t / P : 0, p = ok ? t - n * P : 0;
+    const float *src = a.x + (long)n * CI * P + p;
+#pragma unroll
+    for (int i = 0; i < GPT; ++i)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) rv[i][u] = ok ? src[(long)(8 * (sg + 4 * i) + u) * P] : 0.f;
+  };
+  auto swz = [](int px, int q) { return px * CI + ((q ^ (px & (NQ - 1))) << 3); };
+  auto stage = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < GPT; ++i) {
+      bf16x8 pcs[3];
+      split8(rv[i], pcs);
+      const int o = swz(spx, sg + 4 * i);
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc) *reinterpret_cast<bf16x8 *>(&sB[buf][pc * PL + o]) = pcs[pc];
+    }
+  };
+
+  load(b0);
+  stage(0);
+  __syncthreads();
+  for (int b = b0; b < b1; ++b) {
+    const int buf = (b - b0) & 1;
+    if (b + 1 < b1) load(b + 1);
+    const __bf16 *xs = sB[buf];
+    const int n0b = __builtin_amdgcn_readfirstlane((b * BP) / P), p0b = b * BP - n0b * P;
+#pragma unroll
+    for (int g = 0; g < SW / 16; ++g) {
+      const int px = SW * sub + 16 * g + jj;
+      f32x4 acc[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int cc = 0; cc < NCC; ++cc) {
+        bf16x8 B[3];
+        const int o = swz(px, 4 * cc + kr);
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) B[pc] = *reinterpret_cast<const bf16x8 *>(&xs[pc * PL + o]);
+        acc[0] = mfma_split6(A[cc], B, acc[0]);
+      }
+      const int off = SW * sub + 16 * g + jj;
+      int nn = n0b, pp = p0b + off;
+      while (pp >= P) {
+        pp -= P;
+        ++nn;
+      }
+      pw_store<1, ONH>(a, acc, eb, b * BP + off, cb, kr, nn, pp);
+    }
+    if (b + 1 < b1) {
+      stage(buf ^ 1);
+      __syncthreads();
+    }
+  }
+}
+
 template <int CI, int NB, int NCOH>
 void launch_nb(const PwArgs &a, dim3 grid, hipStream_t st) {
   const dim3 blk(256);
@@ -268,7 +370,12 @@ void launch_nb(const PwArgs &a, dim3 grid, hipStream_t st) {
     const long nblk = ((long)a.N * a.P + bp - 1) / bp;
     long g = (nblk + 3) / 4;  // about 4 blocks per workgroup at least
     if (g > 1024) g = 1024;
-    if (a.out_nhwc)
+    if (CB >= 2 && CI == 64) {  // (at CI = 32 the 64-byte pixel rows would conflict)
+      if (a.out_nhwc)
+        hipLaunchKernelGGL((pw_conv_nchw_s_kernel<CI, CB, 1>), dim3((unsigned)g), blk, 0, st, a);
+      else
+        hipLaunchKernelGGL((pw_conv_nchw_s_kernel<CI, CB, 0>), dim3((unsigned)g), blk, 0, st, a);
+    } else if (a.out_nhwc)
       hipLaunchKernelGGL((pw_conv_nchw_kernel<CI, CB, 1>), dim3((unsigned)g), blk, 0, st, a);
     else
       hipLaunchKernelGGL((pw_conv_nchw_kernel<CI, CB, 0>), dim3((unsigned)g), blk, 0, st, a);
