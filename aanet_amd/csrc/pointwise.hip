@@ -254,13 +254,12 @@ __global__ __launch_bounds__(256) void pw_conv_nchw_kernel(PwArgs a) {
   }
 }
 
-// NCHW input, split once (CI = 64, CB = 2 or 4: 64-pixel blocks).  pw_conv_nchw_kernel splits every
+// NCHW input, split once (CB = 2 or 4: 64-pixel blocks).  pw_conv_nchw_kernel splits every
 // staged value in each of the CB * SUB = 4 waves that read it (3,494 VALU per wave at C2 conv1,
 // 4x the needed split work).  Here the staging thread splits its values once and stores the three
-// bf16 pieces as [piece][pixel][channel] planes (128-byte pixel rows at CI = 64), 16-byte chunk q
-// of pixel px at chunk q ^ (px & (NQ - 1)): the staging writes (8 lanes = 8 pixels of one
-// chunk) and the fragment reads (16 lanes = 16 pixels, lane groups kr and kr + 1) are both
-// conflict-free.  A lane's B fragment is then three ds_read_b128.  Staging: thread = (pixel
+// bf16 pieces as [piece][pixel][channel] planes (CI * 2-byte pixel rows) with the 16-byte chunks
+// XOR-swizzled per pixel (swz below): the staging writes (8 lanes = 8 pixels of one chunk) and
+// the fragment reads (16 lanes = 16 pixels, lane groups kr and kr + 1) are both conflict-free.  A lane's B fragment is then three ds_read_b128.  Staging: thread = (pixel
 // t % 64, 8-channel groups (t / 64) + 4i), eight dword loads per group (lanes = consecutive
 // pixels: 256-byte wave loads), next block's loads in flight during the current block's MFMAs.
 // Measured at C2 scale 0 (64 -> 64, same call): 43.8-44.2 vs 40.3-41.3 us alone (48 KB of LDS:
@@ -309,7 +308,12 @@ __global__ __launch_bounds__(256) void pw_conv_nchw_s_kernel(PwArgs a) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) rv[i][u] = ok ? src[(long)(8 * (sg + 4 * i) + u) * P] : 0.f;
   };
-  auto swz = [](int px, int q) { return px * CI + ((q ^ (px & (NQ - 1))) << 3); };
+  // CI = 64: chunk q ^ (px & 7); CI = 32 (64-byte rows): q ^ ((px + (px >> 1)) & 3) -- both
+  // conflict-free for the staging writes and the fragment reads (checked per lane group)
+  auto swz = [](int px, int q) {
+    const int x = CI == 64 ? (px & 7) : (((px & 3) + ((px >> 1) & 3)) & 3);
+    return px * CI + ((q ^ x) << 3);
+  };
   auto stage = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < GPT; ++i) {
@@ -370,7 +374,7 @@ void launch_nb(const PwArgs &a, dim3 grid, hipStream_t st) {
     const long nblk = ((long)a.N * a.P + bp - 1) / bp;
     long g = (nblk + 3) / 4;  // about 4 blocks per workgroup at least
     if (g > 1024) g = 1024;
-    if (CB >= 2 && CI == 64) {  // (at CI = 32 the 64-byte pixel rows would conflict)
+    if (CB >= 2) {
       if (a.out_nhwc)
         hipLaunchKernelGGL((pw_conv_nchw_s_kernel<CI, CB, 1>), dim3((unsigned)g), blk, 0, st, a);
       else
