@@ -2,7 +2,9 @@
 aanet_conv2d_fused_f32 takes for split-bf16 1x1 convs with 32/64 input channels: against an fp64
 reference, held to the exact-f32 engine's error (as tests/test_gpu_split.py holds the engine),
 over both layouts on each side, bias / folded-BN / residual / activation epilogues, output widths
-1..64 and pixel counts that are not a multiple of the 16-pixel block (blocks spanning images)."""
+1..64 and pixel counts that are not a multiple of the 16-pixel block (blocks spanning images).
+NCHW input with 2 or 4 output-channel blocks takes the split-once kernel (pw_conv_nchw_s_kernel),
+with 1 block the per-wave-split one: both are covered."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -23,6 +25,8 @@ CASES = [
     (1, 64, 9, 13, 54, True, False, True, False, False, None),      # Co = 54 (partial block)
     (2, 32, 3, 5, 1, False, False, True, False, False, None),       # Co = 1
     (1, 64, 128, 416, 64, False, True, True, False, False, "relu"),  # C2 scale-0 conv1, one image
+    (2, 64, 13, 27, 24, False, False, True, True, False, "leaky"),  # NCHW, 2 co blocks (split once)
+    (1, 32, 11, 30, 32, False, True, True, False, True, "relu"),     # NCHW, 32 ch, 2 co blocks
 ]
 
 
