@@ -1748,6 +1748,10 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_nhwc_kernel(MdcnArgs a, cons
 // dynamic LDS: sG [Co][GP], sWt [16][WTP], sCg [16][CP], sS [PT][16], sP [3][9][PT],
 // [FUSEW: sCol [16][CP]], window [WR*WC][16] int64
 constexpr int WHC = 16;  // channels per window slice
+// row pitch of the colg / column tiles of the window kernel: 66 (= 2 mod 32) makes the partials'
+// (rows 4q+u, lanes q), the scatter's and the fused weight gradient's (rows = lane % 16) reads
+// conflict-free; the engine's CP = 80 left them 4- to 8-way conflicted
+constexpr int WCP = PT + 2;
 constexpr int WKMAX = 9; // taps the sP partial buffer holds
 constexpr int WCOMAX = 64;  // output channels (the W^T slice is prefetched in registers)
 template <int DET, int FUSEW = 0>
@@ -1765,11 +1769,11 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
   const int Co = a.Co;
   float *sG = sm;                       // [Co][GP]      gOut tile
   float *sWt = sG + Co * GP;            // [16][WTP]     W^T slice
-  float *sCg = sWt + WHC * WTP;         // [16][CP]      colg slice
-  float *sS = sCg + WHC * CP;           // [PT][16]      per-pixel corners, weights, mask, window pos
+  float *sCg = sWt + WHC * WTP;         // [16][WCP]      colg slice
+  float *sS = sCg + WHC * WCP;           // [PT][16]      per-pixel corners, weights, mask, window pos
   float *sP = sS + PT * 16;             // [3][WKMAX][PT] first slice's grad_offset / mask sums
-  float *sCol = sP + 3 * WKMAX * PT;    // [16][CP]      sampled columns (FUSEW)
-  long long *sAcc = reinterpret_cast<long long *>(sCol + (FUSEW ? WHC * CP : 0));  // [WR*WC][16]
+  float *sCol = sP + 3 * WKMAX * PT;    // [16][WCP]      sampled columns (FUSEW)
+  long long *sAcc = reinterpret_cast<long long *>(sCol + (FUSEW ? WHC * WCP : 0));  // [WR*WC][16]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long P = (long)a.Ho * a.Wo;
   const int ttx = (a.Wo + 7) / 8, tpi = ttx * ((a.Ho + 7) / 8);
@@ -1875,7 +1879,7 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
         cacc = mfma16x16x4(av, bv, cacc);
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sCg[(4 * kr + r) * CP + 16 * wave + jj] = cacc[r];
+      for (int r = 0; r < 4; ++r) sCg[(4 * kr + r) * WCP + 16 * wave + jj] = cacc[r];
       if constexpr (FUSEW) {
 #pragma clang fp contract(off)
         // the forward's sampled value (samp_val order) times the mask; zeros past the slice
@@ -1883,7 +1887,7 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
         const float mq = qq[8];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          sCol[(4 * q + u) * CP + qpx] = (wq[0] * v1[u] + wq[1] * v2[u] + wq[2] * v3[u] + wq[3] * v4[u]) * mq;
+          sCol[(4 * q + u) * WCP + qpx] = (wq[0] * v1[u] + wq[1] * v2[u] + wq[2] * v3[u] + wq[3] * v4[u]) * mq;
       }
       __syncthreads();
       if constexpr (FUSEW) {
@@ -1892,7 +1896,7 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
         f32x4 wacc = {0.f, 0.f, 0.f, 0.f};
         for (int ks = 0; ks < PT / 4; ++ks) {
           const float av = sG[(16 * wave + jj) * GP + 4 * ks + kr];
-          const float bv = sCol[jj * CP + 4 * ks + kr];
+          const float bv = sCol[jj * WCP + 4 * ks + kr];
           wacc = mfma16x16x4(av, bv, wacc);
         }
         if (jj < rows) {
@@ -1910,7 +1914,7 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
         const float hh = 1.f - lh, hw = 1.f - lw;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const float cg = sCg[(4 * q + u) * CP + qpx];
+          const float cg = sCg[(4 * q + u) * WCP + qpx];
           const float val = hh * hw * v1[u] + hh * lw * v2[u] + lh * hw * v3[u] + lh * lw * v4[u];
           gm += cg * val;
           const float wh = -hw * v1[u] - lw * v2[u] + hw * v3[u] + lw * v4[u];
@@ -1931,7 +1935,7 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
           const float *qp = sS + px * 16;
           const f32x4 pi = *reinterpret_cast<const f32x4 *>(qp);
           const f32x4 qw = *reinterpret_cast<const f32x4 *>(qp + 4);
-          const float top = sCg[cl * CP + px] * qp[8];
+          const float top = sCg[cl * WCP + px] * qp[8];
           const float pi0 = pi[0], pi1 = pi[1], pi2 = pi[2], pi3 = pi[3], q12 = qp[12];
           const int j1 = __builtin_bit_cast(int, pi0), j2 = __builtin_bit_cast(int, pi1);
           const int j3 = __builtin_bit_cast(int, pi2), j4 = __builtin_bit_cast(int, pi3);
@@ -3059,8 +3063,12 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
   const int cpg = c / dg, R = 2;
   const int WR = 8 + (kh - 1) * dil + 2 * R, WCw = 8 + (kw - 1) * dil + 2 * R;
   const bool fusew = !det;  // float mode: the weight gradient rides in the window kernel
-  const size_t smem3 = sizeof(float) * ((size_t)co * GP + (size_t)WHC * WTP + (size_t)WHC * CP + (size_t)PT * 16 +
-                                       (size_t)3 * WKMAX * PT + (fusew ? (size_t)WHC * CP : 0)) +
+  // gOut tile pitch of the window kernel: 80 (= 16 mod 32) keeps the colg reads (rows kr,
+  // columns jj) conflict-free; the fused weight gradient also reads it transposed (rows jj), which
+  // that pitch makes 8-way conflicted, so the fused form uses 66 (2-way for both)
+  const int GPW = fusew ? round_pitch(PT, 2) : GP;
+  const size_t smem3 = sizeof(float) * ((size_t)co * GPW + (size_t)WHC * WTP + (size_t)WHC * WCP + (size_t)PT * 16 +
+                                       (size_t)3 * WKMAX * PT + (fusew ? (size_t)WHC * WCP : 0)) +
                        (size_t)WR * WCw * WHC * 8;
   const bool win_ok = nr && stride == 1 && cpg <= 2 * WHC && K <= WKMAX && co <= WCOMAX && smem3 <= 160 * 1024;
   if (algo == AANET_DCN_BWD_WINDOW && !win_ok) return AANET_EUNSUPPORTED;
@@ -3141,7 +3149,7 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
         e = hipMemsetAsync(gwT, 0, sizeof(float) * (size_t)nw, st);
         if (e != hipSuccess) return (int)e;
         hipLaunchKernelGGL((mdcn_bwd_data_win_kernel<0, 1>), gwin, dim3(NT), smem3, st, a, xh, wt, grad_out,
-                           reinterpret_cast<float *>(wb + L.gxi), grad_offset, grad_mask, GP, WTP,
+                           reinterpret_cast<float *>(wb + L.gxi), grad_offset, grad_mask, GPW, WTP,
                            nullptr, scale, WR, WCw, R, gwT);
         hipLaunchKernelGGL(gw_kcoc_add_kernel, dim3(host_div_up(nw, 256) > 1024 ? 1024 : host_div_up(nw, 256)),
                            dim3(256), 0, st, gwT, grad_weight, co, c, K);
