@@ -1903,7 +1903,11 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int co = 16 * wave + 4 * kr + r;
-            if (co < Co) atomicAdd(gwT + ((long)k * Co + co) * C + cb0 + jj, wacc[r]);
+            if (co >= Co) continue;
+            if (DET)  // this tile's partial, stored: part[tile][g][k][co][c of the group]
+              gwT[((((long)blockIdx.x * a.dg + g) * K + k) * Co + co) * cpg + sl * WHC + jj] = wacc[r];
+            else
+              atomicAdd(gwT + ((long)k * Co + co) * C + cb0 + jj, wacc[r]);
           }
         }
       }
@@ -2006,6 +2010,42 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
         atomicAdd(gx + o, (float)((double)v * inv));
     }
   }
+}
+
+// Deterministic weight gradient of the fused window form, stage 1: part2[j][e] = sum over the
+// tiles t of chunk j (ascending) of part[t][e], e = [g][k][co][c of the group]; 8 loads in flight.
+__global__ __launch_bounds__(256) void det_tile_sum_kernel(const float *__restrict__ part,
+                                                           float *__restrict__ part2, long nt,
+                                                           long nw, long per) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  const long j = blockIdx.y, t0 = j * per, t1 = min(nt, t0 + per);
+  if (e >= nw) return;
+  float s = 0.f;
+  long t = t0;
+  for (; t + 8 <= t1; t += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(t + u) * nw + e];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; t < t1; ++t) s += part[t * nw + e];
+  part2[j * nw + e] = s;
+}
+
+// stage 2: grad_weight[co][g cpg + c][k] += sum over the chunks j (ascending) of part2[j][e]
+__global__ __launch_bounds__(256) void det_tile_final_kernel(const float *__restrict__ part2,
+                                                             float *__restrict__ gw, int nch, int Co,
+                                                             int C, int K, int dg) {
+  const long nw = (long)Co * C * K;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= nw) return;
+  const int cpg = C / dg;
+  const int c = (int)(e % cpg), co = (int)((e / cpg) % Co), k = (int)((e / ((long)cpg * Co)) % K),
+            g = (int)(e / ((long)cpg * Co * K));
+  float s = 0.f;
+  for (int j = 0; j < nch; ++j) s += part2[(long)j * nw + e];
+  gw[((long)co * C + g * cpg + c) * K + k] += s;
 }
 
 // grad_weight [Co][C][K] += gwT [K][Co][C] (the fused window form's accumulator)
@@ -2988,8 +3028,24 @@ BwdPlan bwd_plan(const MdcnArgs &a) {
 
 // Deterministic-backward workspace: [grad_x as int64][weight partials][bounds, scale]
 struct DetLayout {
-  size_t gxi, part, bounds, scale, xh, wt, gw, total;
+  size_t gxi, part, bounds, scale, xh, wt, gw, wp, wp2, total;
 };
+
+bool bwd_nhwc_reads(const MdcnArgs &a);
+constexpr int DET_TILE_CHUNKS = 64;  // chunks of the first stage of the tile-partial reduction
+// the window form's LDS (mdcn_bwd_impl), fused weight gradient, and whether a shape takes it
+size_t win_smem(const MdcnArgs &a) {
+  const int GPW = round_pitch(PT, 2), WTP = round_pitch(a.Co, 2);
+  const int WR = 8 + (a.kh - 1) * a.dil + 4, WCw = 8 + (a.kw - 1) * a.dil + 4;
+  return sizeof(float) * ((size_t)a.Co * GPW + (size_t)WHC * WTP + (size_t)WHC * WCP + (size_t)PT * 16 +
+                          (size_t)3 * WKMAX * PT + (size_t)WHC * WCP) +
+         (size_t)WR * WCw * WHC * 8;
+}
+bool win_shape_ok(const MdcnArgs &a) {
+  return bwd_nhwc_reads(a) && a.stride == 1 && a.C / a.dg <= 2 * WHC && a.kh * a.kw <= WKMAX &&
+         a.Co <= WCOMAX && win_smem(a) <= 160 * 1024;
+}
+long win_tiles(const MdcnArgs &a) { return (long)a.N * ((a.Ho + 7) / 8) * ((a.Wo + 7) / 8); }
 
 DetLayout det_layout(const MdcnArgs &a, const BwdPlan &pl) {
   auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
@@ -3003,6 +3059,11 @@ DetLayout det_layout(const MdcnArgs &a, const BwdPlan &pl) {
   L.xh = up(L.scale + 8);  // channels-last x and wT[k][c][co] (mdcn_bwd_data_nhwc_kernel)
   L.wt = up(L.xh + nx * 4);
   L.total = up(L.wt + nw * 4);
+  if (win_shape_ok(a)) {  // the fused window form's per-tile weight-gradient partials
+    L.wp = L.total;
+    L.wp2 = up(L.wp + (size_t)win_tiles(a) * nw * 4);
+    L.total = up(L.wp2 + (size_t)DET_TILE_CHUNKS * nw * 4);
+  }
   return L;
 }
 
@@ -3062,7 +3123,7 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
   // AUTO takes it in both modes; GLOBAL / WINDOW force one form (tests, A/B).
   const int cpg = c / dg, R = 2;
   const int WR = 8 + (kh - 1) * dil + 2 * R, WCw = 8 + (kw - 1) * dil + 2 * R;
-  const bool fusew = !det;  // float mode: the weight gradient rides in the window kernel
+  const bool fusew = true;  // the weight gradient rides in the window kernel (both modes)
   // gOut tile pitch of the window kernel: 80 (= 16 mod 32) keeps the colg reads (rows kr,
   // columns jj) conflict-free; the fused weight gradient also reads it transposed (rows jj), which
   // that pitch makes 8-way conflicted, so the fused form uses 66 (2-way for both)
@@ -3070,7 +3131,7 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
   const size_t smem3 = sizeof(float) * ((size_t)co * GPW + (size_t)WHC * WTP + (size_t)WHC * WCP + (size_t)PT * 16 +
                                        (size_t)3 * WKMAX * PT + (fusew ? (size_t)WHC * WCP : 0)) +
                        (size_t)WR * WCw * WHC * 8;
-  const bool win_ok = nr && stride == 1 && cpg <= 2 * WHC && K <= WKMAX && co <= WCOMAX && smem3 <= 160 * 1024;
+  const bool win_ok = nr && win_shape_ok(a) && smem3 <= 160 * 1024;
   if (algo == AANET_DCN_BWD_WINDOW && !win_ok) return AANET_EUNSUPPORTED;
   const bool use_win = win_ok && (algo == AANET_DCN_BWD_WINDOW || algo == AANET_DCN_BWD_AUTO);
   float *xh = nhs ? reinterpret_cast<float *>(wb + L.xh) : nullptr;
@@ -3115,7 +3176,7 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_nhwc_kernel<1>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_win_kernel<1>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_win_kernel<1, 1>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&mdcn_bwd_data_win_kernel<0, 1>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -3141,8 +3202,15 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
     if (use_win) {
       const dim3 gwin((unsigned)(n * host_div_up(a.Wo, 8) * host_div_up(a.Ho, 8)), (unsigned)dg);
       if (det) {
-        hipLaunchKernelGGL(mdcn_bwd_data_win_kernel<1>, gwin, dim3(NT), smem3, st, a, xh, wt, grad_out,
-                           grad_x, grad_offset, grad_mask, GP, WTP, gxi, scale, WR, WCw, R);
+        float *wp = reinterpret_cast<float *>(wb + L.wp), *wp2 = reinterpret_cast<float *>(wb + L.wp2);
+        const long nw = (long)co * c * K, nt = win_tiles(a);
+        hipLaunchKernelGGL((mdcn_bwd_data_win_kernel<1, 1>), gwin, dim3(NT), smem3, st, a, xh, wt, grad_out,
+                           grad_x, grad_offset, grad_mask, GPW, WTP, gxi, scale, WR, WCw, R, wp);
+        const long per = (nt + DET_TILE_CHUNKS - 1) / DET_TILE_CHUNKS;
+        hipLaunchKernelGGL(det_tile_sum_kernel, dim3((unsigned)host_div_up(nw, 256), DET_TILE_CHUNKS), dim3(256), 0,
+                           st, wp, wp2, nt, nw, per);
+        hipLaunchKernelGGL(det_tile_final_kernel, dim3((unsigned)host_div_up(nw, 256)), dim3(256), 0, st, wp2,
+                           grad_weight, DET_TILE_CHUNKS, co, c, K, dg);
       } else {
         float *gwT = reinterpret_cast<float *>(wb + L.gw);
         const long nw = (long)co * c * K;
@@ -3200,7 +3268,7 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
                        pl.npieces, pl.range, nullptr);
   rc = aanet_launch_status();
   if (rc) return rc;
-  if (det) {
+  if (det && !(use_win && fusew)) {
     const long nw = (long)co * c * K;
     hipLaunchKernelGGL(det_weight_reduce_kernel, dim3(host_div_up(nw, 64)), dim3(256), 0, st,
                        part, grad_weight, nw, pl.nsplit);
