@@ -18,8 +18,8 @@ os.makedirs(dst, exist_ok=True)
 # bench.py kernel_rooflines keys -> kernel names
 KMAP = {"corr_volume_s0": r"corr_reg_kernel<5, 8, 2>", "disp_regress_s0": r"disp_regress_fixed_kernel<64>",
         "corr_pyramid": r"corr_pyramid_reg_kernel",
-        # the streaming 1x1 conv (pointwise.hip), NCHW input, 4 output-channel blocks, NHWC out
-        "conv1x1_s0": r"pw_conv_nchw_kernel<64, 4, 1>",
+        # the streaming 1x1 conv (pointwise.hip, input split once), NCHW input, 4 output-channel blocks, NHWC out
+        "conv1x1_s0": r"pw_conv_nchw_s_kernel<64, 4, 1>",
         # the LDS-window deformable tail (dcn_tile.hip), common form (no post stage)
         "mdcn_pw_s0": r"dcn_tile_kernel<2, 32, false>",
         # MODE, CO_T, PTT, PACKED, TAIL, SCHED, FULL, LAYOUT, CFG, PREC (1: split-bf16), HALO (= dil),
