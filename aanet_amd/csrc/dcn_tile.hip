@@ -150,6 +150,11 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kr = lane >> 4, jj = lane & 15;
   const int H = a.H, W = a.W, C = a.C;
+#ifdef AANET_DEBUG_SWITCHES
+  const int dbg = a.dbg;  // timing-attribution switches (debug build only)
+#else
+  constexpr int dbg = 0;  // product build: every switch branch folds away at compile time
+#endif
   const int tx = (W + TC - 1) / TC, ntiles = tx * ((H + TR - 1) / TR);
   // XCD-aware bijective remap: each XCD walks a contiguous range of tiles (shared window rows)
   const int nwg = gridDim.x, b0 = blockIdx.x;
@@ -179,7 +184,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       const int wy = wy0 + pos / WC, wx = wx0 + pos % WC;
       const bool ok = pos < WR * WC && wy >= 0 && wy < H && wx >= 0 && wx < W;
       const int off = ok ? ((wy * W + wx) * C + 4 * q) * 4 : img_bytes;
-      if (!(a.dbg & 32)) wv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, g * 128, 0));
+      if (!(dbg & 32)) wv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, g * 128, 0));
     }
   };
   auto store_window = [&]() {
@@ -194,7 +199,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   const char *wsp = reinterpret_cast<const char *>(a.wsplit);
   const int ncc = C / 32;
   auto issue_a = [&](int c, char *dst) {
-    if (a.dbg & 64) return;
+    if (dbg & 64) return;
     const int g = c / K, k = c - K * (c / K);
     const char *src = wsp + (long)((k * ncc + g) * 12) * 1024 + lane * 16;
     for (int pc = wave; pc < 3 * NCO; pc += 8)
@@ -243,7 +248,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   // one chunk (tap of a 32-channel K slice): corners -> blend -> split -> 6 NCO MFMAs
   auto tap = [&](int g, int k, const char *sAc, const TapState &s, bool reload) {
     f32x4 cq[4][2];  // corners TL, TR, BL, BR x channel quads 2kr, 2kr+1
-    const int lpos = (s.pos < 0 || (a.dbg & 2)) ? 0 : s.pos;
+    const int lpos = (s.pos < 0 || (dbg & 2)) ? 0 : s.pos;
     const char *base = sWin + (lpos + kr * 2 * NPOS) * 16;
 #pragma unroll
     for (int h2 = 0; h2 < 2; ++h2) {
@@ -263,7 +268,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
         t = __builtin_fmaf(cq[3][h2][u], s.w3, t);
         v[4 * h2 + u] = t;
       }
-    if (!(a.dbg & 4) && __builtin_amdgcn_ballot_w64(s.pos < 0)) {  // wave-uniform: some sample left the window
+    if (!(dbg & 4) && __builtin_amdgcn_ballot_w64(s.pos < 0)) {  // wave-uniform: some sample left the window
       if (s.pos < 0) {
         // global gather of this lane's corners (blended here, so no load is pending at the join)
 #pragma clang fp contract(off)
@@ -315,7 +320,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       bf16x8 A[3];
 #pragma unroll
       for (int pc = 0; pc < 3; ++pc) A[pc] = *reinterpret_cast<const bf16x8 *>(ab + (m * 3 + pc) * 1024);
-      if (!(a.dbg & 1)) acc[m] = mfma_split6(A, B, acc[m]);
+      if (!(dbg & 1)) acc[m] = mfma_split6(A, B, acc[m]);
     }
   };
 
@@ -356,7 +361,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
     }
     tap(g, k, cur, s, NPH == 2 && c == K - 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of A(c+1) landed ...
-    if (!(a.dbg & 8)) __syncthreads();                 // ... and every other wave's
+    if (!(dbg & 8)) __syncthreads();                 // ... and every other wave's
   };
   load_window(0);
   issue_a(0, sA0);
@@ -377,7 +382,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   float eb[EPT];
   long eo[EPT];
   bool eok[EPT];
-  const bool res = a.residual && !(a.dbg & 16), csa = a.csa_out && !(a.dbg & 16);
+  const bool res = a.residual && !(dbg & 16), csa = a.csa_out && !(dbg & 16);
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
     const int e = tid + NT * i, co2 = e >> 5, qi = e & 31, yy = y0 + (qi >> 2), xx = x0 + 4 * (qi & 3);
@@ -498,7 +503,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
     if (!eok[i]) continue;
-    if (a.dbg & 16) {  // no epilogue traffic (keeps the work alive)
+    if (dbg & 16) {  // no epilogue traffic (keeps the work alive)
       if (ev[i][0] == 12345.f) a.out[eo[i]] = ev[i][1];
       continue;
     }

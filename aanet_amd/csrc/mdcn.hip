@@ -67,6 +67,17 @@ struct MdcnArgs {
   float *post_out;        // NHWC [N][Ho][Wo][64]
 };
 
+// the backward's timing switch: a kernel argument in the debug build, a compile-time 0 otherwise
+// (so the product kernels carry no branch for it)
+__device__ __forceinline__ int bwd_dbg(const MdcnArgs &a) {
+#ifdef AANET_DEBUG_SWITCHES
+  return a.dbg_noatom;
+#else
+  (void)a;
+  return 0;
+#endif
+}
+
 // Bilinear sampling state of one (pixel, tap, deformable group).  Invalid corners get
 // weight 0 and a clamped (valid) address, which reproduces the reference's `v = 0` branch
 // exactly: w*0 adds a zero term, as 0-valued v does in kernel.cu:478-493.
@@ -1668,7 +1679,7 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_nhwc_kernel(MdcnArgs a, cons
       }
       // grad_x: lanes 0-31 channel cl of pixel 16w + 2t, lanes 32-63 of pixel 16w + 2t + 1
       const int cl = lane & 31;
-      if (cl < rows && !a.dbg_noatom) {
+      if (cl < rows && !bwd_dbg(a)) {
         const long cbase = (long)n * HW * C + c0 + cl;
         auto nadd = [&](int i, float v) {
           if (DET)
@@ -1930,7 +1941,7 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
       }
       // grad_x: lane (pixel 16 w + 4 t + lane / 16, channel lane % 16)
       const int cl = lane & 15;
-      if (cl < rows && a.dbg_noatom != 1) {
+      if (cl < rows && bwd_dbg(a) != 1) {
         const long cbase = (long)n * HW * C + cb0 + cl;
 #pragma unroll 2
         for (int t = 0; t < 4; ++t) {
@@ -1994,7 +2005,7 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
       }
     }
     __syncthreads();  // the slice's window is complete
-    if (a.dbg_noatom) continue;
+    if (bwd_dbg(a)) continue;
     // add the window to the global accumulator: consecutive threads take consecutive channels of a
     // position (16 lanes = one 64-byte (float) / 128-byte (int64) segment); zero elements skipped
     for (int e = tid; e < nwin; e += NT) {
