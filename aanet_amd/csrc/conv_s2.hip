@@ -73,9 +73,8 @@ struct S2Args {
 };
 
 __device__ __forceinline__ float s2_act(float v, int act) {
-  if (act == 1) return v > 0.f ? v : 0.f;
-  if (act == 2) return v > 0.f ? v : 0.2f * v;
-  return v;
+  const float neg = act == 2 ? 0.2f * v : (act == 1 ? 0.f : v);  // selects, no scalar branches
+  return v > 0.f ? v : neg;
 }
 
 // compile-time step loop: f(integral_constant<int, S>) for S = 0 .. N-1 (straight-line code)

@@ -78,10 +78,11 @@ __device__ __forceinline__ f32x4 mfma_split6(const bf16x8 (&A)[3], const bf16x8 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[0], t, 0, 0, 0);
 }
 
+// branch-free in the wave-uniform act (selects, not scalar branches that split the epilogue
+// into per-value basic blocks); same values as relu / leaky(0.2) / identity
 __device__ __forceinline__ float act_f(float v, int act) {
-  if (act == 1) return v > 0.f ? v : 0.f;
-  if (act == 2) return v > 0.f ? v : 0.2f * v;
-  return v;
+  const float neg = act == 2 ? 0.2f * v : (act == 1 ? 0.f : v);
+  return v > 0.f ? v : neg;
 }
 
 // Sampling state of one (pixel, tap, deformable group): the window position of the top-left

@@ -24,9 +24,8 @@
 namespace {
 
 __device__ __forceinline__ float pw_act(float v, int act) {
-  if (act == 1) return v > 0.f ? v : 0.f;
-  if (act == 2) return v > 0.f ? v : 0.2f * v;
-  return v;
+  const float neg = act == 2 ? 0.2f * v : (act == 1 ? 0.f : v);  // selects, no scalar branches
+  return v > 0.f ? v : neg;
 }
 
 // Epilogue of one 16-pixel column block: lane holds channels c0..c0+3 (c0 = 16 blk + 4kr) of
