@@ -84,9 +84,11 @@ __device__ __forceinline__ void for_steps(F &&f, std::integer_sequence<int, S...
 }
 
 // epilogue: channel co = 16m + 4kr + r of pixel (y, x); rows of 16 pixels = 64-byte segments.
-// Two passes: every value (with its CSA terms) first, then the stores -- the term loads of all
-// the lane's channels are then in flight together (a store between them could alias their
-// sources, so the compiler would otherwise wait for each in turn).
+// Branch-free in the (wave-uniform) term pointers and the (lane-varying) output choice: each pair
+// of co blocks issues all its term loads first (lanes / tensors without a term read x[0] and
+// discard it), then adds them with selects, then stores through a selected pointer.  Written with
+// per-value branches, the compiler waited for every term load in turn (48 serial round trips at
+// the C2 heads launch).  The arithmetic is the reference order: bias, identity, resized term, act.
 template <int NCB>
 __device__ __forceinline__ void s2_epilogue(const S2Args &a, const f32x4 (&acc)[NCB], int n, int y, int x,
                                             int kr, int co_base, bool pv) {
@@ -94,11 +96,12 @@ __device__ __forceinline__ void s2_epilogue(const S2Args &a, const f32x4 (&acc)[
   if (!pv) return;
   const long P = (long)Ho * Wo, pix = (long)y * Wo + x;
   const int cb = a.Co - a.co_a;
+  const bool hid = a.id != nullptr, hup = a.up != nullptr;
   // the resize stencil of this pixel (PyTorch upsample_bilinear2d, align_corners=False, as in
   // csa.hip's bilinear_resize): the same four offsets and weights for every channel plane
   int o00 = 0, o01 = 0, o10 = 0, o11 = 0;
   float h0l = 0.f, h1l = 0.f, w0l = 0.f, w1l = 0.f;
-  if (a.up) {
+  if (hup) {
     float hr = a.up_sh * ((float)y + 0.5f) - 0.5f;
     hr = hr < 0.f ? 0.f : hr;
     float wr = a.up_sw * ((float)x + 0.5f) - 0.5f;
@@ -110,39 +113,73 @@ __device__ __forceinline__ void s2_epilogue(const S2Args &a, const f32x4 (&acc)[
     o00 = h1 * a.up_w + w1, o01 = o00 + w1p;
     o10 = (h1 + h1p) * a.up_w + w1, o11 = o10 + w1p;
   }
-  float res[NCB][4];
+  const long upa = (long)a.up_h * a.up_w;
+  constexpr int MB = NCB >= 2 ? 2 : 1;  // co blocks per batch of term loads
 #pragma unroll
-  for (int m = 0; m < NCB; ++m) {
-    const int c4 = co_base + 16 * m + 4 * kr;
-    const f32x4 bs = a.bias ? *reinterpret_cast<const f32x4 *>(a.bias + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int m0 = 0; m0 < NCB; m0 += MB) {
+    float tid[MB][4] = {}, tq[MB][4][4] = {};
+    if (hid) {  // wave-uniform: whole batches of loads, never one branch per value
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = c4 + r;
-      float v = acc[m][r] + bs[r];
-      if (co < a.co_a) {
-        const long plane = (long)n * a.co_a + co;
-        if (a.id) v += a.id[plane * P + pix];
-        if (a.up) {
-          const float *im = a.up + plane * a.up_h * a.up_w;
-          v += h0l * (w0l * im[o00] + w1l * im[o01]) + h1l * (w0l * im[o10] + w1l * im[o11]);
+      for (int mm = 0; mm < MB; ++mm)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = co_base + 16 * (m0 + mm) + 4 * kr + r;
+          const bool ina = co < a.co_a;
+          tid[mm][r] = *(ina ? a.id + ((long)n * a.co_a + co) * P + pix : a.x);
         }
-        v = s2_act(v, a.act[0]);
-      } else {
-        v = s2_act(v, a.act[1]);
+    }
+    if (hup) {
+#pragma unroll
+      for (int mm = 0; mm < MB; ++mm)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = co_base + 16 * (m0 + mm) + 4 * kr + r;
+          const bool ina = co < a.co_a;
+          const float *im = ina ? a.up + ((long)n * a.co_a + co) * upa : a.x;
+          tq[mm][r][0] = im[ina ? o00 : 0];
+          tq[mm][r][1] = im[ina ? o01 : 0];
+          tq[mm][r][2] = im[ina ? o10 : 0];
+          tq[mm][r][3] = im[ina ? o11 : 0];
+        }
+    }
+#pragma unroll
+    for (int mm = 0; mm < MB; ++mm) {
+      const int m = m0 + mm, c4 = co_base + 16 * m + 4 * kr;
+      const f32x4 bs = a.bias ? *reinterpret_cast<const f32x4 *>(a.bias + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      float res[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = c4 + r;
+        const bool ina = co < a.co_a;
+        float v = acc[m][r] + bs[r];
+        const float vi = v + tid[mm][r];
+        v = (hid && ina) ? vi : v;
+        const float vu = v + (h0l * (w0l * tq[mm][r][0] + w1l * tq[mm][r][1]) +
+                              h1l * (w0l * tq[mm][r][2] + w1l * tq[mm][r][3]));
+        v = (hup && ina) ? vu : v;
+        v = s2_act(v, ina ? a.act[0] : a.act[1]);
+        res[r] = v;
       }
-      res[m][r] = v;
+      // stores: a wave-uniform branch when the whole 16-channel block lies in one output (always
+      // for 16-multiple co_a), a per-lane pointer select otherwise
+      const int cm = co_base + 16 * m;
+      if (cm + 16 <= a.co_a) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a.out[0][((long)n * a.co_a + c4 + r) * P + pix] = res[r];
+      } else if (cm >= a.co_a) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a.out[1][((long)n * cb + c4 + r - a.co_a) * P + pix] = res[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = c4 + r;
+          float *dst = co < a.co_a ? a.out[0] + ((long)n * a.co_a + co) * P + pix
+                                   : a.out[1] + ((long)n * cb + co - a.co_a) * P + pix;
+          *dst = res[r];
+        }
+      }
     }
   }
-#pragma unroll
-  for (int m = 0; m < NCB; ++m)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = co_base + 16 * m + 4 * kr + r;
-      if (co < a.co_a)
-        a.out[0][((long)n * a.co_a + co) * P + pix] = res[m][r];
-      else
-        a.out[1][((long)n * cb + co - a.co_a) * P + pix] = res[m][r];
-    }
 }
 
 // ---- row form for the wide tiles (round 3) ------------------------------------------------
