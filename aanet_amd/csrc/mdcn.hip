@@ -3131,7 +3131,7 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
   // <= 9 taps, <= 64 output channels): 8x8 tile per workgroup in 16-channel slices, int64
   // fixed-point LDS window.
   // AUTO takes it in both modes; GLOBAL / WINDOW force one form (tests, A/B).
-  const int cpg = c / dg, R = 2;
+  const int R = 2;
   const int WR = 8 + (kh - 1) * dil + 2 * R, WCw = 8 + (kw - 1) * dil + 2 * R;
   const bool fusew = true;  // the weight gradient rides in the window kernel (both modes)
   // gOut tile pitch of the window kernel: 80 (= 16 mod 32) keeps the colg reads (rows kr,
