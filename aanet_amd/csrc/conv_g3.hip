@@ -203,6 +203,18 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_g3_kernel(G3Args a) {
   if (!pv) return;
   const int Cog = a.Co / G;
   const long pix = (long)y * W + x;
+  // the biases first, as one batch under one wave-uniform test (clamped rows past Cog read a valid
+  // element and are never stored): loaded per value under the lane-varying cl < Cog, each load
+  // was followed by its own full wait
+  float bv[G][NCB][4] = {};
+  if (a.bias) {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int m = 0; m < NCB; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[g][m][r] = a.bias[g * Cog + min(16 * m + 4 * kr + r, Cog - 1)];
+  }
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -212,7 +224,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_g3_kernel(G3Args a) {
         const int cl = 16 * m + 4 * kr + r;
         if (cl < Cog) {
           const int co = g * Cog + cl;
-          a.out[((long)n * a.Co + co) * HW + pix] = acc[g][m][r] + (a.bias ? a.bias[co] : 0.f);
+          a.out[((long)n * a.Co + co) * HW + pix] = acc[g][m][r] + bv[g][m][r];
         }
       }
 }
