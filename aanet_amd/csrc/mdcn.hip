@@ -1198,6 +1198,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
 #pragma unroll
   for (int i0 = 0; i0 < EPT; i0 += EB) {
     f32x4 ev[EB], er[EB], eu[EB][2][2];
+    float pbi[EB], psc[EB], psh[EB];
     bool eok[EB];
 #pragma unroll
     for (int b = 0; b < EB; ++b) {
@@ -1207,6 +1208,11 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       if (!eok[b]) continue;
       const long pe = pix(4 * q);
       const long o = ((long)n * cout + co) * P + pe;
+      // the channel's parameters in this load pass too: loaded in the use pass, each item
+      // waited for its own
+      pbi[b] = ebias ? ebias[co] : 0.f;
+      psc[b] = esc ? esc[co] : 1.f;
+      psh[b] = esc ? esh[co] : 0.f;
       ev[b] = *reinterpret_cast<const f32x4 *>(sO + col * OP + 4 * q);
       if (a.residual) er[b] = *reinterpret_cast<const f32x4 *>(a.residual + o);
       if (csa) {
@@ -1233,9 +1239,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       const int col = e / QPR, q = e % QPR, co = co0 + col;
       const long pe = pix(4 * q);
       const long o = ((long)n * cout + co) * P + pe;
-      const float bias = ebias ? ebias[co] : 0.f;
-      const float sc = esc ? esc[co] : 1.f;
-      const float sh = esc ? esh[co] : 0.f;
+      const float bias = pbi[b], sc = psc[b], sh = psh[b];
       f32x4 v = ev[b];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
