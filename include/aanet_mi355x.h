@@ -335,8 +335,13 @@ int aanet_mdcn_bwd_ws_f32(const float *x, const float *offset, const float *mask
  *   - grad_x: 64-bit fixed-point atomics. Integer adds are associative, so the sum does not
  *     depend on atomic ordering. The fixed-point scale is a power of two chosen on the device from
  *     max_{c,k} sum_co |W| * max|grad_out| * max|mask|, so there is no host synchronisation.
- *   - grad_weight: per-split partial sums reduced in a fixed order.
- * `workspace` (device, caller-owned) must hold aanet_mdcn_bwd_det_workspace_size(...) bytes.
+ *   - grad_weight: partial sums reduced in a fixed order -- per split of the weight kernel, or,
+ *     when the window form applies (stride 1, <= 32 channels per deformable group, <= 9 taps,
+ *     <= 64 output channels, C and C/dg multiples of 4), one partial per 8x8 output tile of the
+ *     window kernel, summed over 64 chunks of consecutive tiles and then over the chunks.
+ * `workspace` (device, caller-owned) must hold aanet_mdcn_bwd_det_workspace_size(...) bytes; with
+ * the window form that includes tiles * co * c * kh * kw floats of tile partials
+ * (tiles = n * ceil(ho / 8) * ceil(wo / 8)).
  * The atomic col2im of the reference (kernel.cu:688) has no such guarantee. */
 size_t aanet_mdcn_bwd_det_workspace_size(int n, int c, int h, int w, int co, int kh, int kw,
                                          int stride, int pad, int dil, int groups, int dg);

@@ -168,3 +168,10 @@ def test_mdcn_backward_workspace_sizes():
     assert ws >= 4 * (2 * n * c * h * w + co * c * 9)
     assert det >= 8 * n * c * h * w + 4 * (n * c * h * w + co * c * 9)
     assert L.aanet_mdcn_bwd_ws_workspace_size(n, 63, h, w, co, 3, 3, 1, 2, 2, 1, 2) == 0  # C % dg
+    # the window form's per-tile weight-gradient partials (8x8 output tiles, co*c*9 floats each,
+    # plus 64 chunk sums): present when the window applies (32 channels per group here) ...
+    tiles = n * ((h + 7) // 8) * ((w + 7) // 8)
+    assert det >= 8 * n * c * h * w + 4 * (tiles + 64) * co * c * 9
+    # ... and absent when it does not (64 channels per deformable group: dg = 1)
+    det1 = L.aanet_mdcn_bwd_det_workspace_size(n, c, h, w, co, 3, 3, 1, 2, 2, 1, 1)
+    assert det - det1 >= 4 * (tiles + 64) * co * c * 9
