@@ -10,8 +10,10 @@ import torch
 from . import _lib, ops  # noqa: F401
 from . import torch_ops  # noqa: F401  (registers torch.ops.aanet.*)
 
-# fp32 convolutions on MIOpen: scoped to this package's module forwards (_precision.fp32_convs);
-# importing the package changes no global torch setting.
+# fp32 convolutions on MIOpen: scoped to this package's module forwards (_precision.fp32_convs)
+# and, for the backward, to a training step (fp32_scope; Trainer uses it); importing the package
+# changes no global torch setting.
+from ._precision import fp32_scope  # noqa: F401,E402
 
 __version__ = "0.1.0"
 

@@ -2622,42 +2622,48 @@ __global__ __launch_bounds__(256) void det_wbound_kernel(const float *__restrict
   for (int e = blockIdx.x * 256 + threadIdx.x; e < CK; e += gridDim.x * 256) {
     float s = 0.f;
     for (int co = 0; co < Co; ++co) s += fabsf(w[(long)co * CK + e]);
-    atomicMax(bounds, __float_as_uint(s));
+    atomicMax(bounds, __float_as_uint(s) & 0x7fffffffu);  // NaN bits order above +inf
   }
 }
 
 // max |v| into *slot (as the uint bits of a non-negative float): 16-byte loads when v is
 // 16-byte aligned, one atomic per workgroup (a few hundred workgroups: per-wave atomics on one
-// address serialise at the L2 and dominated this kernel).
+// address serialise at the L2 and dominated this kernel).  The max is taken over the bit
+// patterns of |v|, which order like the values and put NaN (0x7fc...) above +inf: a NaN or an
+// inf anywhere reaches the bound (fmaxf would drop a NaN), and det_scale_kernel then poisons.
+__device__ __forceinline__ unsigned abs_bits(float x) { return __float_as_uint(x) & 0x7fffffffu; }
 __global__ __launch_bounds__(256) void det_absmax_kernel(const float *__restrict__ v, long n,
                                                          unsigned *__restrict__ slot) {
-  __shared__ float red[4];
-  float m = 0.f;
+  __shared__ unsigned red[4];
+  unsigned m = 0u;
   const long stride = (long)gridDim.x * 256, t0 = (long)blockIdx.x * 256 + threadIdx.x;
   long tail = 0;
   if ((reinterpret_cast<uintptr_t>(v) & 15) == 0) {
     const long n4 = n >> 2;
     for (long q = t0; q < n4; q += stride) {
       const f32x4 x = reinterpret_cast<const f32x4 *>(v)[q];
-      m = fmaxf(m, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+      m = max(m, max(max(abs_bits(x[0]), abs_bits(x[1])), max(abs_bits(x[2]), abs_bits(x[3]))));
     }
     tail = n4 << 2;
   }
-  for (long e = tail + t0; e < n; e += stride) m = fmaxf(m, fabsf(v[e]));
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  for (long e = tail + t0; e < n; e += stride) m = max(m, abs_bits(v[e]));
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0)
-    atomicMax(slot, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+  if (threadIdx.x == 0) atomicMax(slot, max(max(red[0], red[1]), max(red[2], red[3])));
 }
 
 // scale = 2^(38 - ceil(log2 bound)): a single contribution stays below 2^38, so up to 2^25 of
 // them can meet in one element before the int64 sum could overflow; the fixed-point step
 // (2^-38 of the largest possible contribution) is far below fp32 rounding of typical sums.
+// A non-finite bound (an inf or NaN in the weights, grad_out or mask) gives scale = NaN: the
+// fixed-point sums are then read back through 1/scale = NaN, so grad_x comes out NaN instead
+// of finite garbage from __double2ll_rn(inf/NaN) (the reference's float col2im would propagate
+// the non-finite value).
 __global__ void det_scale_kernel(const unsigned *__restrict__ bounds, double *__restrict__ scale) {
   const double b = (double)__uint_as_float(bounds[0]) * (double)__uint_as_float(bounds[1]) *
                    (double)__uint_as_float(bounds[2]);
-  *scale = (b > 0.0 && isfinite(b)) ? ldexp(1.0, 38 - (int)ceil(log2(b))) : 1.0;
+  *scale = !isfinite(b) ? __builtin_nan("") : (b > 0.0 ? ldexp(1.0, 38 - (int)ceil(log2(b))) : 1.0);
 }
 
 // gw[e] += sum over the splits of part[split][e], in a fixed order: workgroup = 64 consecutive

@@ -13,6 +13,7 @@ from .estimation import DisparityEstimation  # noqa: F401
 from .feature import (BasicConv, Conv2x, FeaturePyramidNetwork, FeaturePyrmaid,  # noqa: F401
                       GANetFeature, GCNetFeature, PSMNetFeature, StereoNetFeature)
 from .hotpath import AANetHotPath  # noqa: F401
+from .options import set_options  # noqa: F401
 from .refinement import HourglassRefinement, StereoDRNetRefinement, StereoNetRefinement  # noqa: F401
 from .resnet import AANetFeature  # noqa: F401
 from .warp import disp_warp  # noqa: F401

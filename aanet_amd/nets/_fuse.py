@@ -4,8 +4,6 @@ into its weights/bias (cached per parameter version), the activation and the bot
 residual add in its epilogue.  Training mode never uses these: modules then run the reference
 op sequence with autograd.
 """
-import os
-
 import torch
 import torch.nn as nn
 
@@ -87,9 +85,10 @@ def dense_grouped_ok(conv, x):
     of 32 channels: run as ONE ungrouped conv with a block-diagonal weight.  Twice the MACs, but
     on the split-bf16 contraction instead of the exact-f32 16-channel form (C2 scale 1, B=8:
     37 -> 29 us, tools/dense_grouped_bench.py); the
-    zero blocks add exact zeros, so only the fp32 summation order differs.  AANET_DENSE_GROUPED=0 keeps the grouped engine (A/B switch)."""
+    zero blocks add exact zeros, so only the fp32 summation order differs.  The conv's
+    `dense_grouped` option (nets/options.py set_options) False keeps the grouped engine."""
     return conv.groups == 2 and (conv.in_channels // 2) % 32 != 0 and conv.in_channels % 32 == 0 \
-        and x.is_cuda and os.environ.get("AANET_DENSE_GROUPED", "1") != "0"
+        and x.is_cuda and getattr(conv, "aanet_dense_grouped", True)
 
 
 def folded_dense(conv, bn):

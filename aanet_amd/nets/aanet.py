@@ -16,6 +16,7 @@ from .aggregation3d import (GCNetAggregation, PSMNetBasicAggregation, PSMNetHGAg
 from .cost import CostVolume, CostVolumePyramid
 from ._fuse import FoldCacheMixin
 from .estimation import DisparityEstimation
+from .options import set_options
 from .feature import (FeaturePyramidNetwork, FeaturePyrmaid, GANetFeature, GCNetFeature,
                       PSMNetFeature, StereoNetFeature)
 from .refinement import HourglassRefinement, StereoDRNetRefinement, StereoNetRefinement
@@ -110,6 +111,10 @@ class AANet(FoldCacheMixin, nn.Module):
                 raise NotImplementedError
             self.refinement = nn.ModuleList([_REFINEMENT[self.refinement_type]()
                                              for _ in range(num_downsample)])
+
+    def set_options(self, **options):
+        """Eval schedule options of the whole model (nets/options.py); returns self."""
+        return set_options(self, **options)
 
     def feature_extraction(self, img):
         """aanet.py:140-144."""

@@ -10,7 +10,6 @@ kernel; training mode runs the reference op sequence with autograd.
 The 3D-conv aggregators (StereoNet/PSMNet/GCNet) are out of scope.
 """
 import contextlib
-import os
 
 import torch
 import torch.nn as nn
@@ -19,6 +18,7 @@ from .. import ops
 from ._fuse import FoldCacheMixin, conv_bn_act, folded, s2_conv_ok, s2_pack, s2_pack_k, use_fused
 from .deform import DeformSimpleBottleneck, SimpleBottleneck
 from .._precision import fp32_convs
+from .options import get_option, set_options
 
 
 _SIDE_STREAMS = {}
@@ -31,29 +31,6 @@ def side_streams(device, n):
     while len(ss) < n:
         ss.append(torch.cuda.Stream(device=device))
     return ss[:n]
-
-
-def concurrent_scales():
-    """AANET_CONCURRENT_SCALES=0 runs the whole eval aggregation on one stream (A/B switch)."""
-    return os.environ.get("AANET_CONCURRENT_SCALES", "1") != "0"
-
-
-def post_fusion():
-    """AANET_POST_FUSION=0 disables the tail kernels' post stage (the next module's conv1 and the
-    final_conv + regression in the previous tail kernel's epilogue): A/B switch."""
-    return os.environ.get("AANET_POST_FUSION", "1") != "0"
-
-
-def post_conv1():
-    """Whether the plain 3x3 tails take the next module's conv1 as their post stage
-    (AANET_POST_FUSION=final keeps only the last module's final_conv + regression stage)."""
-    return os.environ.get("AANET_POST_FUSION", "1") not in ("0", "final")
-
-
-def s2_sums():
-    """AANET_S2_SUMS=0 keeps the coarse branches' CSA sums in aanet_csa_sum_f32 kernels instead of
-    the stride-2 kernels' epilogues (A/B switch)."""
-    return os.environ.get("AANET_S2_SUMS", "1") != "0"
 
 
 def _record(stream):
@@ -183,7 +160,8 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
         Needs the reference's S = 3 structure (one conv from scale 0 to 1, two from 0 to 2, one
         from 1 to 2), every conv on the stride-2 kernel, and sizes that need no resize of the
         same-resolution terms (aggregation.py:395: x1 / x2 already have the down terms' size)."""
-        if len(self.branches) != 3 or len(self.fuse_layers) != 3 or not s2_sums():
+        if len(self.branches) != 3 or len(self.fuse_layers) != 3 or \
+                not get_option(self, "s2_sums"):
             return False
         l10, l20, l21 = self.fuse_layers[1][0], self.fuse_layers[2][0], self.fuse_layers[2][1]
         if len(l10) != 1 or len(l20) != 2 or len(l21) != 1:
@@ -448,13 +426,18 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
             if not self.intermediate_supervision:
                 break
 
+    def set_options(self, **options):
+        """Eval schedule options of this aggregation (nets/options.py: concurrent_scales,
+        post_fusion, s2_sums, dense_grouped); returns self."""
+        return set_options(self, **options)
+
     def _post_for(self, i, regress):
         """The post stage of fusion i's scale-0 tail kernel (eval, fused): the next module's
         bottleneck conv1 + BN1 + ReLU (NHWC), or for the last fusion, with `regress`, final_conv +
         the soft-argmin.  None when the shapes do not fit (64 channels at scale 0, 1x1, one
         stage block)."""
         if i + 1 < self.num_fusions:
-            if not post_conv1():
+            if get_option(self, "post_fusion") != "all":
                 return None
             # the window DCN tail (dcn_tile.hip) pays more for the conv1 stage (spills of its POST
             # instantiation: +60-65 us per launch) than the separate 1x1 launch costs (46-56 us);
@@ -497,7 +480,8 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
         assert isinstance(cost_volume, list)
         fused = use_fused(self, cost_volume[0])
         streams = None
-        if fused and cost_volume[0].is_cuda and self.num_scales > 1 and concurrent_scales():
+        if fused and cost_volume[0].is_cuda and self.num_scales > 1 and \
+                get_option(self, "concurrent_scales"):
             dev = cost_volume[0].device
             main = torch.cuda.current_stream(dev)
             ss = side_streams(dev, self.num_scales - 1)
@@ -506,7 +490,7 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
                 st.wait_stream(main)  # the cost volumes are written on the current stream
             keep = list(cost_volume)
         pre, disp = None, None
-        post_ok = fused and cost_volume[0].is_cuda and post_fusion()
+        post_ok = fused and cost_volume[0].is_cuda and get_option(self, "post_fusion") != "none"
         for i in range(self.num_fusions):
             fusion = self.fusions[i]
             post = self._post_for(i, regress) if post_ok else None

@@ -14,6 +14,7 @@ from .aggregation import AdaptiveAggregation
 from .cost import CostVolume, CostVolumePyramid
 from ._fuse import FoldCacheMixin
 from .estimation import DisparityEstimation
+from .options import set_options
 from .._precision import fp32_convs
 
 
@@ -38,6 +39,10 @@ class AANetHotPath(FoldCacheMixin, nn.Module):
                                                intermediate_supervision=not no_intermediate_supervision)
         match_similarity = feature_similarity not in ['difference', 'concat']
         self.disparity_estimation = DisparityEstimation(max_disp, match_similarity)
+
+    def set_options(self, **options):
+        """Eval schedule options of the path (nets/options.py); returns self."""
+        return set_options(self, **options)
 
     def cost_volume_construction(self, left_feature, right_feature):
         cost_volume = self.cost_volume(left_feature, right_feature)

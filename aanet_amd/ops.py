@@ -569,13 +569,29 @@ def resize_bilinear(x, size):
 DCN_BWD_ALGOS = {"auto": 0, "global": 1, "window": 2}  # AANET_DCN_BWD_* (include/aanet_mi355x.h)
 
 
+def window_bwd_ok(C, Co, kh, kw, stride, dilation, deformable_groups):
+    """Whether AANET_DCN_BWD_WINDOW takes a DCN backward shape (mdcn.hip win_shape_ok; the full
+    list of include/aanet_mi355x.h).  The LDS term: gOut tile, W^T slice, sampling / partial
+    buffers, sampled columns and the int64 window of (8 + (k-1) dil + 4)^2 positions x 16
+    channels, within the CU's 160 KiB."""
+    cpg = C // deformable_groups
+    if stride != 1 or cpg > 32 or C % 4 or cpg % 4 or kh * kw > 9 or Co > 64:
+        return False
+    pitch = lambda v: v + (2 - v % 32) % 32  # noqa: E731  (mdcn.hip round_pitch(v, 2))
+    wr, wc = 8 + (kh - 1) * dilation + 4, 8 + (kw - 1) * dilation + 4
+    smem = 4 * (Co * pitch(64) + 16 * pitch(Co) + 16 * 66 + 64 * 16 + 3 * 9 * 64 + 16 * 66) \
+        + wr * wc * 16 * 8
+    return smem <= 160 * 1024
+
+
 def mdcn_backward(x, offset, mask, weight, grad_out, with_bias, stride, padding, dilation, groups,
                   deformable_groups, deterministic=None, nchw_scatter=False, algo="auto"):
     """deform_conv_cuda.cpp:571-685 -> (gX, gOffset, gMask, gW, gB or None).
 
     Default: aanet_mdcn_bwd_algo_f32 with the caller-owned workspace; algo "auto" takes the
-    LDS-window form of grad_x where it applies (stride 1, <= 32 channels per deformable group,
-    channel counts divisible by 4; int64 fixed-point window in both modes) and the global-atomic
+    LDS-window form of grad_x where it applies (window_bwd_ok: stride 1, <= 32 channels per
+    deformable group, C and C/dg divisible by 4, <= 9 taps, Co <= 64, and the window's LDS within
+    160 KiB; int64 fixed-point window in both modes) and the global-atomic
     form otherwise; "window" / "global" force one form (AANET_EUNSUPPORTED if the window form
     does not apply).  nchw_scatter=True: the workspace-free aanet_mdcn_bwd_f32 (global atomics in NCHW).
 

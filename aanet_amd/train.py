@@ -30,6 +30,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
+from ._precision import fp32_scope
 from .nets._fuse import clear_fold_caches
 
 # model.py:98-107: pyramid weights by pyramid length
@@ -212,12 +213,13 @@ class Trainer:
             self.model.train()
 
             def body():
-                pyramid = self.model(left_feature, right_feature)
-                if self.highest_loss_only:
-                    pyramid = [pyramid[-1]]
-                total, _ = disparity_loss(pyramid, gt_disp, mask,
-                                          pyramid_weights(len(pyramid), self.highest_loss_only))
-                total.backward()
+                with fp32_scope():  # forward AND backward convs in fp32 (_precision.py)
+                    pyramid = self.model(left_feature, right_feature)
+                    if self.highest_loss_only:
+                        pyramid = [pyramid[-1]]
+                    total, _ = disparity_loss(pyramid, gt_disp, mask,
+                                              pyramid_weights(len(pyramid), self.highest_loss_only))
+                    total.backward()
                 self.optimizer.step()
                 return total.detach()
             # the warm-up steps must not count: parameters, BN buffers and the optimizer state are
@@ -283,7 +285,7 @@ class Trainer:
         sync_ctx = contextlib.nullcontext()
         if not boundary and isinstance(self.model, nn.parallel.DistributedDataParallel):
             sync_ctx = self.model.no_sync()
-        with sync_ctx:
+        with sync_ctx, fp32_scope():  # forward AND backward convs in fp32 (_precision.py)
             pyramid = self.model(left_feature, right_feature)
             if self.highest_loss_only:
                 pyramid = [pyramid[-1]]

@@ -360,8 +360,10 @@ enum {
   AANET_DCN_BWD_GLOBAL = 1, /* one global atomic per (pixel, tap, corner, channel) contribution,
                                the reference's col2im pattern (kernel.cu:635-693), into an NHWC
                                accumulator */
-  AANET_DCN_BWD_WINDOW = 2  /* stride 1, <= 32 channels per deformable group, channel counts
-                               divisible by 4: each (8x8 output tile, 16-channel slice) sums its
+  AANET_DCN_BWD_WINDOW = 2  /* stride 1, <= 32 channels per deformable group, C and C/dg
+                               divisible by 4, <= 9 taps, Co <= 64, and the window's LDS
+                               (grows with the dilation) within the CU's 160 KiB: each
+                               (8x8 output tile, 16-channel slice) sums its
                                contributions in an int64 fixed-point LDS window and adds the
                                window once -- float atomics (deterministic = 0) or int64 ones
                                (AANET_EUNSUPPORTED for other shapes) */

@@ -45,6 +45,11 @@ MODELS = {
                       no_intermediate_supervision=True), (48, 96), 1, 15),
     "psmnet_aa": (dict(feature_type="psmnet", feature_pyramid=True,
                        no_intermediate_supervision=True), (256, 256), 1, 16),
+    # the same model and inputs WITHOUT the conditioning below: the near-tie regime in which the
+    # reference's own fp32 run flips pixels against its fp64 run, kept (non-strict) so the flip
+    # bounds of tests/test_gpu_models.py stay exercised
+    "psmnet_aa_raw": (dict(feature_type="psmnet", feature_pyramid=True,
+                           no_intermediate_supervision=True), (256, 256), 1, 16),
     # 3-D aggregators on concat / difference volumes (C5)
     "psmnet_hg": (dict(feature_type="psmnet", feature_similarity="concat",
                        aggregation_type="psmnet_hourglass", refinement_type=None), (256, 256), 1, 17),
@@ -56,7 +61,7 @@ MODELS = {
                           aggregation_type="stereonet", refinement_type="stereonet"), (64, 128), 1, 20),
 }
 # max_disp per config (the image-resolution disparity range; GC-Net needs D/2 divisible by 16)
-MAX_DISP_OF = {"gcnet_3d": 64, "psmnet_aa": 64, "psmnet_hg": 64, "psmnet_basic": 64}
+MAX_DISP_OF = {"gcnet_3d": 64, "psmnet_aa": 64, "psmnet_aa_raw": 64, "psmnet_hg": 64, "psmnet_basic": 64}
 MAX_DISP = 48
 # Fixture conditioning ({state-dict name: factor}, applied after the name-keyed fill and saved in
 # the fixture as `scales`).  PSMNet-AA's plain fill gives un-normalised PSMNet features (std 31)

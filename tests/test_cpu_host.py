@@ -1,5 +1,6 @@
 """CPU-side checks of the host layer: C-ABI library exports, drop-in module API / state-dict keys,
 and loud failure (no silent CPU fallback)."""
+import contextlib
 import ctypes
 import os
 import re
@@ -89,6 +90,29 @@ def test_import_leaves_global_torch_flags_alone():
     out = subprocess.run([sys.executable, "-c", code], cwd=REPO, capture_output=True, text=True,
                          timeout=120).stdout.split()
     assert out == ["True", "True", "False"], out
+
+
+def test_fp32_scope_covers_the_conv_backward():
+    """autograd's conv backward reads the global TF32 flag at loss.backward(), outside
+    the decorated forward.  fp32_scope (what Trainer runs its step in) keeps it off there too; a
+    bare decorated forward alone does not (the documented reason for the scope)."""
+    from aanet_amd._precision import fp32_convs, fp32_scope
+    conv = torch.nn.Conv2d(2, 2, 3)
+    fwd = fp32_convs(lambda x: conv(x))
+    prev = torch.backends.cudnn.allow_tf32
+    torch.backends.cudnn.allow_tf32 = True
+    try:
+        for scoped in (True, False):
+            seen = []
+            h = conv.weight.register_hook(lambda g: seen.append(torch.backends.cudnn.allow_tf32))
+            ctx = fp32_scope() if scoped else contextlib.nullcontext()
+            with ctx:
+                fwd(torch.randn(1, 2, 5, 5)).sum().backward()
+            h.remove()
+            assert seen == [not scoped], (scoped, seen)
+            assert torch.backends.cudnn.allow_tf32 is True
+    finally:
+        torch.backends.cudnn.allow_tf32 = prev
 
 
 def test_ops_fail_loudly_on_cpu_tensors():

@@ -2,14 +2,13 @@
 3x3, dilation 2) runs in eval as one ungrouped block-diagonal conv on the split-bf16 engine
 (nets/_fuse.py dense_grouped_ok): against fp64, held to the grouped exact-f32 engine's error, and
 the weight cache follows parameter updates."""
-import os
-
 import pytest
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from aanet_amd.nets._fuse import conv_bn_act, dense_grouped_ok
+from aanet_amd.nets.options import set_options
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -31,15 +30,10 @@ def test_dense_grouped_offset_conv_vs_fp64(N, H, W, nhwc):
                      dilation=2, groups=2) + 1.0
     with torch.no_grad():
         got = conv_bn_act(xin, conv)
-        prev = os.environ.get("AANET_DENSE_GROUPED")
-        os.environ["AANET_DENSE_GROUPED"] = "0"
-        try:
-            grouped = conv_bn_act(xin, conv)  # the grouped engine (exact-f32 16-channel form)
-        finally:
-            if prev is None:
-                del os.environ["AANET_DENSE_GROUPED"]
-            else:
-                os.environ["AANET_DENSE_GROUPED"] = prev
+        set_options(conv, dense_grouped=False)
+        assert not dense_grouped_ok(conv, xin)
+        grouped = conv_bn_act(xin, conv)  # the grouped engine (exact-f32 16-channel form)
+        set_options(conv, dense_grouped=True)
     err = ((got.double().cpu() - y64).abs() / scale).max().item()
     err_g = ((grouped.double().cpu() - y64).abs() / scale).max().item()
     assert err <= max(4 * err_g, 2e-7), (err, err_g)

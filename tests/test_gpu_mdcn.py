@@ -306,8 +306,10 @@ def test_mdcn_backward_window_form_vs_oracle(case, algo):
                                     dg, deterministic=det, algo=algo)
         except _lib.AanetError as e:
             assert algo == "window" and e.status == _lib.EUNSUPPORTED and \
-                (s != 1 or C // dg > 32 or C % 4 or (C // dg) % 4), (case, e)
+                not ops.window_bwd_ok(C, Co, k, k, s, d, dg), (case, e)
             return
+        if algo == "window":
+            assert ops.window_bwd_ok(C, Co, k, k, s, d, dg), case
         ref = oracle.mdcn_backward(x, off, msk, w, go, True, s, p, d, 1, dg)
         for name, gt, r in zip(("grad_input", "grad_offset", "grad_mask", "grad_weight", "grad_bias"), got, ref):
             err = np.abs(t2n(gt) - r)
@@ -333,6 +335,29 @@ def test_mdcn_backward_c4_agg_s0_vs_oracle(form):
         err = np.abs(t2n(gt) - r)
         scale = np.abs(r).max() + 1e-12
         assert err.max() <= 1e-4 * scale + 1e-6, f"{form} {name}: max err {err.max():.3g} (scale {scale:.3g})"
+
+
+@pytest.mark.parametrize("det", [False, True])
+@pytest.mark.parametrize("bad", [np.inf, np.nan])
+def test_mdcn_backward_nonfinite_grad_out_propagates(det, bad):
+    """a non-finite grad_out value must give a non-finite grad_input, as the reference's
+    float col2im does, in the window (fixed-point) form of both modes -- not finite garbage from
+    converting inf/NaN to int64.  The other gradients stay computed in float and carry it too."""
+    N, C, H, W, Co, k, s, p, d, dg = 1, 64, 16, 24, 64, 3, 1, 2, 2, 2
+    x, off, msk, w, b = make_case(31, N, C, H, W, Co, k, s, p, d, dg, off_scale=0.7)
+    go = np.random.default_rng(32).standard_normal((N, Co, H, W)).astype(np.float32)
+    go[0, 5, 7, 9] = bad
+    assert ops.window_bwd_ok(C, Co, k, k, s, d, dg)
+    got = ops.mdcn_backward(g2t(x), g2t(off), g2t(msk), g2t(w), g2t(go), True, s, p, d, 1, dg,
+                            deterministic=det, algo="window")
+    gx = t2n(got[0])
+    assert not np.isfinite(gx).all()
+    assert not np.isfinite(t2n(got[3])).all()       # grad_weight
+    # a clean grad_out through the same form is finite (the poison comes from the bad value)
+    go[0, 5, 7, 9] = 0.0
+    clean = ops.mdcn_backward(g2t(x), g2t(off), g2t(msk), g2t(w), g2t(go), True, s, p, d, 1, dg,
+                              deterministic=det, algo="window")
+    assert all(np.isfinite(t2n(t)).all() for t in clean if t is not None)
 
 
 def test_mdcn_backward_window_deterministic_bit_reproducible():

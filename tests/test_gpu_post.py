@@ -2,10 +2,8 @@
 the scale-0 tail kernel's epilogue on its CSA output -- the next AAModule's bottleneck conv1 +
 BN1 + ReLU (channels-last), or final_conv + the soft-argmin (nets/aggregation.py:443-447,
 nets/estimation.py:13-30).  Checked against the same stages run as separate kernels on the
-tail's own CSA output, and the module path against the post-free path (AANET_POST_FUSION=0 is
-read per forward)."""
-import os
-
+tail's own CSA output, and the module path against the post-free schedules
+(set_options(post_fusion="none" / "final"), nets/options.py)."""
 import pytest
 import torch
 
@@ -86,9 +84,10 @@ def test_plain_tail_post_stage_matches_separate_kernel():
     assert r[2] is None and torch.equal(r[0], out0) and torch.equal(r[1], csa0)
 
 
-def test_hot_path_post_fusion_matches_unfused(monkeypatch):
+@pytest.mark.parametrize("mode", ["none", "final"])
+def test_hot_path_post_fusion_matches_unfused(mode):
     """C2-width hot path (D=64) on a small pyramid: disparities with the post stages (conv1 folds,
-    tail regression) vs without them."""
+    tail regression) vs without them (post_fusion="none") or with the last one only ("final")."""
     torch.manual_seed(0)
     m = nets.AANetHotPath(64, no_intermediate_supervision=True, num_deform_blocks=3)
     fill_synthetic(m.aggregation, 7)
@@ -97,7 +96,7 @@ def test_hot_path_post_fusion_matches_unfused(monkeypatch):
     left, right = [t.to(DEV) for t in left], [t.to(DEV) for t in right]
     with torch.no_grad():
         d_post = m(left, right)[0]
-        monkeypatch.setenv("AANET_POST_FUSION", "0")
+        m.set_options(post_fusion=mode)
         d_ref = m(left, right)[0]
     err = (d_post - d_ref).abs().max().item()
     assert err <= 2e-4, err

@@ -17,7 +17,7 @@ channels wide, so they exercise the exact-f32 NCHW engine only.  Here:
 Tolerances: disparity 5e-4 px max abs (half the north-star bar of 1e-3) and 5e-5 px mean abs;
 aggregated cost 1e-4 x its scale.  The max is set by near-tie pixels of the soft-argmin, where
 the fp32 summation order alone moves it: the same kernels with the CSA sums of branches 1 / 2 in
-aanet_csa_sum_f32 kernels or in the stride-2 kernels' epilogues (AANET_S2_SUMS=0 / 1: the same
+aanet_csa_sum_f32 kernels or in the stride-2 kernels' epilogues (set_options(s2_sums=False / True): the same
 terms in another fp32 order) measured C3 1.2e-4 / 1.6e-4 px and C3 pair 0 vs oracle 1.8e-4 /
 2.1e-4 px, d64 2.3e-4 px with the epilogue sums, every mean unchanged.
 """
@@ -220,20 +220,17 @@ def test_two_stream_schedule_graph_replay_and_single_stream_match():
     """The eval aggregation's concurrent-scale schedule (each coarse scale on its own side stream,
     every cross-stream edge through the capturing stream) captured in a HIP graph, as bench.py
     runs it: replays give the eager result bit for bit, at every pyramid level, and so does the
-    one-stream schedule (AANET_CONCURRENT_SCALES=0: the kernels and their inputs are the same,
-    only their issue order differs)."""
-    import os
-    from aanet_amd.nets import aggregation
+    one-stream schedule (set_options(concurrent_scales=False): the kernels and their inputs are
+    the same, only their issue order differs)."""
+    from aanet_amd.nets.options import get_option
     g, sd, m, left, right = _model("hotpath_d64")
     with torch.no_grad():
         eager = [t.clone() for t in m(left, right)]
-        os.environ["AANET_CONCURRENT_SCALES"] = "0"
-        try:
-            assert not aggregation.concurrent_scales()
-            single = [t.clone() for t in m(left, right)]
-        finally:
-            del os.environ["AANET_CONCURRENT_SCALES"]
-        assert aggregation.concurrent_scales()
+        m.set_options(concurrent_scales=False)
+        assert not get_option(m.aggregation, "concurrent_scales")
+        single = [t.clone() for t in m(left, right)]
+        m.set_options(concurrent_scales=True)
+        assert get_option(m.aggregation, "concurrent_scales")
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             static = m(left, right)
@@ -242,3 +239,18 @@ def test_two_stream_schedule_graph_replay_and_single_stream_match():
             torch.cuda.synchronize()
             for a, b, c in zip(eager, static, single):
                 assert torch.equal(a, b) and torch.equal(a, c)
+
+
+def test_s2_sums_option_matches_separate_csa_sums():
+    """The coarse branches' CSA sums in the stride-2 kernels' epilogues (s2_sums=True, default)
+    against separate aanet_csa_sum_f32 kernels (s2_sums=False): the same terms in another fp32
+    order, so the disparities agree within the near-tie bound, and each matches the reference."""
+    g, _, m, left, right = _model("hotpath_d64")
+    with torch.no_grad():
+        a = m(left, right)[0].cpu().numpy()
+        m.set_options(s2_sums=False)
+        b = m(left, right)[0].cpu().numpy()
+        m.set_options(s2_sums=True)
+    for d in (a, b):
+        assert np.abs(d - g["disp0"]).max() <= DISP_TOL
+    assert np.abs(a - b).max() <= DISP_TOL

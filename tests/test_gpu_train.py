@@ -50,6 +50,41 @@ def test_trainer_steps_hot_path():
     assert 0 < d_off < 0.5 * d_base, (d_off, d_base)
 
 
+def test_trainer_backward_convs_run_fp32_under_global_tf32():
+    """with torch's global allow_tf32=True, the MIOpen conv backward of a Trainer step
+    runs with TF32 off (it reads the flag at backward time), and the weight gradient of such a
+    conv matches an fp64 recomputation at fp32 tolerance."""
+    m = _model(3)
+    conv = m.aggregation.fusions[0].branches[0][0].conv1    # a MIOpen nn.Conv2d in training
+    seen, captured = [], {}
+
+    def hook(g):
+        seen.append(torch.backends.cudnn.allow_tf32)
+        captured["g"] = g.detach().clone()
+    conv.weight.register_hook(hook)
+    xin, gout = {}, {}
+
+    def fwd_hook(mod, inp, out):
+        xin["x"] = inp[0].detach().clone()
+        out.register_hook(lambda g: gout.setdefault("g", g.detach().clone()))
+    conv.register_forward_hook(fwd_hook)
+    prev = torch.backends.cudnn.allow_tf32
+    torch.backends.cudnn.allow_tf32 = True
+    try:
+        t = train.Trainer(m, lr=1e-3, accumulation_steps=2)   # no optimizer step yet
+        l, r, gt = _inputs(2, 4)
+        t.step(l, r, gt)
+        assert torch.backends.cudnn.allow_tf32 is True
+    finally:
+        torch.backends.cudnn.allow_tf32 = prev
+    assert seen == [False], seen
+    x64, g64 = xin["x"].double(), gout["g"].double()
+    ref = torch.nn.grad.conv2d_weight(x64, conv.weight.shape, g64)
+    scale = torch.nn.grad.conv2d_weight(x64.abs(), conv.weight.shape, g64.abs()).max()
+    err = (captured["g"].double() - ref).abs().max() / scale
+    assert err <= 1e-5, float(err)
+
+
 def test_deterministic_training_step_is_bit_reproducible():
     """Same seed and data, deterministic algorithms on: every gradient of the path is
     bit-identical across two runs (the DCN weight/input gradients come from the fixed-point
