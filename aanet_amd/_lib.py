@@ -63,6 +63,7 @@ _SIZE_FUNCTIONS = [
     ("aanet_conv_weight_pack_split_bytes", [_I] * 5, _L),
     ("aanet_conv3x3s2_pack_bytes", [_I, _I], ctypes.c_size_t),
     ("aanet_conv3x3_grouped_pack_bytes", [_I, _I, _I], ctypes.c_size_t),
+    ("aanet_mdcn_window_fwd_supported", [_I] * 10, _I),
 ]
 
 _lib = None

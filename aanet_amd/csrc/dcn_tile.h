@@ -6,7 +6,7 @@
 #include "common.h"
 
 struct DcnTileArgs {
-  const float *x;        // conv1 output, channels-last [N][H][W][C]
+  const float *x;        // conv1 output, channels-last [N][H][W][C] (or NCHW: x_nchw)
   const float *offset;   // offset_conv output planes (NCHW), offsets of group g, tap k at 2(gK+k)
   long off_bs;
   const float *mask;     // mask logits (or values) plane g*K + k
@@ -38,6 +38,8 @@ struct DcnTileArgs {
   float *post_disp;
   int post_skip;  // the post stage's outputs only (out / csa_out not stored)
   int N, C, H, W, Co, Co2, dil, dg;
+  int x_nchw;  // x is NCHW [N][C][H][W] (plain form only)
+  int plain;   // op-level DCN: out = act(post_scale*(DCN + bias) + post_shift), NCHW; no tail
   int dbg;  // AANET_DCN_DBG timing-attribution switches (wrong results; tools/dcn_tile_bench.py)
 };
 

@@ -48,22 +48,16 @@ constexpr int K = 9;             // 3x3 taps
 constexpr int OP = TR * TC + 4;  // epilogue tile pitch (floats)
 
 // ---- split-bf16 contraction (same scheme as mdcn.hip split3 / mfma_split6) -------------------
-__device__ __forceinline__ unsigned hi_pair(float a, float b) {
-  return __builtin_amdgcn_perm(__builtin_bit_cast(unsigned, b), __builtin_bit_cast(unsigned, a), 0x07060302u);
-}
-__device__ __forceinline__ float trunc16(float a) {
-  return __builtin_bit_cast(float, __builtin_bit_cast(unsigned, a) & 0xffff0000u);
-}
-// 8 values -> their three exact bf16 pieces (x = h + m + l)
+// 8 values -> their three exact bf16 pieces (x = h + m + l; common.h split_pair)
 __device__ __forceinline__ void split8(const float (&v)[8], bf16x8 (&b)[3]) {
   u32x4 hh, mm, ll;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const float x0 = v[2 * i], x1 = v[2 * i + 1];
-    hh[i] = hi_pair(x0, x1);
-    const float r0 = x0 - trunc16(x0), r1 = x1 - trunc16(x1);
-    mm[i] = hi_pair(r0, r1);
-    ll[i] = hi_pair(r0 - trunc16(r0), r1 - trunc16(r1));
+    unsigned h, m, l;
+    split_pair(v[2 * i], v[2 * i + 1], h, m, l);
+    hh[i] = h;
+    mm[i] = m;
+    ll[i] = l;
   }
   b[0] = __builtin_bit_cast(bf16x8, hh);
   b[1] = __builtin_bit_cast(bf16x8, mm);
@@ -126,7 +120,9 @@ __device__ __forceinline__ TapState tap_state(float oh, float ow, float ml, int 
 // CG = channels per deformable group (two groups): 32 (scale 0: C = 64) or 16 (scale 1: C = 32).
 // A chunk is one tap of a 32-channel K slice ("phase"): with CG = 32 a phase is one group, with
 // CG = 16 it holds both groups (lane groups kr = 0, 1 carry group 0's channels, kr = 2, 3 group 1's).
-template <int DIL, int CG, bool POST>
+// XN: x is NCHW (the op-level forward, ModulatedDeformConvFunction) instead of channels-last.
+// PLAIN: no bottleneck tail -- out = act(post_scale * (DCN + bias) + post_shift), NCHW.
+template <int DIL, int CG, bool POST, bool XN = false, bool PLAIN = false>
 __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   constexpr int CT = 2 * CG;             // channels = Co = Co2
   constexpr int NPH = CT / 32;           // phases
@@ -177,22 +173,44 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   // ---- window staging: quad q of window position pos -> LDS [q][pos]; 8 consecutive lanes take
   // one quad of 8 consecutive positions (each wave-instruction covers 8 whole 128-B lines of x,
   // and 8 consecutive lanes write 8 different LDS banks quads).  Outside the image: zeros.
+  // NCHW (XN): element e = one 16-byte segment (4 window columns) of one window row of one of
+  // the phase's 32 channels, segments fastest (a row's 96 bytes are contiguous); the store
+  // scatters its 4 values to the 4 positions' slots of channel quad ch/4.  W % 4 == 0 and
+  // wx0 % 4 == 0, so a segment lies wholly inside or wholly outside the image.
+  static_assert(!XN || (WC % 4 == 0 && 32 * WR * (WC / 4) == NT * NWI), "NCHW window staging");
   f32x4 wv[NWI] = {};
   auto load_window = [&](int g) {
 #pragma unroll
     for (int i = 0; i < NWI; ++i) {
-      const int e = tid + NT * i, q = (e >> 3) & 7, pos = (e & 7) | ((e >> 6) << 3);
-      const int wy = wy0 + pos / WC, wx = wx0 + pos % WC;
-      const bool ok = pos < WR * WC && wy >= 0 && wy < H && wx >= 0 && wx < W;
-      const int off = ok ? ((wy * W + wx) * C + 4 * q) * 4 : img_bytes;
-      if (!(dbg & 32)) wv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, g * 128, 0));
+      const int e = tid + NT * i;
+      if constexpr (XN) {
+        const int seg = e % (WC / 4), rest = e / (WC / 4), row = rest % WR, ch = rest / WR;
+        const int wy = wy0 + row, wx = wx0 + 4 * seg;
+        const bool ok = wy >= 0 && wy < H && wx >= 0 && wx < W;
+        const int off = ok ? (((g * 32 + ch) * H + wy) * W + wx) * 4 : img_bytes;
+        if (!(dbg & 32)) wv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+      } else {
+        const int q = (e >> 3) & 7, pos = (e & 7) | ((e >> 6) << 3);
+        const int wy = wy0 + pos / WC, wx = wx0 + pos % WC;
+        const bool ok = pos < WR * WC && wy >= 0 && wy < H && wx >= 0 && wx < W;
+        const int off = ok ? ((wy * W + wx) * C + 4 * q) * 4 : img_bytes;
+        if (!(dbg & 32)) wv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, g * 128, 0));
+      }
     }
   };
   auto store_window = [&]() {
 #pragma unroll
     for (int i = 0; i < NWI; ++i) {
-      const int e = tid + NT * i, q = (e >> 3) & 7, pos = (e & 7) | ((e >> 6) << 3);
-      *reinterpret_cast<f32x4 *>(sWin + (q * NPOS + pos) * 16) = wv[i];
+      const int e = tid + NT * i;
+      if constexpr (XN) {
+        const int seg = e % (WC / 4), rest = e / (WC / 4), row = rest % WR, ch = rest / WR;
+        float *dst = reinterpret_cast<float *>(sWin + ((ch >> 2) * NPOS + row * WC + 4 * seg) * 16) + (ch & 3);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) dst[4 * u] = wv[i][u];
+      } else {
+        const int q = (e >> 3) & 7, pos = (e & 7) | ((e >> 6) << 3);
+        *reinterpret_cast<f32x4 *>(sWin + (q * NPOS + pos) * 16) = wv[i];
+      }
     }
   };
 
@@ -281,7 +299,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
         const float w = (float)(px - DIL + j * DIL) + ow;
         const int hl = (int)floorf(h), wl = (int)floorf(w);
         // pos < 0 only for valid samples; corners outside the image carry weight 0, read as 0
-        const int rb = C * 4, qo = (g * 8 + 2 * kr) * 16;
+        const int rb = XN ? 4 : C * 4, qo = XN ? (g * 32 + 8 * kr) * P * 4 : (g * 8 + 2 * kr) * 16;
         int o[4];
         o[0] = (hl >= 0 && wl >= 0) ? (hl * W + wl) * rb + qo : img_bytes;
         o[1] = (hl >= 0 && wl + 1 <= W - 1) ? (hl * W + wl + 1) * rb + qo : img_bytes;
@@ -291,8 +309,17 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
 #pragma unroll
         for (int cc = 0; cc < 4; ++cc)
 #pragma unroll
-          for (int h2 = 0; h2 < 2; ++h2)
-            gq[cc][h2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o[cc], h2 * 16, 0));
+          for (int h2 = 0; h2 < 2; ++h2) {
+            if constexpr (XN) {  // 8 channel planes; an invalid corner stays past the image
+              const int pl = o[cc] == img_bytes ? 0 : P * 4;
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                gq[cc][h2][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                    xr, o[cc] + (4 * h2 + u) * pl, 0, 0));
+            } else {
+              gq[cc][h2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, o[cc], h2 * 16, 0));
+            }
+          }
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2)
 #pragma unroll
@@ -350,13 +377,19 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       if (k == t0 && k + TPP < K) load_pass(g, k + TPP);
     }
     if (c + 1 < NCH) issue_a(c + 1, nxt);
-    if (NPH == 2 && c == 3 && tid < WR * WC) {
+    if (NPH == 2 && c == 3 && !XN && tid < WR * WC) {
       const int wy = wy0 + tid / WC, wx = wx0 + tid % WC;
       const bool ok = wy >= 0 && wy < H && wx >= 0 && wx < W;
       pf_win = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
           xr, ok ? (wy * W + wx) * C * 4 : img_bytes, 128, 0));
     }
-    if (c == NCH - 6 && a.residual) {
+    if (NPH == 2 && c == 3 && XN && tid < 32 * WR) {  // one dword per window row of group 1
+      const int wy = wy0 + (tid % WR);
+      const bool ok = wy >= 0 && wy < H && wx0 + 4 >= 0;
+      pf_win = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+          xr, ok ? (((32 + tid / WR) * H + wy) * W + max(wx0, 0)) * 4 : img_bytes, 0, 0));
+    }
+    if (!PLAIN && c == NCH - 6 && a.residual) {
       const int yy = min(y0 + (tid & 7), H - 1), co2 = min(tid >> 3, a.Co2 - 1);
       pf_res = a.residual[((long)(n * a.Co2 + co2) * H + yy) * W + x0];
     }
@@ -374,6 +407,32 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   }
   if constexpr (NCH % 2) step(NCH - 1, sA0, sA1);
   asm volatile("" ::"v"(pf_res));
+
+  if constexpr (PLAIN) {
+    // ---- op-level DCN: act(post_scale * (acc + bias) + post_shift) -> LDS [co][px] -> NCHW rows
+    // (the window is free: every wave passed the last chunk's barrier)
+    float *sO = reinterpret_cast<float *>(sWin);
+#pragma unroll
+    for (int m = 0; m < NCO; ++m) {
+      const int co = 16 * m + 4 * kr;
+      const f32x4 bs = a.bias ? *reinterpret_cast<const f32x4 *>(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 sc = a.post_scale ? *reinterpret_cast<const f32x4 *>(a.post_scale + co) : f32x4{1.f, 1.f, 1.f, 1.f};
+      const f32x4 sh = a.post_scale ? *reinterpret_cast<const f32x4 *>(a.post_shift + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        sO[(co + r) * OP + wave * 16 + jj] = act_f((acc[m][r] + bs[r]) * sc[r] + sh[r], a.act);
+    }
+    __syncthreads();
+    constexpr int EPP = CT * TR * (TC / 4) / NT;  // 4-pixel items per thread
+#pragma unroll
+    for (int i = 0; i < EPP; ++i) {
+      const int e = tid + NT * i, co = e >> 5, qi = e & 31, yy = y0 + (qi >> 2), xx = x0 + 4 * (qi & 3);
+      if (yy < H && xx < W)
+        *reinterpret_cast<f32x4 *>(a.out + ((long)(n * CT + co) * H + yy) * W + xx) =
+            *reinterpret_cast<const f32x4 *>(sO + co * OP + (qi >> 2) * 16 + 4 * (qi & 3));
+    }
+    return;
+  }
 
   // ---- epilogue items (4 pixels x 1 channel): addresses, bias and identity loads, issued before
   // the conv3 tail so their latency overlaps its weight DMA and MFMAs
@@ -637,9 +696,11 @@ int dcn_tile_supported(int c, int co, int co2, int kh, int kw, int stride, int p
 }
 
 int dcn_tile_launch(const DcnTileArgs &a, hipStream_t stream) {
-  if (!dcn_tile_supported(a.C, a.Co, a.Co2, 3, 3, 1, a.dil, a.dil, a.dg, 1, a.W))
+  if (!dcn_tile_supported(a.C, a.Co, a.plain ? a.Co : a.Co2, 3, 3, 1, a.dil, a.dil, a.dg, 1, a.W))
     return AANET_EUNSUPPORTED;
-  if (!a.x || !a.offset || !a.mask || !a.wsplit || !a.tail_wsplit || !a.out) return AANET_EINVAL;
+  if (a.plain && (a.post_wsplit || a.csa_out || a.residual)) return AANET_EINVAL;
+  if (!a.x || !a.offset || !a.mask || !a.wsplit || (!a.plain && !a.tail_wsplit) || !a.out)
+    return AANET_EINVAL;
   if (a.post_scale && !a.post_shift) return AANET_EINVAL;
   if (a.csa_out) {
     if (a.num_up < 0 || a.num_up > 2) return AANET_EUNSUPPORTED;
@@ -669,6 +730,19 @@ int dcn_tile_launch(const DcnTileArgs &a, hipStream_t stream) {
   DcnTileArgs b = a;
   b.dbg = dbg;
   if (a.post_wsplit && a.C != 64) return AANET_EUNSUPPORTED;
+  const dim3 grid((unsigned)(a.N * tiles));
+  if (a.plain) {
+    if (a.C == 64 && a.x_nchw)
+      hipLaunchKernelGGL((dcn_tile_kernel<2, 32, false, true, true>), grid, dim3(NT), 0, stream, b);
+    else if (a.C == 64)
+      hipLaunchKernelGGL((dcn_tile_kernel<2, 32, false, false, true>), grid, dim3(NT), 0, stream, b);
+    else if (a.x_nchw)
+      hipLaunchKernelGGL((dcn_tile_kernel<2, 16, false, true, true>), grid, dim3(NT), 0, stream, b);
+    else
+      hipLaunchKernelGGL((dcn_tile_kernel<2, 16, false, false, true>), grid, dim3(NT), 0, stream, b);
+    return aanet_launch_status();
+  }
+  if (a.x_nchw) return AANET_EUNSUPPORTED;  // the bottleneck tail reads conv1's NHWC output
   if (a.C == 64 && a.post_wsplit)
     hipLaunchKernelGGL((dcn_tile_kernel<2, 32, true>), dim3((unsigned)(a.N * tiles)), dim3(NT), 0, stream, b);
   else if (a.C == 64)

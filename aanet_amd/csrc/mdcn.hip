@@ -354,26 +354,17 @@ __host__ __device__ inline long split_frag_count(int co, int cg, int kk, int gro
   return (long)groups * ((cog + 63) / 64) * kk * (cg / 32) * 4 * 3 * 64;
 }
 
-// Activations are split by truncation, two values at a time: h = the upper 16 bits of x, r = x - h
-// (exact, <= 16 significant bits), m = the upper 16 bits of r, l = r - m (exact, <= 8 significant
-// bits, so its upper half IS its bf16 value): x = h + m + l exactly.  v_perm_b32 packs two upper
-// halves into one bf16x2 register: 11 VALU ops per two values.
-__device__ __forceinline__ unsigned hi_pair(float a, float b) {  // (bf16 hi(a), bf16 hi(b))
-  return __builtin_amdgcn_perm(__builtin_bit_cast(unsigned, b), __builtin_bit_cast(unsigned, a), 0x07060302u);
-}
-__device__ __forceinline__ float trunc16(float a) {
-  return __builtin_bit_cast(float, __builtin_bit_cast(unsigned, a) & 0xffff0000u);
-}
+// Activations are split two values at a time by common.h split_pair (x = h + m + l exactly).
 __device__ __forceinline__ void split3(f32x4 v, bf16x4 &h, bf16x4 &m, bf16x4 &l) {
   typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
   u32x2 hh, mm, ll;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const float x0 = v[2 * i], x1 = v[2 * i + 1];
-    hh[i] = hi_pair(x0, x1);
-    const float r0 = x0 - trunc16(x0), r1 = x1 - trunc16(x1);
-    mm[i] = hi_pair(r0, r1);
-    ll[i] = hi_pair(r0 - trunc16(r0), r1 - trunc16(r1));
+    unsigned a, b, c;
+    split_pair(v[2 * i], v[2 * i + 1], a, b, c);
+    hh[i] = a;
+    mm[i] = b;
+    ll[i] = c;
   }
   h = __builtin_bit_cast(bf16x4, hh);
   m = __builtin_bit_cast(bf16x4, mm);
@@ -2017,7 +2008,9 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
       if (wc >= rows || gy < 0 || gy >= a.H || gxp < 0 || gxp >= a.W) continue;
       const long o = ((long)n * HW + (long)gy * a.W + gxp) * C + cb0 + wc;
       const long long v = sAcc[e];
-      if (!v) continue;
+      // a non-finite bound (scale = NaN) converts every contribution to 0: add the NaN read-back
+      // anyway (float mode), so grad_x is poisoned like the reference's float col2im
+      if (!v && (DET || inv == inv)) continue;
       if (DET)
         atomicAdd(reinterpret_cast<unsigned long long *>(gxi + o), (unsigned long long)v);
       else
@@ -2889,7 +2882,7 @@ extern "C" int aanet_mdcn_pw_f32(const float *x, const float *offset, long offse
   // the deformable bottleneck tail of the aggregation: LDS-window form (dcn_tile.hip)
   if (!generic && a.split && layout == 1 && a.Ho == h && a.Wo == w &&
       dcn_tile_supported(c, co, co2, kh, kw, stride, pad, dil, dg, 1, w)) {
-    DcnTileArgs t;
+    DcnTileArgs t{};
     t.x = x;
     t.offset = a.offset;
     t.off_bs = a.off_bs;
@@ -2959,8 +2952,45 @@ extern "C" int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset,
                          mask_scale, weight, bias, post_scale, post_shift, act, out, n, c, h, w,
                          co, kh, kw, stride, pad, dil, groups, dg);
   set_split(a, layout, weight_packed);
-  a.layout = layout & ~(AANET_CONV_EXACT_F32 | AANET_CONV_WEIGHTS_SPLIT);
+  const bool generic = (layout & AANET_CONV_GENERIC_DCN) != 0;
+  a.layout = layout & ~(AANET_CONV_EXACT_F32 | AANET_CONV_WEIGHTS_SPLIT | AANET_CONV_GENERIC_DCN);
+  // the aggregation's deformable convs (3x3, dil 2, two groups of 16 / 32 channels): LDS-window
+  // form with the plain epilogue (dcn_tile.hip), NCHW or channels-last x, NCHW out
+  if (!generic && a.split && (a.layout == 0 || a.layout == 1) && groups == 1 && a.Ho == h &&
+      a.Wo == w && dcn_tile_supported(c, co, co, kh, kw, stride, pad, dil, dg, 1, w)) {
+    DcnTileArgs t{};
+    t.x = x;
+    t.offset = a.offset;
+    t.off_bs = a.off_bs;
+    t.mask = a.mask;
+    t.mask_bs = a.mask_bs;
+    t.mask_logits = mask_logits;
+    t.mask_scale = mask_scale;
+    t.wsplit = a.wsplit;
+    t.bias = bias;
+    t.post_scale = post_scale;
+    t.post_shift = post_shift;
+    t.act = act;
+    t.out = out;
+    t.N = n;
+    t.C = c;
+    t.H = h;
+    t.W = w;
+    t.Co = co;
+    t.Co2 = co;
+    t.dil = dil;
+    t.dg = dg;
+    t.x_nchw = a.layout == 0;
+    t.plain = 1;
+    const int rc = dcn_tile_launch(t, as_hip(stream));
+    if (rc != AANET_EUNSUPPORTED) return rc;
+  }
   return launch_fwd<1>(a, weight_packed, as_hip(stream));
+}
+
+extern "C" int aanet_mdcn_window_fwd_supported(int c, int co, int kh, int kw, int stride, int pad,
+                                               int dil, int groups, int dg, int w) {
+  return groups == 1 && dcn_tile_supported(c, co, co, kh, kw, stride, pad, dil, dg, 1, w);
 }
 
 extern "C" int aanet_conv_weight_pack_f32(const float *weight, float *weight_packed, int co,

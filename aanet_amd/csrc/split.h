@@ -9,24 +9,17 @@
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// (bf16 hi(a), bf16 hi(b)) packed into one register
-__device__ __forceinline__ unsigned hi_pair(float a, float b) {
-  return __builtin_amdgcn_perm(__builtin_bit_cast(unsigned, b), __builtin_bit_cast(unsigned, a), 0x07060302u);
-}
-__device__ __forceinline__ float trunc16(float a) {
-  return __builtin_bit_cast(float, __builtin_bit_cast(unsigned, a) & 0xffff0000u);
-}
-// 8 values -> their three exact bf16 pieces (activations: truncation split)
+// 8 values -> their three exact bf16 pieces (activations: common.h split_pair)
 __device__ __forceinline__ void split8(const float (&v)[8], bf16x8 (&b)[3]) {
   typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
   u32x4_t hh, mm, ll;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const float x0 = v[2 * i], x1 = v[2 * i + 1];
-    hh[i] = hi_pair(x0, x1);
-    const float r0 = x0 - trunc16(x0), r1 = x1 - trunc16(x1);
-    mm[i] = hi_pair(r0, r1);
-    ll[i] = hi_pair(r0 - trunc16(r0), r1 - trunc16(r1));
+    unsigned h, m, l;
+    split_pair(v[2 * i], v[2 * i + 1], h, m, l);
+    hh[i] = h;
+    mm[i] = m;
+    ll[i] = l;
   }
   b[0] = __builtin_bit_cast(bf16x8, hh);
   b[1] = __builtin_bit_cast(bf16x8, mm);

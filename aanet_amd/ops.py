@@ -209,15 +209,52 @@ class DispWarpFunction(Function):
 
 
 # ------------------------------------------------------- modulated deformable conv ------
+def window_fwd_ok(C, Co, kh, kw, stride, padding, dilation, groups, deformable_groups, W):
+    """Whether the LDS-window DCN kernel takes an op-level forward shape
+    (aanet_mdcn_window_fwd_supported): the aggregation's deformable convs -- 3x3, stride 1,
+    padding = dilation = 2, one conv group, two deformable groups of 32 or 16 channels
+    (C = Co = 64 or 32), W % 4 == 0."""
+    return bool(_lib.lib().aanet_mdcn_window_fwd_supported(C, Co, kh, kw, stride, padding, dilation,
+                                                           groups, deformable_groups, W))
+
+
+_SPLIT_CACHE = {}
+
+
+def _split_weight(weight):
+    """pack_weight_split(weight), cached per (storage, version): an optimizer step bumps the
+    version, so training re-packs once per step; eval packs once."""
+    key = (weight.data_ptr(), weight._version, tuple(weight.shape), weight.device)
+    wp = _SPLIT_CACHE.get(key)
+    if wp is None:
+        if len(_SPLIT_CACHE) >= 64:
+            _SPLIT_CACHE.clear()
+        wp = _SPLIT_CACHE[key] = pack_weight_split(weight)
+    return wp
+
+
 def mdcn_forward(x, offset, mask, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
-                 deformable_groups=1, out=None):
-    """deform_conv_cuda.cpp:490-569 -> [N, Co, Ho, Wo]."""
+                 deformable_groups=1, out=None, algo="auto"):
+    """deform_conv_cuda.cpp:490-569 -> [N, Co, Ho, Wo].
+
+    algo "auto": the aggregation's DCN shapes (window_fwd_ok) run the LDS-window kernel on the
+    split-bf16 contraction (weights packed by pack_weight_split, cached per weight version),
+    the rest the generic engine (aanet_mdcn_fwd_f32); "generic" forces the latter."""
     require_gpu(x, offset, mask, weight, bias, names=("input", "offset", "mask", "weight", "bias"))
     N, C, H, W = x.shape
     Co, _, kh, kw = weight.shape
     Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
     if out is None:
         out = torch.empty((N, Co, Ho, Wo), device=x.device, dtype=x.dtype)
+    if algo == "auto" and not _lib._exact_f32 and \
+            window_fwd_ok(C, Co, kh, kw, stride, padding, dilation, groups, deformable_groups, W):
+        wp = _split_weight(weight)
+        K = kh * kw
+        call("aanet_mdcn_fwd_fused_f32", ptr(x), ptr(offset), 2 * deformable_groups * K * Ho * Wo,
+             ptr(mask), deformable_groups * K * Ho * Wo, 0, 1.0, ptr(wp), 1, ptr(bias), None, None,
+             0, ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation, groups,
+             deformable_groups, _lib.CONV_WEIGHTS_SPLIT, stream_of(x))
+        return out
     call("aanet_mdcn_fwd_f32", ptr(x), ptr(offset), ptr(mask), ptr(weight), ptr(bias), ptr(out),
          N, C, H, W, Co, kh, kw, stride, padding, dilation, groups, deformable_groups, stream_of(x))
     return out

@@ -619,8 +619,10 @@ DCN_SHAPES = [("agg_s0", 64, 128, 416, 1), ("agg_s1", 32, 64, 208, 1), ("agg_s2"
 
 
 def dcn_sweep_main(args, device, rank):
-    """C4 microbench: the drop-in modulated DCN entry points (aanet_mdcn_fwd_f32 = the reference's
-    modulated_deform_conv_cuda_forward; aanet_mdcn_bwd_f32 / _det_f32 = ..._backward) per shape,
+    """C4 microbench: the modulated DCN op (ops.mdcn_forward = the reference's
+    modulated_deform_conv_cuda_forward: the LDS-window kernel for the aggregation shapes,
+    `fwd_generic_us` the generic engine of aanet_mdcn_fwd_f32; aanet_mdcn_bwd_f32 / _det_f32 =
+    ..._backward) per shape,
     B=--batch, offsets N(0, 0.5^2) (fractional, some out of the image), mask U(0, 1).
     Flops: forward 2*B*Ho*Wo*Co*C*9 (the MFMA contraction; bilinear lerps excluded); backward
     counts dgrad + wgrad contractions (2x the forward).  One JSON line per shape on rank 0, then
@@ -643,6 +645,8 @@ def dcn_sweep_main(args, device, rank):
         out = torch.empty((B, C, Ho, Wo), device=device)
         go = torch.randn((B, C, Ho, Wo), device=device, generator=gen)
         fwd = lambda: ops.mdcn_forward(x, off, mask, w, None, stride, pad, dil, 1, dg, out=out)  # noqa: E731
+        fwd_gen = lambda: ops.mdcn_forward(x, off, mask, w, None, stride, pad, dil, 1, dg, out=out,  # noqa: E731
+                                           algo="generic")
         bwd = lambda: ops.mdcn_backward(x, off, mask, w, go, False, stride, pad, dil, 1, dg,  # noqa: E731
                                         deterministic=False)
         bwd_det = lambda: ops.mdcn_backward(x, off, mask, w, go, False, stride, pad, dil, 1, dg,  # noqa: E731
@@ -650,9 +654,12 @@ def dcn_sweep_main(args, device, rank):
         bwd_glob = lambda: ops.mdcn_backward(x, off, mask, w, go, False, stride, pad, dil, 1, dg,  # noqa: E731
                                              deterministic=False, algo="global")
         flops = 2.0 * B * Ho * Wo * C * C * k * k
-        ms_f, ms_b, ms_d, ms_g = (time_events(f, iters, stream) for f in (fwd, bwd, bwd_det, bwd_glob))
+        ms_f, ms_fg, ms_b, ms_d, ms_g = (time_events(f, iters, stream)
+                                         for f in (fwd, fwd_gen, bwd, bwd_det, bwd_glob))
         line = {"bench": "dcn_sweep (C4)", "shape": name, "input": [B, C, H, W], "stride": stride,
-                "deformable_groups": dg, "dilation": dil, "fwd_us": ms_f * 1e3, "bwd_us": ms_b * 1e3,
+                "deformable_groups": dg, "dilation": dil, "fwd_us": ms_f * 1e3,
+                "fwd_window": ops.window_fwd_ok(C, C, k, k, stride, pad, dil, 1, dg, W),
+                "fwd_generic_us": ms_fg * 1e3, "bwd_us": ms_b * 1e3,
                 "bwd_det_us": ms_d * 1e3, "bwd_global_atomic_us": ms_g * 1e3,
                 "fwd_tflops": flops / ms_f / 1e9, "bwd_tflops": 2 * flops / ms_b / 1e9,
                 "fwd_frac_f32_mfma": flops / ms_f / 1e9 / FP32_MFMA_PEAK_TF,

@@ -143,7 +143,13 @@ int aanet_mdcn_fwd_f32(const float *x, const float *offset, const float *mask, c
  *   - epilogue: y = act(post_scale[co] * (conv + bias[co]) + post_shift[co]); act 0 none,
  *     1 ReLU, 2 LeakyReLU(0.2).  post_scale / post_shift may be NULL (identity);
  *   - weight_packed != 0: weight is in the [kh][kw][co][c/groups] layout produced by
- *     aanet_conv_weight_pack_f32 (coalesced K-chunk loads); 0: reference [co][c/groups][kh][kw]. */
+ *     aanet_conv_weight_pack_f32 (coalesced K-chunk loads); 0: reference [co][c/groups][kh][kw];
+ *   - layout: AANET_LAYOUT_NCHW or AANET_LAYOUT_IN_NHWC, plus AANET_CONV_WEIGHTS_SPLIT when the
+ *     weight is an aanet_conv_weight_pack_split_f32 buffer (split-bf16 contraction).  With split
+ *     weights the shapes of aanet_mdcn_window_fwd_supported run the LDS-window kernel (NCHW or
+ *     channels-last x, NCHW out); AANET_CONV_GENERIC_DCN forces the generic engine.
+ * This is also the op-level forward of the aggregation's DCNs (mask_logits = 0, separate
+ * offset / mask tensors): aanet_amd.ops.mdcn_forward packs the weight and calls it. */
 int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset, long offset_batch_stride,
                              const float *mask, long mask_batch_stride, int mask_logits,
                              float mask_scale, const float *weight, int weight_packed,
@@ -152,6 +158,12 @@ int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset, long offset_ba
                              int n, int c, int h, int w, int co, int kh, int kw, int stride,
                              int pad, int dil, int groups, int dg, int layout,
                              aanet_stream_t stream);
+
+/* 1 when aanet_mdcn_fwd_fused_f32 with split weights runs the LDS-window DCN kernel for this
+ * shape (output size = input size): 3x3, stride 1, pad = dil = 2, groups 1, dg 2, c = co = 64 or
+ * 32, w % 4 == 0 -- the aggregation's deformable convs (nets/deform.py:216-226). */
+int aanet_mdcn_window_fwd_supported(int c, int co, int kh, int kw, int stride, int pad, int dil,
+                                    int groups, int dg, int w);
 
 /* Plain convolution on the same implicit-GEMM engine, for the eval fast path of every other
  * conv in the ISA/CSA blocks (nets/deform.py:6-14 conv1x1/conv3x3, nets/deform.py:70-72

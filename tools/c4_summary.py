@@ -21,7 +21,8 @@ for l in open(os.path.join(src, "sweep.jsonl")):
         d = json.loads(l)
         if "shape" in d:
             lines.append(f"{d['shape']:8s} in {d['input']} s{d['stride']}: fwd {d['fwd_us']:8.1f} us "
-                         f"({d['fwd_tflops']:5.1f} TF/s, {d['fwd_frac_f32_mfma']:.2f} of f32 MFMA)  "
+                         f"({d['fwd_tflops']:5.1f} TF/s, {d['fwd_frac_f32_mfma']:.2f} of f32 MFMA"
+                         f"{', window' if d.get('fwd_window') else ''}; generic {d.get('fwd_generic_us', 0):.1f} us)  "
                          f"bwd {d['bwd_us']:8.1f} us  bwd det {d['bwd_det_us']:8.1f} us")
         else:
             lines.append(f"num_scales {d['num_scales']}: fwd {d['fwd_us']:.1f} us, fwd+bwd {d['fwd_bwd_us']:.1f} us")
