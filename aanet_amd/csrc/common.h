@@ -29,17 +29,14 @@ __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
 
 __device__ __forceinline__ int div_up(int a, int b) { return (a + b - 1) / b; }
 
-// ---- split-bf16 activations: two fp32 values -> their three exact bf16 pieces each, x = h + m + l.
-// h = RNE(x) (v_cvt_pk_bf16_f32, both values in one op); r = x - h is exactly representable and is
-// formed by v_dot2c_f32_bf16 of the packed h with (-1, 0) / (0, -1) accumulated onto x (each
-// product and the sum exact); m = RNE(r); l = r - m the same way (|l| <= 2^-17 |x| with at most 8
-// significant bits, so RNE(l) = l).  7 VALU per two values (the truncation split, upper halves by
-// v_perm_b32 and residuals by and + sub, was 11).  |h| <= |x| rounds up only for |x| within half a
-// bf16 ulp of FLT_MAX.  AANET_SPLIT_TRUNC builds the truncation form (A/B).
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
+// ---- split-bf16 activations: two fp32 values -> their three exact bf16 pieces each, x = h + m + l,
+// by truncation: h = the upper 16 bits of x, r = x - h (exact, <= 16 significant bits), m = the
+// upper 16 bits of r, l = r - m (exact, <= 8 significant bits, so its upper half IS its bf16
+// value); v_perm_b32 packs two upper halves into one bf16x2 register: 11 VALU per two values.
+// (A 7-op form -- h = v_cvt_pk_bf16_f32, residuals by v_dot2c_f32_bf16 against (-1, 0) -- is NOT
+// exact on gfx950: tools/split_rne_lab.hip found h + m + l != x for about half of random fp32
+// values, i.e. v_dot2c does not return x - h exactly)
 __device__ __forceinline__ void split_pair(float a, float b, unsigned &h, unsigned &m, unsigned &l) {
-#ifdef AANET_SPLIT_TRUNC
   auto hi2 = [](float x, float y) {
     return __builtin_amdgcn_perm(__builtin_bit_cast(unsigned, y), __builtin_bit_cast(unsigned, x), 0x07060302u);
   };
@@ -48,19 +45,6 @@ __device__ __forceinline__ void split_pair(float a, float b, unsigned &h, unsign
   const float r0 = a - t16(a), r1 = b - t16(b);
   m = hi2(r0, r1);
   l = hi2(r0 - t16(r0), r1 - t16(r1));
-#else
-  const bf16x2_t nlo = {(__bf16)-1.f, (__bf16)0.f}, nhi = {(__bf16)0.f, (__bf16)-1.f};
-  const bf16x2_t hp = __builtin_convertvector((f32x2_t){a, b}, bf16x2_t);
-  const float ra = __builtin_amdgcn_fdot2_f32_bf16(hp, nlo, a, false);
-  const float rb = __builtin_amdgcn_fdot2_f32_bf16(hp, nhi, b, false);
-  const bf16x2_t mp = __builtin_convertvector((f32x2_t){ra, rb}, bf16x2_t);
-  const float la = __builtin_amdgcn_fdot2_f32_bf16(mp, nlo, ra, false);
-  const float lb = __builtin_amdgcn_fdot2_f32_bf16(mp, nhi, rb, false);
-  const bf16x2_t lp = __builtin_convertvector((f32x2_t){la, lb}, bf16x2_t);
-  h = __builtin_bit_cast(unsigned, hp);
-  m = __builtin_bit_cast(unsigned, mp);
-  l = __builtin_bit_cast(unsigned, lp);
-#endif
 }
 
 static inline int host_div_up(long a, long b) { return (int)((a + b - 1) / b); }

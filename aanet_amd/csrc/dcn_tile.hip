@@ -147,6 +147,9 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kr = lane >> 4, jj = lane & 15;
   const int H = a.H, W = a.W, C = a.C;
+#ifdef AANET_DCN_SETPRIO  // A/B: static priority for the second-dispatched half (MI355X_MICROARCH.md)
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
 #ifdef AANET_DEBUG_SWITCHES
   const int dbg = a.dbg;  // timing-attribution switches (debug build only)
 #else
