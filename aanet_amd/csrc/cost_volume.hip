@@ -696,10 +696,14 @@ __global__ __launch_bounds__(256) void shift_volume_band_kernel(const float *__r
   }
 }
 
-// rows per band: 8, fewer when the band's two LDS rows would exceed 64 KB (so S4 = rows * W / 4
-// <= 2048: the band kernel's 8 thread slots)
+// rows per band: 16 (round 5: C5 concat 283-285 -> 278-279 us against 8 rows, difference
+// unchanged; 24 rows: no better), fewer when the band's two LDS rows would exceed 64 KB (so
+// S4 = rows * W / 4 <= 2048: the band kernel's 8 thread slots)
+#ifndef AANET_BAND_ROWS
+#define AANET_BAND_ROWS 16
+#endif
 int band_rows(int w) {
-  int yb = 8;
+  int yb = AANET_BAND_ROWS;
   while (yb > 1 && 2L * yb * w * 4 > 64 * 1024) yb >>= 1;
   return yb;
 }

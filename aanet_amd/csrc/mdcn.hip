@@ -16,6 +16,7 @@
 #include "common.h"
 #include "dcn_tile.h"
 #include "pointwise.h"
+#include "small_conv.h"
 
 #include <cstdio>
 #include <stdlib.h>
@@ -2806,6 +2807,30 @@ extern "C" int aanet_conv2d_fused_f32(const float *x, const float *weight, const
   a.residual = residual;
   set_split(a, layout, weight_packed);
   a.layout = layout & ~(AANET_CONV_EXACT_F32 | AANET_CONV_WEIGHTS_SPLIT);
+  // few-channel convs (Cin <= 6 or Co == 1): the direct VALU kernel (small_conv.hip)
+  if ((a.layout == 0 || a.layout == 1) && groups == 1 && kh == kw && !check_shapes(a)) {
+    DirectArgs d;
+    d.x = x;
+    d.w = weight;
+    d.bias = bias;
+    d.post_scale = post_scale;
+    d.post_shift = post_shift;
+    d.residual = residual;
+    d.out = out;
+    d.act = act;
+    d.packed = weight_packed != 0;
+    d.in_nhwc = a.layout & 1;
+    d.N = n;
+    d.C = c;
+    d.H = h;
+    d.W = w;
+    d.Co = co;
+    d.Ho = a.Ho;
+    d.Wo = a.Wo;
+    d.pad = pad;
+    const int rc = conv_direct_launch(d, kh, stride, dil, as_hip(stream));
+    if (rc != AANET_EUNSUPPORTED) return rc;
+  }
   if (a.split && a.layout >= 0 && a.layout <= 3 && !check_shapes(a) &&
       pw_conv_supported(c, co, kh, kw, stride, pad, groups, (long)n * h * w, a.layout >> 1, h * w)) {
     PwArgs p;  // 1x1: the streaming kernel (pointwise.hip)

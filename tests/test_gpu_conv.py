@@ -54,6 +54,52 @@ def test_conv2d_fused_vs_torch_cpu(case, epi, packed):
     assert err <= 2e-5 * (1 + ref.abs().max().item()), err
 
 
+# the few-channel shapes of aanet_amd/csrc/small_conv.hip (direct VALU conv): AANet's first
+# feature conv (3 -> 32, 7x7 / 3), GA-Net's conv_start (3 -> 32, 3x3), the refinement stems
+# (6 / 1 -> 16) and final_conv (32 -> 1); ragged tiles (H % 8, W % 32)
+DIRECT_CASES = [
+    (2, 3, 40, 70, 32, 7, 3, 3, 1, 1),
+    (2, 3, 17, 45, 32, 3, 1, 1, 1, 1),
+    (2, 3, 17, 45, 20, 3, 1, 1, 1, 1),
+    (2, 6, 17, 45, 16, 3, 1, 1, 1, 1),
+    (2, 1, 17, 45, 16, 3, 1, 1, 1, 1),
+    (2, 32, 17, 45, 1, 3, 1, 1, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", DIRECT_CASES)
+@pytest.mark.parametrize("epi", ["plain", "bias_relu", "bn_leaky_res"])
+@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("nhwc", [False, True])
+def test_conv2d_direct_shapes_vs_torch(case, epi, packed, nhwc):
+    """Few-channel convs on the direct kernel vs torch fp64 (exact f32 FMAs: 1e-5 relative)."""
+    N, C, H, W, Co, k, s, p, d, g = case
+    if nhwc and C % 4:
+        pytest.skip("channels-last input needs C % 4 == 0")
+    gen = torch.Generator().manual_seed(7 + C + Co)
+    x = torch.randn(N, C, H, W, generator=gen)
+    w = torch.randn(Co, C, k, k, generator=gen) / (C * k * k) ** 0.5
+    b, sc, sh = torch.randn(Co, generator=gen), torch.rand(Co, generator=gen) + 0.5, torch.randn(Co, generator=gen)
+    ref = F.conv2d(x.double(), w.double(), None if epi == "plain" else b.double(), s, p, d, g)
+    res = None
+    if epi == "bn_leaky_res":
+        res = torch.randn(ref.shape, generator=gen)
+        ref = F.leaky_relu(ref * sc.double().view(1, -1, 1, 1) + sh.double().view(1, -1, 1, 1) + res.double(), 0.2)
+    elif epi == "bias_relu":
+        ref = F.relu(ref)
+    act = {"plain": None, "bias_relu": "relu", "bn_leaky_res": "leaky"}[epi]
+    wd, xd = w.to(DEV), x.to(DEV)
+    if nhwc:
+        xd = xd.contiguous(memory_format=torch.channels_last)
+    got = ops.conv2d_fused(xd, wd, None if epi == "plain" else b.to(DEV), s, p, d, g, act,
+                           None if res is None else res.to(DEV),
+                           sc.to(DEV) if epi == "bn_leaky_res" else None,
+                           sh.to(DEV) if epi == "bn_leaky_res" else None,
+                           packed_weight=ops.pack_weight(wd) if (packed or nhwc) else None).cpu().double()
+    err = (got - ref).abs().max().item()
+    assert err <= 1e-5 * (1 + ref.abs().max().item()), err
+
+
 def _packed(wd, groups, packed):
     """None (reference layout), pack_weight (exact f32 engine) or the split-bf16 buffer (falls
     back to pack_weight where the shape has no split form)."""
