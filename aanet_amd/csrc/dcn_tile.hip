@@ -527,14 +527,31 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   // above) is issued before the first use: the item loop would otherwise pay one L2/HBM round
   // trip per item and term (the stores may alias the sources, so the compiler cannot hoist them)
   f32x4 ev[EPT], eu[EPT][2][2];
-  // the CSA terms' resize ratios ih / H (PyTorch's area_pixel_compute_scale), divided once
-  float rsc[2] = {1.f, 1.f};
+  // every item of a thread has the same 4-pixel quad (qi = tid & 31; NT is a multiple of 32): the
+  // CSA source rows, segment start and row weights are computed once per thread (round 5: per
+  // item and term, in both passes, before)
+  const int qit = tid & 31, yyt = y0 + (qit >> 2), xxt = x0 + 4 * (qit & 3);
+  int urow0[2] = {0, 0}, urow1[2] = {0, 0}, us0[2] = {0, 0};
+  float uh0[2] = {1.f, 1.f}, uh1[2] = {0.f, 0.f};
+  if (csa) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
-    if (csa && j < a.num_up) rsc[j] = (float)a.up_h[j] / (float)H;
+    for (int j = 0; j < 2; ++j) {
+      if (j >= a.num_up) break;
+      const int ih = a.up_h[j], iw = a.up_w[j], r = a.up_r[j];
+      // PyTorch's area_pixel_compute_scale (ih / H) and source row, align_corners=False
+      float hr = ((float)ih / (float)H) * ((float)yyt + 0.5f) - 0.5f;
+      hr = hr < 0.f ? 0.f : hr;
+      const int h1 = (int)hr, h1p = h1 < ih - 1 ? 1 : 0;
+      urow0[j] = h1 * iw;
+      urow1[j] = (h1 + h1p) * iw;
+      us0[j] = r == 2 ? 2 * (xxt >> 2) - 1 : (xxt >> 2) - 1;
+      uh1[j] = hr - (float)h1;
+      uh0[j] = 1.f - uh1[j];
+    }
+  }
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
-    const int e = tid + NT * i, co2 = e >> 5, qi = e & 31, yy = y0 + (qi >> 2), xx = x0 + 4 * (qi & 3);
+    const int e = tid + NT * i, co2 = e >> 5, qi = e & 31;
     ev[i] = *reinterpret_cast<const f32x4 *>(sO + co2 * OP + (qi >> 2) * 16 + 4 * (qi & 3));
     if (!eok[i]) continue;
     if (csa) {
@@ -542,14 +559,10 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         if (j >= a.num_up) break;
-        const int ih = a.up_h[j], iw = a.up_w[j], r = a.up_r[j];
-        float hr = rsc[j] * ((float)yy + 0.5f) - 0.5f;
-        hr = hr < 0.f ? 0.f : hr;
-        const int h1 = (int)hr, h1p = h1 < ih - 1 ? 1 : 0;
-        const float *im = a.up[j] + plane * ih * iw;
-        const int s0 = r == 2 ? 2 * (xx >> 2) - 1 : (xx >> 2) - 1;
-        eu[i][j][0] = load_seg(im + (long)h1 * iw, iw, s0);
-        eu[i][j][1] = load_seg(im + (long)(h1 + h1p) * iw, iw, s0);
+        const int iw = a.up_w[j];
+        const float *im = a.up[j] + plane * (a.up_h[j] * iw);
+        eu[i][j][0] = load_seg(im + urow0[j], iw, us0[j]);
+        eu[i][j][1] = load_seg(im + urow1[j], iw, us0[j]);
       }
     }
   }
@@ -572,7 +585,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       if (ev[i][0] == 12345.f) a.out[eo[i]] = ev[i][1];
       continue;
     }
-    const int e = tid + NT * i, qi = e & 31, yy = y0 + (qi >> 2);
+    const int e = tid + NT * i, qi = e & 31;
     f32x4 v = ev[i];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -585,10 +598,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         if (j >= a.num_up) break;
-        float hr = rsc[j] * ((float)yy + 0.5f) - 0.5f;
-        hr = hr < 0.f ? 0.f : hr;
-        const float h1l = hr - (float)(int)hr, h0l = 1.f - h1l;
-        v += h0l * hlerp(eu[i][j][0], a.up_r[j]) + h1l * hlerp(eu[i][j][1], a.up_r[j]);
+        v += uh0[j] * hlerp(eu[i][j][0], a.up_r[j]) + uh1[j] * hlerp(eu[i][j][1], a.up_r[j]);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) v[u] = act_f(v[u], a.csa_act);

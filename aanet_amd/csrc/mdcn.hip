@@ -1181,12 +1181,33 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   // expose the HBM / L2 latency once per item.
   constexpr int EB = EPT >= 2 ? 2 : 1;
   const bool csa = TAIL && a.csa_out;
-  // the resize ratios of the CSA terms (area_pixel_compute_scale), once per thread: an IEEE
-  // division is a ~10-instruction sequence, and the item loop would repeat it per item and term
-  float rsc[2] = {0.f, 0.f};
+  // Every item of a thread has the same quad q = tid % QPR (FNT is a multiple of QPR): its pixel,
+  // and for the CSA terms the source rows, segment start and row weights, are computed once per
+  // thread here (round 5: they were recomputed per item in both passes -- an integer division and
+  // 64-bit address math per item and term); per item only the channel plane changes.
+  static_assert(FNT % QPR == 0, "items of a thread share their quad");
+  const int qt = tid % QPR;
+  const long pet = pix(4 * qt);
+  const bool qokt = quad_ok(qt);
+  int urow0[2] = {0, 0}, urow1[2] = {0, 0}, us0[2] = {0, 0};
+  float uh0[2] = {1.f, 1.f}, uh1[2] = {0.f, 0.f};
+  if (csa && qokt) {
+    const int y = (int)(pet / a.Wo), qq = (int)(pet % a.Wo) >> 2;  // Wo % 4 == 0 (launcher)
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
-    if (csa && j < a.num_up) rsc[j] = (float)a.up_h[j] / (float)a.Ho;
+    for (int j = 0; j < 2; ++j) {
+      if (j >= a.num_up) break;
+      const int ih = a.up_h[j], iw = a.up_w[j], r = a.up_r[j];
+      // PyTorch's area_pixel_compute_scale (ih / Ho) and source row, align_corners=False
+      float hr = ((float)ih / (float)a.Ho) * ((float)y + 0.5f) - 0.5f;
+      hr = hr < 0.f ? 0.f : hr;
+      const int h1 = (int)hr, h1p = h1 < ih - 1 ? 1 : 0;
+      urow0[j] = h1 * iw;
+      urow1[j] = (h1 + h1p) * iw;
+      us0[j] = r == 2 ? 2 * qq - 1 : qq - 1;
+      uh1[j] = hr - (float)h1;
+      uh0[j] = 1.f - uh1[j];
+    }
+  }
 #pragma unroll
   for (int i0 = 0; i0 < EPT; i0 += EB) {
     f32x4 ev[EB], er[EB], eu[EB][2][2];
@@ -1195,32 +1216,26 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
 #pragma unroll
     for (int b = 0; b < EB; ++b) {
       const int e = tid + (i0 + b) * FNT;
-      const int col = e / QPR, q = e % QPR, co = co0 + col;
-      eok[b] = (NE % FNT == 0 || e < NE) && co < cend_o && quad_ok(q);
+      const int col = e / QPR, co = co0 + col;
+      eok[b] = (NE % FNT == 0 || e < NE) && co < cend_o && qokt;
       if (!eok[b]) continue;
-      const long pe = pix(4 * q);
-      const long o = ((long)n * cout + co) * P + pe;
+      const long o = ((long)n * cout + co) * P + pet;
       // the channel's parameters in this load pass too: loaded in the use pass, each item
       // waited for its own
       pbi[b] = ebias ? ebias[co] : 0.f;
       psc[b] = esc ? esc[co] : 1.f;
       psh[b] = esc ? esh[co] : 0.f;
-      ev[b] = *reinterpret_cast<const f32x4 *>(sO + col * OP + 4 * q);
+      ev[b] = *reinterpret_cast<const f32x4 *>(sO + col * OP + 4 * qt);
       if (a.residual) er[b] = *reinterpret_cast<const f32x4 *>(a.residual + o);
       if (csa) {
-        const int y = (int)(pe / a.Wo), qq = (int)(pe % a.Wo) >> 2;  // Wo % 4 == 0 (launcher)
         const long plane = (long)n * cout + co;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           if (j >= a.num_up) break;
-          const int ih = a.up_h[j], iw = a.up_w[j], r = a.up_r[j];
-          float hr = rsc[j] * ((float)y + 0.5f) - 0.5f;
-          hr = hr < 0.f ? 0.f : hr;
-          const int h1 = (int)hr, h1p = h1 < ih - 1 ? 1 : 0;
-          const float *im = a.up[j] + plane * ih * iw;
-          const int s0 = r == 2 ? 2 * qq - 1 : qq - 1;
-          eu[b][j][0] = load_seg(im + (long)h1 * iw, iw, s0);
-          eu[b][j][1] = load_seg(im + (long)(h1 + h1p) * iw, iw, s0);
+          const int iw = a.up_w[j];
+          const float *im = a.up[j] + plane * (a.up_h[j] * iw);
+          eu[b][j][0] = load_seg(im + urow0[j], iw, us0[j]);
+          eu[b][j][1] = load_seg(im + urow1[j], iw, us0[j]);
         }
       }
     }
@@ -1228,9 +1243,8 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
     for (int b = 0; b < EB; ++b) {
       if (!eok[b]) continue;
       const int e = tid + (i0 + b) * FNT;
-      const int col = e / QPR, q = e % QPR, co = co0 + col;
-      const long pe = pix(4 * q);
-      const long o = ((long)n * cout + co) * P + pe;
+      const int col = e / QPR, co = co0 + col;
+      const long o = ((long)n * cout + co) * P + pet;
       const float bias = pbi[b], sc = psc[b], sh = psh[b];
       f32x4 v = ev[b];
 #pragma unroll
@@ -1244,20 +1258,16 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       if (csa) {
         // cross-scale sum of this output branch (nets/aggregation.py:387-400): the block output
         // (the identity term) + exact 2x/4x upsamplings of the coarser exchange terms, LeakyReLU
-        const int y = (int)(pe / a.Wo);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           if (j >= a.num_up) break;
-          float hr = rsc[j] * ((float)y + 0.5f) - 0.5f;
-          hr = hr < 0.f ? 0.f : hr;
-          const float h1l = hr - (float)(int)hr, h0l = 1.f - h1l;
-          v += h0l * hlerp(eu[b][j][0], a.up_r[j]) + h1l * hlerp(eu[b][j][1], a.up_r[j]);
+          v += uh0[j] * hlerp(eu[b][j][0], a.up_r[j]) + uh1[j] * hlerp(eu[b][j][1], a.up_r[j]);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) v[u] = apply_act(v[u], a.csa_act);
         *reinterpret_cast<f32x4 *>(a.csa_out + o) = v;
         // post stage: the CSA output back into the item's own slot (its B operand)
-        if constexpr (POST) *reinterpret_cast<f32x4 *>(sO + col * OP + 4 * q) = v;
+        if constexpr (POST) *reinterpret_cast<f32x4 *>(sO + col * OP + 4 * qt) = v;
       }
     }
   }
