@@ -21,7 +21,7 @@ KMAP = {"corr_volume_s0": r"corr_reg_kernel<5, 8, 2>", "disp_regress_s0": r"disp
         # the streaming 1x1 conv (pointwise.hip, input split once), NCHW input, 4 output-channel blocks, NHWC out
         "conv1x1_s0": r"pw_conv_nchw_s_kernel<64, 4, 1>",
         # the LDS-window deformable tail (dcn_tile.hip), common form (no post stage)
-        "mdcn_pw_s0": r"dcn_tile_kernel<2, 32, false>",
+        "mdcn_pw_s0": r"dcn_tile_kernel<2, 32, false, false, false>",
         # MODE, CO_T, PTT, PACKED, TAIL, SCHED, FULL, LAYOUT, CFG, PREC (1: split-bf16), HALO (= dil),
         # POST (0: no post stage)
         "conv3x3_pw_s0": r"conv_fwd_kernel<0, 64, 128, 1, 1, 1, 1, 1, 0, 1, 1, 0>",
