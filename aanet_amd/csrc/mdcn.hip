@@ -1757,10 +1757,12 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_nhwc_kernel(MdcnArgs a, cons
 // (the forward's (w1 v1 + w2 v2 + w3 v3 + w4 v4) * mask, from the corner quads the offset / mask
 // partials load anyway) go to LDS, one 16x16x4 f32 MFMA run per (tap, slice) forms the tile's
 // [64 co][16 c] product with the staged gOut tile, and it is added with float atomics into a
-// [K][Co][C] accumulator (64-byte segments; transposed into grad_weight afterwards).  The
-// deterministic mode keeps mdcn_bwd_weight_kernel: the same partials as int64 fixed-point atomics
-// (8-byte adds) took agg_s0 from 3.60 to 3.96 ms.  This
-// replaces mdcn_bwd_weight_kernel, whose 18 chunks each re-read gOut and re-gathered the corners.
+// [K][Co][C] accumulator (64-byte segments; transposed into grad_weight afterwards).  DET: the
+// same products go to an int64 fixed-point [K][Co][C] accumulator (scale det_scale[1]), so the sum
+// does not depend on the order of the tiles and the workspace holds one copy of the weight
+// gradient (round 4 stored a float partial per tile and reduced them in a fixed order: ~0.08 ms
+// faster at agg_s0, but ~0.9 GB of workspace at B = 8).  This replaces mdcn_bwd_weight_kernel,
+// whose 18 chunks each re-read gOut and re-gathered the corners.
 // dynamic LDS: sG [Co][GP], sWt [16][WTP], sCg [16][CP], sS [PT][16], sP [3][9][PT],
 // [FUSEW: sCol [16][CP]], window [WR*WC][16] int64
 constexpr int WHC = 16;  // channels per window slice
@@ -1770,6 +1772,7 @@ constexpr int WHC = 16;  // channels per window slice
 constexpr int WCP = PT + 2;
 constexpr int WKMAX = 9; // taps the sP partial buffer holds
 constexpr int WCOMAX = 64;  // output channels (the W^T slice is prefetched in registers)
+constexpr int GW_COPIES = 8; // copies of the fused weight-gradient accumulator, summed afterwards
 template <int DET, int FUSEW = 0>
 __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, const float *__restrict__ xh,
                                                                const float *__restrict__ wT,
@@ -1780,7 +1783,8 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
                                                                int WTP, long long *__restrict__ gxi,
                                                                const double *__restrict__ det_scale,
                                                                int WR, int WCc, int R,
-                                                               float *__restrict__ gwT = nullptr) {
+                                                               float *__restrict__ gwT = nullptr,
+                                                               long long *__restrict__ gwi = nullptr) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int Co = a.Co;
   float *sG = sm;                       // [Co][GP]      gOut tile
@@ -1800,6 +1804,10 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
   const long HW = (long)a.H * a.W;
   const double scale = *det_scale;
   const double inv = 1.0 / scale;
+  const double wscale = DET && FUSEW ? det_scale[1] : 1.0;  // the weight gradient's fixed point
+  // the weight-gradient accumulator copy of this workgroup (consecutive workgroups run on
+  // different XCDs: one copy per XCD keeps the atomics on one element from crossing them)
+  const long gwc = (long)(blockIdx.x & (GW_COPIES - 1)) * K * Co * C;
   const float *xn = xh + (long)n * HW * C;
   const int wy0 = ty0 - a.pad - R, wx0 = tx0 - a.pad - R;  // window origin (stride 1)
   const int nwin = WR * WCc * WHC;
@@ -1920,10 +1928,11 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
           for (int r = 0; r < 4; ++r) {
             const int co = 16 * wave + 4 * kr + r;
             if (co >= Co) continue;
-            if (DET)  // this tile's partial, stored: part[tile][g][k][co][c of the group]
-              gwT[((((long)blockIdx.x * a.dg + g) * K + k) * Co + co) * cpg + sl * WHC + jj] = wacc[r];
+            if (DET)  // int64 fixed point: the sum does not depend on the order of the tiles
+              atomicAdd(reinterpret_cast<unsigned long long *>(gwi) + gwc + ((long)k * Co + co) * C + cb0 + jj,
+                        (unsigned long long)__double2ll_rn((double)wacc[r] * wscale));
             else
-              atomicAdd(gwT + ((long)k * Co + co) * C + cb0 + jj, wacc[r]);
+              atomicAdd(gwT + gwc + ((long)k * Co + co) * C + cb0 + jj, wacc[r]);
           }
         }
       }
@@ -2030,40 +2039,20 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
   }
 }
 
-// Deterministic weight gradient of the fused window form, stage 1: part2[j][e] = sum over the
-// tiles t of chunk j (ascending) of part[t][e], e = [g][k][co][c of the group]; 8 loads in flight.
-__global__ __launch_bounds__(256) void det_tile_sum_kernel(const float *__restrict__ part,
-                                                           float *__restrict__ part2, long nt,
-                                                           long nw, long per) {
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  const long j = blockIdx.y, t0 = j * per, t1 = min(nt, t0 + per);
-  if (e >= nw) return;
-  float s = 0.f;
-  long t = t0;
-  for (; t + 8 <= t1; t += 8) {
-    float v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = part[(t + u) * nw + e];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) s += v[u];
-  }
-  for (; t < t1; ++t) s += part[t * nw + e];
-  part2[j * nw + e] = s;
-}
-
-// stage 2: grad_weight[co][g cpg + c][k] += sum over the chunks j (ascending) of part2[j][e]
-__global__ __launch_bounds__(256) void det_tile_final_kernel(const float *__restrict__ part2,
-                                                             float *__restrict__ gw, int nch, int Co,
-                                                             int C, int K, int dg) {
+// grad_weight [Co][C][K] += gwi [K][Co][C] / scale (the deterministic window form's int64
+// fixed-point weight-gradient accumulator; NaN scale -> NaN, as det_scale_kernel says)
+__global__ __launch_bounds__(256) void det_gw_final_kernel(const long long *__restrict__ gwi,
+                                                           float *__restrict__ gw, int Co, int C, int K,
+                                                           const double *__restrict__ wscale) {
   const long nw = (long)Co * C * K;
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
-  if (e >= nw) return;
-  const int cpg = C / dg;
-  const int c = (int)(e % cpg), co = (int)((e / cpg) % Co), k = (int)((e / ((long)cpg * Co)) % K),
-            g = (int)(e / ((long)cpg * Co * K));
-  float s = 0.f;
-  for (int j = 0; j < nch; ++j) s += part2[(long)j * nw + e];
-  gw[((long)co * C + g * cpg + c) * K + k] += s;
+  const double inv = 1.0 / *wscale;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < nw; e += (long)gridDim.x * 256) {
+    const int k = (int)(e % K), c = (int)((e / K) % C), co = (int)(e / ((long)K * C));
+    long long v = 0;
+#pragma unroll
+    for (int j = 0; j < GW_COPIES; ++j) v += gwi[j * nw + ((long)k * Co + co) * C + c];
+    gw[e] += (float)((double)v * inv);
+  }
 }
 
 // grad_weight [Co][C][K] += gwT [K][Co][C] (the fused window form's accumulator)
@@ -2072,7 +2061,10 @@ __global__ __launch_bounds__(256) void gw_kcoc_add_kernel(const float *__restric
   const long nw = (long)Co * C * K;
   for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < nw; e += (long)gridDim.x * 256) {
     const int k = (int)(e % K), c = (int)((e / K) % C), co = (int)(e / ((long)K * C));
-    gw[e] += gwT[((long)k * Co + co) * C + c];
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < GW_COPIES; ++j) v += gwT[j * nw + ((long)k * Co + co) * C + c];
+    gw[e] += v;
   }
 }
 
@@ -2657,17 +2649,24 @@ __global__ __launch_bounds__(256) void det_absmax_kernel(const float *__restrict
   if (threadIdx.x == 0) atomicMax(slot, max(max(red[0], red[1]), max(red[2], red[3])));
 }
 
-// scale = 2^(38 - ceil(log2 bound)): a single contribution stays below 2^38, so up to 2^25 of
+// scale[0] = 2^(38 - ceil(log2 bound)): a single contribution stays below 2^38, so up to 2^25 of
 // them can meet in one element before the int64 sum could overflow; the fixed-point step
 // (2^-38 of the largest possible contribution) is far below fp32 rounding of typical sums.
 // A non-finite bound (an inf or NaN in the weights, grad_out or mask) gives scale = NaN: the
 // fixed-point sums are then read back through 1/scale = NaN, so grad_x comes out NaN instead
 // of finite garbage from __double2ll_rn(inf/NaN) (the reference's float col2im would propagate
 // the non-finite value).
-__global__ void det_scale_kernel(const unsigned *__restrict__ bounds, double *__restrict__ scale) {
+// scale[1]: the deterministic window form's weight-gradient accumulator.  Every element is a sum
+// over the npix output pixels of gOut * column, |column| <= max|x| * max|mask| (bilinear weights
+// sum to <= 1), so the whole sum is bounded by bw = npix * bounds[1] * bounds[3] * bounds[2] and
+// 2^(62 - ceil(log2 bw)) keeps it (plus half a step per tile of rounding) inside int64.
+__global__ void det_scale_kernel(const unsigned *__restrict__ bounds, double *__restrict__ scale, long npix) {
   const double b = (double)__uint_as_float(bounds[0]) * (double)__uint_as_float(bounds[1]) *
                    (double)__uint_as_float(bounds[2]);
-  *scale = !isfinite(b) ? __builtin_nan("") : (b > 0.0 ? ldexp(1.0, 38 - (int)ceil(log2(b))) : 1.0);
+  scale[0] = !isfinite(b) ? __builtin_nan("") : (b > 0.0 ? ldexp(1.0, 38 - (int)ceil(log2(b))) : 1.0);
+  const double bw = (double)npix * (double)__uint_as_float(bounds[1]) * (double)__uint_as_float(bounds[2]) *
+                    (double)__uint_as_float(bounds[3]);
+  scale[1] = !isfinite(bw) ? __builtin_nan("") : (bw > 0.0 ? ldexp(1.0, 62 - (int)ceil(log2(bw))) : 1.0);
 }
 
 // gw[e] += sum over the splits of part[split][e], in a fixed order: workgroup = 64 consecutive
@@ -3111,13 +3110,14 @@ BwdPlan bwd_plan(const MdcnArgs &a) {
   return pl;
 }
 
-// Deterministic-backward workspace: [grad_x as int64][weight partials][bounds, scale]
+// Deterministic-backward workspace, per chunk of images (det_chunk): [grad_x as int64]
+// [weight-gradient partials (global form) | int64 [K][Co][C] accumulator (window form)]
+// [bounds, scales][x channels-last][W^T]
 struct DetLayout {
-  size_t gxi, part, bounds, scale, xh, wt, gw, wp, wp2, total;
+  size_t gxi, part, bounds, scale, xh, wt, gw, total;
 };
 
 bool bwd_nhwc_reads(const MdcnArgs &a);
-constexpr int DET_TILE_CHUNKS = 64;  // chunks of the first stage of the tile-partial reduction
 // the window form's LDS (mdcn_bwd_impl), fused weight gradient, and whether a shape takes it
 size_t win_smem(const MdcnArgs &a) {
   const int GPW = round_pitch(PT, 2), WTP = round_pitch(a.Co, 2);
@@ -3130,25 +3130,36 @@ bool win_shape_ok(const MdcnArgs &a) {
   return bwd_nhwc_reads(a) && a.stride == 1 && a.C / a.dg <= 2 * WHC && a.kh * a.kw <= WKMAX &&
          a.Co <= WCOMAX && win_smem(a) <= 160 * 1024;
 }
-long win_tiles(const MdcnArgs &a) { return (long)a.N * ((a.Ho + 7) / 8) * ((a.Wo + 7) / 8); }
 
-DetLayout det_layout(const MdcnArgs &a, const BwdPlan &pl) {
+// The deterministic backward runs over the batch in chunks of images whose int64 grad_x
+// accumulator + channels-last x (12 bytes per input element) fit DET_CHUNK_BYTES: the workspace
+// no longer grows with the batch (agg_s0 at B = 8: 377 MB unchunked).  Chunks are a fixed
+// function of the shape, so the result stays bit-reproducible.
+constexpr size_t DET_CHUNK_BYTES = (size_t)96 << 20;
+int det_chunk(const MdcnArgs &a) {
+  const size_t per = (size_t)12 * a.C * a.H * a.W;
+  size_t nc = per ? DET_CHUNK_BYTES / per : (size_t)a.N;
+  if (nc < 1) nc = 1;
+  return nc < (size_t)a.N ? (int)nc : a.N;
+}
+
+DetLayout det_layout(const MdcnArgs &a0, const BwdPlan &) {
   auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
-  DetLayout L;
+  MdcnArgs a = a0;
+  a.N = det_chunk(a0);
+  const BwdPlan pl = bwd_plan(a);
+  DetLayout L{};
   const size_t nx = (size_t)a.N * a.C * a.H * a.W;
   const size_t nw = (size_t)a.Co * a.C * a.kh * a.kw;
+  const size_t part = (size_t)pl.nsplit * nw * 4;
   L.gxi = 0;
   L.part = up(L.gxi + nx * 8);
-  L.bounds = up(L.part + (size_t)pl.nsplit * nw * 4);
+  L.gw = L.part;  // the window form's accumulator shares the region with the global form's partials
+  L.bounds = up(L.part + (part > GW_COPIES * nw * 8 ? part : GW_COPIES * nw * 8));
   L.scale = L.bounds + 16;
-  L.xh = up(L.scale + 8);  // channels-last x and wT[k][c][co] (mdcn_bwd_data_nhwc_kernel)
+  L.xh = up(L.scale + 16);  // channels-last x and wT[k][c][co] (mdcn_bwd_data_nhwc_kernel)
   L.wt = up(L.xh + nx * 4);
   L.total = up(L.wt + nw * 4);
-  if (win_shape_ok(a)) {  // the fused window form's per-tile weight-gradient partials
-    L.wp = L.total;
-    L.wp2 = up(L.wp + (size_t)win_tiles(a) * nw * 4);
-    L.total = up(L.wp2 + (size_t)DET_TILE_CHUNKS * nw * 4);
-  }
   return L;
 }
 
@@ -3164,14 +3175,14 @@ DetLayout ws_layout(const MdcnArgs &a) {
   L.wt = up(L.xh + nx * 4);
   L.bounds = up(L.wt + nw * 4);
   L.scale = L.bounds + 16;
-  L.gw = up(L.scale + 8);  // [K][Co][C] weight-gradient accumulator of the fused window form
-  L.total = up(L.gw + nw * 4);
+  L.gw = up(L.scale + 16);  // [GW_COPIES][K][Co][C] weight-gradient accumulator of the fused window form
+  L.total = up(L.gw + GW_COPIES * nw * 4);
   return L;
 }
 
 bool bwd_nhwc_reads(const MdcnArgs &a) { return a.C % 4 == 0 && (a.C / a.dg) % 4 == 0; }
 
-int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const float *weight,
+int mdcn_bwd_core(const float *x, const float *offset, const float *mask, const float *weight,
                   const float *grad_out, float *grad_x, float *grad_offset, float *grad_mask,
                   float *grad_weight, float *grad_bias, int n, int c, int h, int w, int co,
                   int kh, int kw, int stride, int pad, int dil, int groups, int dg, int det,
@@ -3243,7 +3254,12 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
                        dim3(256), 0, st, grad_out, ng, bounds + 1);
     hipLaunchKernelGGL(det_absmax_kernel, dim3(host_div_up(nm, 1024) > 512 ? 512 : host_div_up(nm, 1024)),
                        dim3(256), 0, st, mask, nm, bounds + 2);
-    hipLaunchKernelGGL(det_scale_kernel, dim3(1), dim3(1), 0, st, bounds, scale);
+    if (det && use_win) {  // max|x|: the window form's weight-gradient bound (det_scale_kernel)
+      const long nxl = (long)nx;
+      hipLaunchKernelGGL(det_absmax_kernel, dim3(host_div_up(nxl, 1024) > 512 ? 512 : host_div_up(nxl, 1024)),
+                         dim3(256), 0, st, x, nxl, bounds + 3);
+    }
+    hipLaunchKernelGGL(det_scale_kernel, dim3(1), dim3(1), 0, st, bounds, scale, (long)n * P);
   }
   const size_t smem = sizeof(float) * ((size_t)co * GP + (size_t)KC * WTP + (size_t)KC * CP + 3 * 4 * 64 +
                                       (size_t)PT * 12);
@@ -3287,19 +3303,18 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
     if (use_win) {
       const dim3 gwin((unsigned)(n * host_div_up(a.Wo, 8) * host_div_up(a.Ho, 8)), (unsigned)dg);
       if (det) {
-        float *wp = reinterpret_cast<float *>(wb + L.wp), *wp2 = reinterpret_cast<float *>(wb + L.wp2);
-        const long nw = (long)co * c * K, nt = win_tiles(a);
+        long long *gwi = reinterpret_cast<long long *>(wb + L.gw);
+        const long nw = (long)co * c * K;
+        e = hipMemsetAsync(gwi, 0, sizeof(long long) * GW_COPIES * (size_t)nw, st);
+        if (e != hipSuccess) return (int)e;
         hipLaunchKernelGGL((mdcn_bwd_data_win_kernel<1, 1>), gwin, dim3(NT), smem3, st, a, xh, wt, grad_out,
-                           grad_x, grad_offset, grad_mask, GPW, WTP, gxi, scale, WR, WCw, R, wp);
-        const long per = (nt + DET_TILE_CHUNKS - 1) / DET_TILE_CHUNKS;
-        hipLaunchKernelGGL(det_tile_sum_kernel, dim3((unsigned)host_div_up(nw, 256), DET_TILE_CHUNKS), dim3(256), 0,
-                           st, wp, wp2, nt, nw, per);
-        hipLaunchKernelGGL(det_tile_final_kernel, dim3((unsigned)host_div_up(nw, 256)), dim3(256), 0, st, wp2,
-                           grad_weight, DET_TILE_CHUNKS, co, c, K, dg);
+                           grad_x, grad_offset, grad_mask, GPW, WTP, gxi, scale, WR, WCw, R, nullptr, gwi);
+        hipLaunchKernelGGL(det_gw_final_kernel, dim3(host_div_up(nw, 256) > 1024 ? 1024 : host_div_up(nw, 256)),
+                           dim3(256), 0, st, gwi, grad_weight, co, c, K, scale + 1);
       } else {
         float *gwT = reinterpret_cast<float *>(wb + L.gw);
         const long nw = (long)co * c * K;
-        e = hipMemsetAsync(gwT, 0, sizeof(float) * (size_t)nw, st);
+        e = hipMemsetAsync(gwT, 0, sizeof(float) * GW_COPIES * (size_t)nw, st);
         if (e != hipSuccess) return (int)e;
         hipLaunchKernelGGL((mdcn_bwd_data_win_kernel<0, 1>), gwin, dim3(NT), smem3, st, a, xh, wt, grad_out,
                            reinterpret_cast<float *>(wb + L.gxi), grad_offset, grad_mask, GPW, WTP,
@@ -3365,6 +3380,40 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
     rc = aanet_launch_status();
   }
   return rc;
+}
+
+// The backward entry: the deterministic mode (det == 1) runs mdcn_bwd_core over chunks of images
+// (det_chunk) that share one workspace -- grad_x / grad_offset / grad_mask are per image, the
+// weight gradient is added per chunk in chunk order -- and the bias gradient once over the batch.
+int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const float *weight,
+                  const float *grad_out, float *grad_x, float *grad_offset, float *grad_mask,
+                  float *grad_weight, float *grad_bias, int n, int c, int h, int w, int co,
+                  int kh, int kw, int stride, int pad, int dil, int groups, int dg, int det,
+                  int algo, void *ws, size_t ws_bytes, hipStream_t st) {
+  MdcnArgs a = make_args(x, offset, -1, mask, -1, 0, 1.f, weight, nullptr, nullptr, nullptr, 0,
+                         nullptr, n, c, h, w, co, kh, kw, stride, pad, dil, groups, dg);
+  if (det != 1 || check_shapes(a) || !x || !offset || !mask || !grad_out || !grad_x || !grad_offset ||
+      !grad_mask)
+    return mdcn_bwd_core(x, offset, mask, weight, grad_out, grad_x, grad_offset, grad_mask, grad_weight,
+                         grad_bias, n, c, h, w, co, kh, kw, stride, pad, dil, groups, dg, det, algo, ws,
+                         ws_bytes, st);
+  const int nc = det_chunk(a);
+  if (ws_bytes < det_layout(a, BwdPlan{}).total) return AANET_EINVAL;
+  const long P = (long)a.Ho * a.Wo, K = (long)kh * kw;
+  const long sx = (long)c * h * w, soff = 2L * dg * K * P, sm = (long)dg * K * P, sg = (long)co * P;
+  for (int i0 = 0; i0 < n; i0 += nc) {
+    const int m = n - i0 < nc ? n - i0 : nc;
+    const int rc = mdcn_bwd_core(x + i0 * sx, offset + i0 * soff, mask + i0 * sm, weight, grad_out + i0 * sg,
+                                 grad_x + i0 * sx, grad_offset + i0 * soff, grad_mask + i0 * sm, grad_weight,
+                                 nullptr, m, c, h, w, co, kh, kw, stride, pad, dil, groups, dg, det, algo, ws,
+                                 ws_bytes, st);
+    if (rc) return rc;
+  }
+  if (grad_bias) {
+    hipLaunchKernelGGL(bias_grad_kernel, dim3(co), dim3(1024), 0, st, grad_out, grad_bias, n, co, P);
+    return aanet_launch_status();
+  }
+  return 0;
 }
 
 // aanet_conv2d_wgrad_f32: the weight kernel in PLAIN form (a.dg = groups), then for det the

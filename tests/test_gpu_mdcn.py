@@ -383,6 +383,38 @@ def test_mdcn_backward_window_deterministic_bit_reproducible():
         assert err.max() <= 1e-4 * scale + 1e-6, f"{name}: max err {err.max():.3g}"
 
 
+def test_mdcn_backward_deterministic_chunks_images():
+    """The deterministic backward runs over the batch in chunks of images (two at a time for the
+    agg_s0 shape: 96 MB of int64 grad_x + channels-last x each), so its workspace stays <= 128 MB
+    at any batch.  Each chunk is its own fixed-point problem: the per-image gradients of the last
+    chunk are bit-identical to a run over that image alone, the weight / bias gradients are the
+    chunk sums added in chunk order, bits repeat run to run, and the result matches the float
+    (atomic) form."""
+    N, C, H, W, Co, k, s, p, d, dg = 3, 64, 128, 416, 64, 3, 1, 2, 2, 2
+    L = _lib.lib()
+    ws = L.aanet_mdcn_bwd_det_workspace_size(N, C, H, W, Co, k, k, s, p, d, 1, dg)
+    assert ws == L.aanet_mdcn_bwd_det_workspace_size(2, C, H, W, Co, k, k, s, p, d, 1, dg) <= 128 << 20
+    x, off, msk, w, b = make_case(41, N, C, H, W, Co, k, s, p, d, dg, off_scale=1.0)
+    go = np.random.default_rng(42).standard_normal((N, Co, H, W)).astype(np.float32)
+    xt, ot, mt, wt, gt = g2t(x), g2t(off), g2t(msk), g2t(w), g2t(go)
+
+    def run(sl, det=True):
+        return ops.mdcn_backward(xt[sl].contiguous(), ot[sl].contiguous(), mt[sl].contiguous(), wt,
+                                 gt[sl].contiguous(), True, s, p, d, 1, dg, deterministic=det)
+
+    full, again = run(slice(0, 3)), run(slice(0, 3))
+    for u, v in zip(full, again):
+        assert torch.equal(u, v)
+    head, tail = run(slice(0, 2)), run(slice(2, 3))
+    for i in range(3):  # grad_input, grad_offset, grad_mask: per image
+        assert torch.equal(full[i][:2], head[i]) and torch.equal(full[i][2:], tail[i])
+    assert torch.equal(full[3], head[3] + tail[3])  # grad_weight: chunk sums in chunk order
+    atomic = run(slice(0, 3), det=False)
+    for name, u, v in zip(("grad_input", "grad_offset", "grad_mask", "grad_weight", "grad_bias"), full, atomic):
+        scale = v.abs().max().item() + 1e-12
+        assert (u - v).abs().max().item() <= 1e-5 * scale, name
+
+
 WINDOW_FWD = [
     # N, C, H, W, off_scale: ragged tiles (H % 8, W % 16), offsets that leave the window
     (2, 64, 16, 52, 0.7),
