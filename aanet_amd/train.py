@@ -191,8 +191,13 @@ class Trainer:
         self.accumulation_steps = accumulation_steps
         self.highest_loss_only = highest_loss_only
         self.max_disp = max_disp
+        # fused Adam (one multi-tensor kernel per step) when every parameter is on the GPU: the
+        # foreach form's capturable branch divides by 0-dim step tensors, which this torch build
+        # runs as two broadcast kernels PER PARAMETER (~360 launches, ~2 ms of a 20 ms step);
+        # same update rule (torch.optim.Adam), different rounding order only
+        fused = all(p.is_cuda and p.dtype == torch.float32 for p in model.parameters())
         self.optimizer = torch.optim.Adam(param_groups(model, lr), weight_decay=weight_decay,
-                                          capturable=capturable)
+                                          capturable=capturable, fused=fused or None)
         self.micro = 0
         self._graph = None
 
