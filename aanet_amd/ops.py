@@ -572,14 +572,23 @@ def csa_sum(inputs, act="leaky"):
 
 
 class ResizeBilinearFunction(Function):
-    """F.interpolate(x, size, mode='bilinear', align_corners=False) whose backward is the HIP
-    gather (aanet_resize_bilinear_bwd_f32): atomic-free and bit-reproducible, where torch's CUDA
-    backward scatters with atomics (or, under deterministic algorithms, sorts for index_put)."""
+    """F.interpolate(x, size, mode='bilinear', align_corners=False) on the HIP kernels: the
+    forward one thread per output element (aanet_resize_bilinear_f32; torch's NCHW kernel loops
+    over the planes inside a thread), the backward a gather (aanet_resize_bilinear_bwd_f32):
+    atomic-free and bit-reproducible, where torch's CUDA backward scatters with atomics (or, under
+    deterministic algorithms, sorts for index_put)."""
 
     @staticmethod
     def forward(ctx, x, size):
+        x = x.contiguous()
+        require_gpu(x, names=("input",))
         ctx.in_hw = tuple(x.shape[2:])
-        return torch.nn.functional.interpolate(x, size=size, mode="bilinear", align_corners=False)
+        N, C, ih, iw = x.shape
+        y = x.new_empty((N, C) + tuple(size))
+        if y.numel() == 0:
+            return y
+        call("aanet_resize_bilinear_f32", ptr(x), ptr(y), N * C, ih, iw, size[0], size[1], stream_of(x))
+        return y
 
     @staticmethod
     @once_differentiable

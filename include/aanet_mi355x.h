@@ -315,6 +315,12 @@ int aanet_conv3x3s2_terms_f32(const float *x, const void *wsplit, const float *b
                               float *out_b, int act_b, const aanet_s2_terms_t *terms,
                               aanet_stream_t stream);
 
+/* F.interpolate(x, size=(out_h, out_w), mode='bilinear', align_corners=False) on [planes, in_h,
+ * in_w] -> y [planes, out_h, out_w] (aggregation.py:395-396 in training; the loss's upsampling,
+ * model.py:115-117): one thread per output element, the reference kernel's stencil and order. */
+int aanet_resize_bilinear_f32(const float *x, float *y, long planes, int in_h, int in_w, int out_h,
+                              int out_w, aanet_stream_t stream);
+
 /* Backward of F.interpolate(x, size=(out_h, out_w), mode='bilinear', align_corners=False)
  * (aggregation.py:395-396 in training; the loss's upsampling, model.py:115-117):
  * grad_in [planes, in_h, in_w] is OVERWRITTEN with the gather-form sum over grad_out

@@ -117,10 +117,11 @@ def test_engine_convs_model_gradients_and_reproducibility():
 
 @pytest.mark.parametrize("hw,out", [((12, 20), (24, 40)), ((6, 10), (24, 40)), ((32, 64), (96, 192)),
                                     ((8, 16), (96, 192)), ((7, 11), (20, 33)), ((20, 33), (7, 11)),
-                                    ((1, 5), (4, 9))])
+                                    ((1, 5), (4, 9)), ((96, 192), (288, 576))])
 def test_resize_bilinear_backward_matches_torch(hw, out):
-    """ops.resize_bilinear's HIP gather backward against torch's bilinear backward (2x/4x CSA
-    exchanges, 3x/12x loss upsampling, non-integer and downsampling ratios, a 1-pixel axis)."""
+    """ops.resize_bilinear's HIP forward (bit-identical to torch's kernel: same stencil, same
+    order) and gather backward against torch's bilinear backward (2x/4x CSA exchanges, 3x/12x
+    loss upsampling, non-integer and downsampling ratios, a 1-pixel axis)."""
     g = torch.Generator().manual_seed(2)
     x = torch.randn(2, 3, *hw, generator=g).to(DEV)
     gy = torch.randn(2, 3, *out, generator=g).to(DEV)
