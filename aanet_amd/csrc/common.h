@@ -72,6 +72,32 @@ __device__ __forceinline__ f32x4 load_seg(const float *__restrict__ row, int iw,
   return v;
 }
 
+// ---- buffer-resource access for the epilogues: one SGPR resource per image plane set, 32-bit
+// byte offsets per lane (no per-access 64-bit address math); range-checked (bytes < 2^31)
+typedef __amdgpu_buffer_rsrc_t brsrc_t;
+__device__ __forceinline__ brsrc_t buf_rsrc(const void *p, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 buf_ld4(brsrc_t r, unsigned off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ float buf_ld1(brsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void buf_st4(brsrc_t r, unsigned off, f32x4 v) {
+  typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_, v), r, (int)off, 0, 0);
+}
+// the 4-column source segment starting at column s0 of a row at byte offset `row` (load_seg's
+// clamping), wave-uniform choice: `fast` (every lane's segment inside its row) = one 16-byte load
+__device__ __forceinline__ f32x4 buf_seg(brsrc_t r, unsigned row, int s0, int iw, bool fast) {
+  if (fast) return buf_ld4(r, row + 4u * (unsigned)s0);
+  f32x4 v;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) v[u] = buf_ld1(r, row + 4u * (unsigned)min(max(s0 + u, 0), iw - 1));
+  return v;
+}
+
 __device__ __forceinline__ f32x4 hlerp(const f32x4 v, int r) {
   if (r == 2)
     return f32x4{0.25f * v[0] + 0.75f * v[1], 0.75f * v[1] + 0.25f * v[2],

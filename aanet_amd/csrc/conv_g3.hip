@@ -133,12 +133,15 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_g3_kernel(G3Args a) {
     }
   };
   // one piece per wave: pieces 0..NPC-1 of the step's A fragments, waves past them a dummy copy
+  // (the step's base address in an SGPR pair, the lane's offset in one VGPR for the whole
+  // kernel: a per-step 64-bit VALU address was ~40 of the kernel's VALU instructions)
+  const int pcw = wave < NPC ? wave : 0;
+  const unsigned avo = pcw * 1024 + lane * 16;
   auto issue_a = [&](int s, char *dst) {
-    const int pc = wave < NPC ? wave : 0;
-    const char *src = a.wsplit + (long)s * AB + pc * 1024 + lane * 16;
-    char *dp = wave < NPC ? dst + pc * 1024 : sDummy;
+    const char *sb = a.wsplit + (long)s * AB;
+    char *dp = wave < NPC ? dst + pcw * 1024 : sDummy;
     const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void *)dp);
-    asm volatile("global_load_lds_dwordx4 %0, off" :: "v"(src), "{m0}"(m0) : "memory");
+    asm volatile("global_load_lds_dwordx4 %0, %1" :: "v"(avo), "s"(sb), "{m0}"(m0) : "memory");
   };
   // wait until at most CNT of this wave's vector-memory ops are in flight, then the workgroup
   // barrier, in ONE asm statement (the halo values in flight pass through as operands, so no use
@@ -202,19 +205,31 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_g3_kernel(G3Args a) {
   // epilogue: channel g Cog + 16m + 4kr + r of pixel (y, x), NCHW (16 lanes = 64-byte segments)
   if (!pv) return;
   const int Cog = a.Co / G;
-  const long pix = (long)y * W + x;
-  // the biases first, as one batch under one wave-uniform test (clamped rows past Cog read a valid
-  // element and are never stored): loaded per value under the lane-varying cl < Cog, each load
-  // was followed by its own full wait
+  // the biases first, as one batch under one wave-uniform test (rows past Cog are never stored):
+  // loaded per value under the lane-varying cl < Cog, each load was followed by its own full wait
+  // (buffer loads: channel offset in the SGPR operand, rows past Co read 0 by the range check)
   float bv[G][NCB][4] = {};
   if (a.bias) {
+    const u32x4 br = make_rsrc(a.bias, a.Co * 4);
+    const unsigned bvo = 16u * kr;
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
       for (int m = 0; m < NCB; ++m)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bv[g][m][r] = a.bias[g * Cog + min(16 * m + 4 * kr + r, Cog - 1)];
+        for (int r = 0; r < 4; ++r) {
+          const int so = __builtin_amdgcn_readfirstlane((g * Cog + 16 * m + r) * 4);
+          asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "=v"(bv[g][m][r]) : "v"(bvo), "s"(br), "s"(so) : "memory");
+        }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  // buffer stores over this image's output: the thread's byte offset (channel 4kr, its pixel) in
+  // one VGPR, the channel offset (g Cog + 16m + r) * HW * 4 in the SGPR operand, and channels past
+  // Cog pushed out of the buffer's range (dropped by the range check) instead of branched around:
+  // no per-store 64-bit address or exec-mask branch
+  const u32x4 orr = make_rsrc(a.out + (long)n * a.Co * HW, (int)((long)a.Co * HW * 4));
+  const int hw4 = (int)HW * 4;
+  const unsigned vo = (unsigned)((4 * kr) * hw4 + (y * W + x) * 4);
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -222,10 +237,10 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_g3_kernel(G3Args a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int cl = 16 * m + 4 * kr + r;
-        if (cl < Cog) {
-          const int co = g * Cog + cl;
-          a.out[((long)n * a.Co + co) * HW + pix] = acc[g][m][r] + bv[g][m][r];
-        }
+        const unsigned v = cl < Cog ? vo : OOB;
+        const int so = __builtin_amdgcn_readfirstlane((g * Cog + 16 * m + r) * hw4);
+        const float val = acc[g][m][r] + bv[g][m][r];
+        asm volatile("buffer_store_dword %0, %1, %2, %3 offen" :: "v"(val), "v"(v), "s"(orr), "s"(so) : "memory");
       }
 }
 
@@ -278,7 +293,7 @@ int aanet_conv3x3_grouped_nhwc_f32(const float *x, const void *wsplit, const flo
                                    aanet_stream_t stream) {
   if (!x || !wsplit || !out || n < 0 || h < 0 || w < 0 || dil < 1) return AANET_EINVAL;
   if (!aanet_conv3x3_grouped_pack_bytes(co, c, groups)) return AANET_EUNSUPPORTED;
-  if ((long)h * w * c * 4 >= (1L << 31)) return AANET_EUNSUPPORTED;
+  if ((long)h * w * c * 4 >= (1L << 31) || (long)h * w * co * 4 >= (1L << 31)) return AANET_EUNSUPPORTED;
   if (n == 0 || h == 0 || w == 0) return AANET_OK;
   const int ncb = g3_ncb(co, groups), ncc = c / groups / 32;
   G3Args a;

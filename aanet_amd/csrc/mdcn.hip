@@ -1189,25 +1189,51 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   const int qt = tid % QPR;
   const long pet = pix(4 * qt);
   const bool qokt = quad_ok(qt);
-  int urow0[2] = {0, 0}, urow1[2] = {0, 0}, us0[2] = {0, 0};
+  // buffer resources over image n's planes (SGPRs) and 32-bit byte offsets per item: the output,
+  // CSA output and residual at (co P + pixel) * 4, the CSA sources at (co ih iw + row + column) * 4
+  // (round 5: per item a 64-bit plane product and pointer per access)
+  const long img = (long)n * cout * P;
+  const brsrc_t ro = buf_rsrc(a.out + img, (long)cout * P * 4);
+  const brsrc_t rcs = buf_rsrc(csa ? a.csa_out + img : a.out + img, (long)cout * P * 4);
+  const brsrc_t rre = buf_rsrc(a.residual ? a.residual + img : a.out + img, (long)cout * P * 4);
+  const unsigned pq = qokt ? 4u * (unsigned)pet : 0u;
+  brsrc_t ru[2] = {ro, ro};
+  unsigned urow0[2] = {0u, 0u}, urow1[2] = {0u, 0u}, uhw[2] = {0u, 0u};
+  int us0[2] = {0, 0}, uiw[2] = {4, 4};
   float uh0[2] = {1.f, 1.f}, uh1[2] = {0.f, 0.f};
-  if (csa && qokt) {
-    const int y = (int)(pet / a.Wo), qq = (int)(pet % a.Wo) >> 2;  // Wo % 4 == 0 (launcher)
+  bool sfast = true;
+  if (csa) {
+    // (the halo tile knows its row and column; the flat form divides in 32 bits: a 64-bit
+    // division here was ~150 instructions of the epilogue)
+    int y, qq;
+    if constexpr (HALO) {
+      y = hy0 + ((4 * qt) >> 4);
+      qq = (hx0 + 4 * (qt & 3)) >> 2;
+    } else {
+      y = qokt ? (int)pet / a.Wo : 0;
+      qq = qokt ? ((int)pet % a.Wo) >> 2 : 0;  // Wo % 4 == 0 (launcher)
+    }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       if (j >= a.num_up) break;
       const int ih = a.up_h[j], iw = a.up_w[j], r = a.up_r[j];
+      ru[j] = buf_rsrc(a.up[j] + (long)n * cout * ih * iw, (long)cout * ih * iw * 4);
+      uhw[j] = 4u * (unsigned)(ih * iw);
+      uiw[j] = iw;
       // PyTorch's area_pixel_compute_scale (ih / Ho) and source row, align_corners=False
       float hr = ((float)ih / (float)a.Ho) * ((float)y + 0.5f) - 0.5f;
       hr = hr < 0.f ? 0.f : hr;
       const int h1 = (int)hr, h1p = h1 < ih - 1 ? 1 : 0;
-      urow0[j] = h1 * iw;
-      urow1[j] = (h1 + h1p) * iw;
+      urow0[j] = 4u * (unsigned)(h1 * iw);
+      urow1[j] = 4u * (unsigned)((h1 + h1p) * iw);
       us0[j] = r == 2 ? 2 * qq - 1 : qq - 1;
+      sfast = sfast && us0[j] >= 0 && us0[j] + 3 <= iw - 1;
       uh1[j] = hr - (float)h1;
       uh0[j] = 1.f - uh1[j];
     }
   }
+  // the image-edge quads read clamped columns: a wave with one takes the per-column loads
+  const bool wfast = __all(sfast || !qokt);
 #pragma unroll
   for (int i0 = 0; i0 < EPT; i0 += EB) {
     f32x4 ev[EB], er[EB], eu[EB][2][2];
@@ -1219,23 +1245,20 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       const int col = e / QPR, co = co0 + col;
       eok[b] = (NE % FNT == 0 || e < NE) && co < cend_o && qokt;
       if (!eok[b]) continue;
-      const long o = ((long)n * cout + co) * P + pet;
       // the channel's parameters in this load pass too: loaded in the use pass, each item
       // waited for its own
       pbi[b] = ebias ? ebias[co] : 0.f;
       psc[b] = esc ? esc[co] : 1.f;
       psh[b] = esc ? esh[co] : 0.f;
       ev[b] = *reinterpret_cast<const f32x4 *>(sO + col * OP + 4 * qt);
-      if (a.residual) er[b] = *reinterpret_cast<const f32x4 *>(a.residual + o);
+      if (a.residual) er[b] = buf_ld4(rre, 4u * (unsigned)(co * (int)P) + pq);
       if (csa) {
-        const long plane = (long)n * cout + co;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           if (j >= a.num_up) break;
-          const int iw = a.up_w[j];
-          const float *im = a.up[j] + plane * (a.up_h[j] * iw);
-          eu[b][j][0] = load_seg(im + urow0[j], iw, us0[j]);
-          eu[b][j][1] = load_seg(im + urow1[j], iw, us0[j]);
+          const unsigned pl = (unsigned)co * uhw[j];
+          eu[b][j][0] = buf_seg(ru[j], pl + urow0[j], us0[j], uiw[j], wfast);
+          eu[b][j][1] = buf_seg(ru[j], pl + urow1[j], us0[j], uiw[j], wfast);
         }
       }
     }
@@ -1244,7 +1267,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       if (!eok[b]) continue;
       const int e = tid + (i0 + b) * FNT;
       const int col = e / QPR, co = co0 + col;
-      const long o = ((long)n * cout + co) * P + pet;
+      const unsigned po = 4u * (unsigned)(co * (int)P) + pq;
       const float bias = pbi[b], sc = psc[b], sh = psh[b];
       f32x4 v = ev[b];
 #pragma unroll
@@ -1254,7 +1277,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
         if (a.residual) t += er[b][u];
         v[u] = apply_act(t, eact);
       }
-      *reinterpret_cast<f32x4 *>(a.out + o) = v;
+      buf_st4(ro, po, v);
       if (csa) {
         // cross-scale sum of this output branch (nets/aggregation.py:387-400): the block output
         // (the identity term) + exact 2x/4x upsamplings of the coarser exchange terms, LeakyReLU
@@ -1265,7 +1288,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) v[u] = apply_act(v[u], a.csa_act);
-        *reinterpret_cast<f32x4 *>(a.csa_out + o) = v;
+        buf_st4(rcs, po, v);
         // post stage: the CSA output back into the item's own slot (its B operand)
         if constexpr (POST) *reinterpret_cast<f32x4 *>(sO + col * OP + 4 * qt) = v;
       }
@@ -2404,6 +2427,9 @@ int check_shapes(const MdcnArgs &a) {
     return AANET_EINVAL;
   if (a.C % a.groups || a.Co % a.groups || a.C % a.dg) return AANET_EINVAL;
   if (a.Ho <= 0 || a.Wo <= 0) return AANET_EINVAL;
+  // one image's planes are addressed by 32-bit buffer offsets (the epilogues)
+  if ((long)a.C * a.H * a.W * 4 >= (1L << 31) || (long)a.Co * a.Ho * a.Wo * 4 >= (1L << 31))
+    return AANET_EUNSUPPORTED;
   return AANET_OK;
 }
 
