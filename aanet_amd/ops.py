@@ -218,18 +218,23 @@ def window_fwd_ok(C, Co, kh, kw, stride, padding, dilation, groups, deformable_g
                                                            groups, deformable_groups, W))
 
 
-_SPLIT_CACHE = {}
-
-
 def _split_weight(weight):
-    """pack_weight_split(weight), cached per (storage, version): an optimizer step bumps the
-    version, so training re-packs once per step; eval packs once."""
-    key = (weight.data_ptr(), weight._version, tuple(weight.shape), weight.device)
-    wp = _SPLIT_CACHE.get(key)
-    if wp is None:
-        if len(_SPLIT_CACHE) >= 64:
-            _SPLIT_CACHE.clear()
-        wp = _SPLIT_CACHE[key] = pack_weight_split(weight)
+    """pack_weight_split(weight), kept on the weight tensor itself with the (storage, version,
+    shape) it was packed from: an optimizer step bumps the version, so training re-packs once per
+    step; eval packs once.  (A module-level dict keyed by data_ptr returned a freed weight's packing
+    to a new tensor that reused its address at version 0.)  During HIP graph capture it always
+    packs, so every replay re-packs from the weights' current values."""
+    key = (weight.data_ptr(), weight._version, tuple(weight.shape))
+    capturing = torch.cuda.is_current_stream_capturing()
+    hit = getattr(weight, "_aanet_split_pack", None)
+    if hit is not None and hit[0] == key and not capturing:
+        return hit[1]
+    wp = pack_weight_split(weight)
+    if not capturing:
+        try:
+            weight._aanet_split_pack = (key, wp)
+        except (AttributeError, RuntimeError):
+            pass
     return wp
 
 

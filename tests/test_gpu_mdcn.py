@@ -415,6 +415,25 @@ def test_mdcn_backward_deterministic_chunks_images():
         assert (u - v).abs().max().item() <= 1e-5 * scale, name
 
 
+def test_split_weight_cache_follows_the_tensor_not_its_address():
+    """ops._split_weight keeps the packed weight on the tensor: a new weight that reuses a freed
+    one's device address (the caching allocator hands the block straight back) at version 0 must
+    be packed from its own values (round 5: a dict keyed by data_ptr returned the old packing and
+    the window forward came out wrong in 1 of ~4 suite runs)."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    w1 = torch.randn(64, 64, 3, 3, device=DEV, generator=g)
+    p1 = ops._split_weight(w1).clone()
+    addr = w1.data_ptr()
+    del w1
+    w2 = torch.randn(64, 64, 3, 3, device=DEV, generator=g)
+    p2 = ops._split_weight(w2)
+    assert torch.equal(p2, ops.pack_weight_split(w2))
+    if w2.data_ptr() == addr:  # the case the old cache got wrong
+        assert not torch.equal(p2, p1)
+    w2.mul_(2.0)  # in place: new version, re-packed
+    assert torch.equal(ops._split_weight(w2), ops.pack_weight_split(w2))
+
+
 WINDOW_FWD = [
     # N, C, H, W, off_scale: ragged tiles (H % 8, W % 16), offsets that leave the window
     (2, 64, 16, 52, 0.7),
