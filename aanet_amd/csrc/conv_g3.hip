@@ -143,15 +143,19 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_g3_kernel(G3Args a) {
     const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void *)dp);
     asm volatile("global_load_lds_dwordx4 %0, %1" :: "v"(avo), "s"(sb), "{m0}"(m0) : "memory");
   };
-  // wait until at most CNT of this wave's vector-memory ops are in flight, then the workgroup
-  // barrier, in ONE asm statement (the halo values in flight pass through as operands, so no use
-  // is scheduled ahead of the wait)
+  // wait until at most CNT of this wave's vector-memory ops are in flight AND its LDS reads have
+  // completed, then the workgroup barrier, in ONE asm statement (the halo values in flight pass
+  // through as operands, so no use is scheduled ahead of the wait).  lgkmcnt(0): a wave could
+  // reach the barrier with its reads of a weight slot still queued at the LDS, and the DMA
+  // another wave issues into that slot right after the barrier enters the LDS by the memory
+  // return path, unordered with them -- a stale-slot race that showed as run-to-run differences
+  // of the offset (1-3 runs in 30 beside other work, tools/race_probe.py; round 5)
   auto wait_bar = [&](auto cnt_c, f32x4 (&hv)[HIT]) {
     constexpr int CNT = decltype(cnt_c)::value;
     if constexpr (HIT == 4)
-      asm volatile("s_waitcnt vmcnt(%4)\n\ts_barrier" : "+v"(hv[0]), "+v"(hv[1]), "+v"(hv[2]), "+v"(hv[3]) : "n"(CNT) : "memory");
+      asm volatile("s_waitcnt vmcnt(%4) lgkmcnt(0)\n\ts_barrier" : "+v"(hv[0]), "+v"(hv[1]), "+v"(hv[2]), "+v"(hv[3]) : "n"(CNT) : "memory");
     else
-      asm volatile("s_waitcnt vmcnt(%3)\n\ts_barrier" : "+v"(hv[0]), "+v"(hv[1]), "+v"(hv[2]) : "n"(CNT) : "memory");
+      asm volatile("s_waitcnt vmcnt(%3) lgkmcnt(0)\n\ts_barrier" : "+v"(hv[0]), "+v"(hv[1]), "+v"(hv[2]) : "n"(CNT) : "memory");
   };
   auto slot = [&](int i) -> char * { return i == 0 ? sA0 : (i == 1 ? sA1 : sA2); };
 

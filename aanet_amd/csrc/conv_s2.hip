@@ -261,10 +261,12 @@ __global__ __launch_bounds__(NT, 4) void conv3x3s2_rows_kernel(S2Args a) {
   // A read hoisted between wait and barrier would race with the other waves' DMAs), and
   // __syncthreads' fence would wait for every load in flight.  A branch between two such
   // statements would make the compiler copy the pending registers before them.  The row values
-  // about to be used pass through as operands so that no use is scheduled ahead of the wait
+  // about to be used pass through as operands so that no use is scheduled ahead of the wait.
+  // lgkmcnt(0): this wave's reads of the weight slot must have completed before another wave's
+  // LDS-DMA into it, issued after the barrier, can land (conv_g3.hip wait_bar; round 5)
   auto wait_bar = [&](auto cnt_c, f32x3 (&v)[8]) {
     constexpr int CNT = decltype(cnt_c)::value;
-    asm volatile("s_waitcnt vmcnt(%8)\n\ts_barrier"
+    asm volatile("s_waitcnt vmcnt(%8) lgkmcnt(0)\n\ts_barrier"
                  : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
                  : "n"(CNT) : "memory");
   };

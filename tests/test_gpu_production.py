@@ -25,7 +25,7 @@ import numpy as np
 import pytest
 import torch
 
-from aanet_amd import nets
+from aanet_amd import nets, ops
 from aanet_amd.nets._fuse import folded
 from aanet_amd.nets.aggregation import csa_epilogue_ok
 from oracle import aggregation as oagg
@@ -254,3 +254,51 @@ def test_s2_sums_option_matches_separate_csa_sums():
     for d in (a, b):
         assert np.abs(d - g["disp0"]).max() <= DISP_TOL
     assert np.abs(a - b).max() <= DISP_TOL
+
+
+def test_offset_conv_and_heads_deterministic_beside_other_work():
+    """The LDS-DMA kernels (offset conv conv_g3, stride-2 heads conv_s2) give the same bits on
+    every run while another stream keeps the CUs busy.  Their barrier now also waits for the
+    wave's own LDS reads (lgkmcnt(0)): without it a wave could reach the barrier with reads of a
+    weight slot still queued while another wave's DMA into that slot landed, and the concurrent
+    schedule differed from the one-stream schedule in a few runs of 30 (round 5)."""
+    g = torch.Generator(device=DEV).manual_seed(0)
+    B, C, H, W = 8, 64, 64, 208
+    x = torch.randn(B, C, H, W, device=DEV, generator=g).relu_().contiguous(
+        memory_format=torch.channels_last)
+    wsp = ops.pack_conv3x3_grouped(torch.randn(54, 32, 3, 3, device=DEV, generator=g) * 0.05, 2)
+    b = torch.randn(54, device=DEV, generator=g)
+    xn = x.contiguous()
+    ws2 = ops.pack_conv3x3s2(torch.randn(96, C, 3, 3, device=DEV, generator=g) * 0.04)
+    b2 = torch.randn(96, device=DEV, generator=g)
+    big = torch.randn(4096, 4096, device=DEV, generator=g)
+    side = torch.cuda.Stream()
+    fns = [lambda: ops.conv3x3_grouped_nhwc(x, wsp, b, 54, 2, 2),
+           lambda: torch.cat([t.flatten() for t in ops.conv3x3_s2(xn, ws2, b2, 96, 32, "leaky", "leaky")])]
+    for fn in fns:
+        ref = fn().clone()
+        torch.cuda.synchronize()
+        for _ in range(20):
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                torch.mm(big, big)
+                fns[0]()
+            out = fn()
+            torch.cuda.current_stream().wait_stream(side)
+            assert torch.equal(out, ref)
+
+
+def test_concurrent_schedule_is_run_to_run_deterministic():
+    """The eval aggregation's concurrent-scale schedule repeated eagerly gives the one-stream
+    result bit for bit on every run (round 5: before the LDS-DMA barrier fix, 2-4 of 5 runs
+    differed by up to 7e-4 px)."""
+    from aanet_amd.nets.options import get_option  # noqa: F401
+    g, sd, m, left, right = _model("hotpath_d64")
+    with torch.no_grad():
+        m.set_options(concurrent_scales=False)
+        single = [t.clone() for t in m(left, right)]
+        m.set_options(concurrent_scales=True)
+        for _ in range(5):
+            got = m(left, right)
+            for a, c in zip(got, single):
+                assert torch.equal(a, c)
