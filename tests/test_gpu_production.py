@@ -289,10 +289,9 @@ def test_offset_conv_and_heads_deterministic_beside_other_work():
 
 
 def test_concurrent_schedule_is_run_to_run_deterministic():
-    """The eval aggregation's concurrent-scale schedule repeated eagerly gives the one-stream
-    result bit for bit on every run (round 5: before the LDS-DMA barrier fix, 2-4 of 5 runs
-    differed by up to 7e-4 px)."""
-    from aanet_amd.nets.options import get_option  # noqa: F401
+    """The eval aggregation's concurrent-scale schedule repeated eagerly, and replayed from a
+    HIP graph, gives the one-stream result bit for bit on every run (round 5: before the LDS-DMA
+    barrier fix, 2-4 of 5 runs differed by up to 7e-4 px)."""
     g, sd, m, left, right = _model("hotpath_d64")
     with torch.no_grad():
         m.set_options(concurrent_scales=False)
@@ -301,4 +300,12 @@ def test_concurrent_schedule_is_run_to_run_deterministic():
         for _ in range(5):
             got = m(left, right)
             for a, c in zip(got, single):
+                assert torch.equal(a, c)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            static = m(left, right)
+        for _ in range(3):
+            graph.replay()
+            torch.cuda.synchronize()
+            for a, c in zip(static, single):
                 assert torch.equal(a, c)
