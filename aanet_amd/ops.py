@@ -681,8 +681,11 @@ def conv2d_wgrad(x, grad_out, weight_shape, with_bias, stride=1, padding=0, dila
                  deterministic=None):
     """(grad_weight, grad_bias or None) of an ordinary convolution (aanet_conv2d_wgrad_f32):
     the DCN weight-gradient kernel with the tap's shifted window as its column.
-    deterministic (default: torch.are_deterministic_algorithms_enabled()): per-split partials
-    reduced in a fixed order instead of float atomics."""
+    deterministic (default True): per-split partials reduced in a fixed order; False: one float
+    atomic per (workgroup, element).  The fixed-order form is also the faster one: in the
+    training step (bench.py --train, profiles/r05d_train_breakdown*.txt) the atomic form's
+    launches averaged 35.7 us, the partials 18.0 us + 6.3 us for the reduction -- every pixel
+    split of a chunk adds into the same weight elements, so the atomics contend."""
     require_gpu(x, grad_out, names=("input", "grad_output"))
     N, C, H, W = x.shape
     Co, _, kh, kw = weight_shape
@@ -691,7 +694,7 @@ def conv2d_wgrad(x, grad_out, weight_shape, with_bias, stride=1, padding=0, dila
     gw = x.new_zeros(tuple(weight_shape))
     gb = x.new_zeros((Co,)) if with_bias else None
     if deterministic is None:
-        deterministic = torch.are_deterministic_algorithms_enabled()
+        deterministic = True
     ws, nbytes = None, 0
     if deterministic:
         nbytes = _lib.lib().aanet_conv2d_wgrad_workspace_size(N, C, H, W, Co, kh, kw, stride, padding,

@@ -108,9 +108,9 @@ def wrap_data_parallel(model, device, sync_bn=True, bucket_cap_mb=32):
 class EngineConv2dFunction(torch.autograd.Function):
     """An nn.Conv2d on the HIP engine end to end: forward aanet_conv2d_fused_f32, data gradient
     as the engine's forward conv of grad_out (ops.conv2d_dgrad), weight/bias gradient
-    aanet_conv2d_wgrad_f32 -- deterministic (fixed-order partial sums) under
-    torch.use_deterministic_algorithms(True), where MIOpen would fall back to its naive
-    kernels."""
+    aanet_conv2d_wgrad_f32 with fixed-order partial sums (deterministic in every mode, and faster
+    than its float-atomic form; under torch.use_deterministic_algorithms(True) MIOpen would fall
+    back to its naive kernels)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, stride, padding, dilation, groups):

@@ -82,6 +82,11 @@ def test_deterministic_wgrad_is_bit_reproducible(shape):
         assert torch.equal(gw, outs[0][0])
         if b:
             assert torch.equal(gb, outs[0][1])
+    # the default is the fixed-order form; the float-atomic form agrees to fp32 summation order
+    dflt = ops.conv2d_wgrad(x, gy, w.shape, b, s, p, d, g)
+    assert torch.equal(dflt[0], outs[0][0])
+    gw_at, _ = ops.conv2d_wgrad(x, gy, w.shape, b, s, p, d, g, deterministic=False)
+    assert (gw_at - outs[0][0]).abs().max().item() <= 1e-4 * max(1.0, outs[0][0].abs().max().item())
 
 
 def test_engine_convs_model_gradients_and_reproducibility():
