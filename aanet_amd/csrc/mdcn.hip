@@ -3120,14 +3120,14 @@ struct BwdPlan {
   long range;
 };
 
-BwdPlan bwd_plan(const MdcnArgs &a) {
+BwdPlan bwd_plan(const MdcnArgs &a, long target = 2048) {
   BwdPlan pl;
   const long P = (long)a.Ho * a.Wo, T = (long)a.N * P;
   const int K = a.kh * a.kw, cpg = a.C / a.dg;
   pl.npieces = host_div_up(cpg, KC);
   pl.nchunks = K * a.dg * pl.npieces;
-  // ~2048 workgroups in total; each covers `range` flattened pixels
-  long nsplit = 2048 / pl.nchunks;
+  // ~target workgroups in total; each covers `range` flattened pixels
+  long nsplit = target / pl.nchunks;
   if (nsplit < 1) nsplit = 1;
   long range = (T + nsplit - 1) / nsplit;
   range = ((range + PT - 1) / PT) * PT;
@@ -3442,6 +3442,13 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
   return 0;
 }
 
+// Workgroups per conv weight-gradient launch (pixel splits x chunks x co tiles, before rounding):
+// fewer splits mean longer MFMA accumulation per workgroup and less partial-sum traffic for the
+// reduction.  Training step (bench.py --train, same-call A/B): 14.44 ms at 1024, 14.59 at 2048,
+// 14.42 at 768, 14.53 at 512, 14.87 at 4096.
+#ifndef AANET_WGRAD_WGS
+#define AANET_WGRAD_WGS 1024
+#endif
 // aanet_conv2d_wgrad_f32: the weight kernel in PLAIN form (a.dg = groups), then for det the
 // fixed-order reduction of the per-split partials; the bias gradient is a per-channel sum in a
 // fixed order either way.
@@ -3453,7 +3460,7 @@ int conv_wgrad_impl(const float *x, const float *grad_out, float *grad_weight, f
   int rc = check_shapes(a);
   if (rc) return rc;
   if (!x || !grad_out || !grad_weight) return AANET_EINVAL;
-  const BwdPlan pl = bwd_plan(a);
+  const BwdPlan pl = bwd_plan(a, AANET_WGRAD_WGS);
   const long nw = (long)co * (c / groups) * kh * kw;
   float *part = nullptr;
   if (det) {
@@ -3492,7 +3499,7 @@ extern "C" size_t aanet_conv2d_wgrad_workspace_size(int n, int c, int h, int w, 
                          nullptr, 0, nullptr, n, c, h, w, co, kh, kw, stride, pad, dil, groups,
                          groups);
   if (check_shapes(a)) return 0;
-  return (size_t)bwd_plan(a).nsplit * co * (c / groups) * kh * kw * 4;
+  return (size_t)bwd_plan(a, AANET_WGRAD_WGS).nsplit * co * (c / groups) * kh * kw * 4;
 }
 
 extern "C" int aanet_conv2d_wgrad_f32(const float *x, const float *grad_out, float *grad_weight,
