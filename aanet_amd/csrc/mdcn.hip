@@ -2365,7 +2365,7 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_weight_kernel(MdcnArgs a, const f
 // loads when P % 4 == 0, fixed-order tree reduction (bit-reproducible).
 __global__ __launch_bounds__(1024) void bias_grad_kernel(const float *__restrict__ gout,
                                                          float *__restrict__ gb, int N, int Co,
-                                                         long P) {
+                                                         long P, int overwrite = 0) {
   const int co = blockIdx.x;
   float s = 0.f;
   if ((P & 3) == 0 && (reinterpret_cast<uintptr_t>(gout) & 15) == 0) {
@@ -2387,7 +2387,7 @@ __global__ __launch_bounds__(1024) void bias_grad_kernel(const float *__restrict
     if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) gb[co] += red[0];
+  if (threadIdx.x == 0) gb[co] = overwrite ? red[0] : gb[co] + red[0];
 }
 
 // grad_x NHWC workspace [N][HW][C] -> NCHW: 32 x 32 tiles through LDS (both sides coalesced).
@@ -2700,7 +2700,7 @@ __global__ void det_scale_kernel(const unsigned *__restrict__ bounds, double *__
 // 4 lane sums are added in lane order -- bit-reproducible for a given nsplit.
 __global__ __launch_bounds__(256) void det_weight_reduce_kernel(const float *__restrict__ part,
                                                                 float *__restrict__ gw, long n,
-                                                                int nsplit) {
+                                                                int nsplit, int overwrite = 0) {
   __shared__ float red[4][64];
   const int ex = threadIdx.x & 63, sl = threadIdx.x >> 6;
   const long e = (long)blockIdx.x * 64 + ex;
@@ -2719,7 +2719,10 @@ __global__ __launch_bounds__(256) void det_weight_reduce_kernel(const float *__r
   }
   red[sl][ex] = s;
   __syncthreads();
-  if (sl == 0 && e < n) gw[e] += ((red[0][ex] + red[1][ex]) + red[2][ex]) + red[3][ex];
+  if (sl == 0 && e < n) {
+    const float v = ((red[0][ex] + red[1][ex]) + red[2][ex]) + red[3][ex];
+    gw[e] = overwrite ? v : gw[e] + v;
+  }
 }
 
 __global__ void pack_weight_kernel(const float *__restrict__ w, float *__restrict__ wp, int Co,
@@ -3451,7 +3454,8 @@ int mdcn_bwd_impl(const float *x, const float *offset, const float *mask, const 
 #endif
 // aanet_conv2d_wgrad_f32: the weight kernel in PLAIN form (a.dg = groups), then for det the
 // fixed-order reduction of the per-split partials; the bias gradient is a per-channel sum in a
-// fixed order either way.
+// fixed order either way.  det == 2: the same, but the reduction and the bias sum STORE their
+// results (grad_weight / grad_bias need no zero fill beforehand).
 int conv_wgrad_impl(const float *x, const float *grad_out, float *grad_weight, float *grad_bias,
                     int n, int c, int h, int w, int co, int kh, int kw, int stride, int pad,
                     int dil, int groups, int det, void *ws, size_t ws_bytes, hipStream_t st) {
@@ -3459,7 +3463,7 @@ int conv_wgrad_impl(const float *x, const float *grad_out, float *grad_weight, f
                          0, nullptr, n, c, h, w, co, kh, kw, stride, pad, dil, groups, groups);
   int rc = check_shapes(a);
   if (rc) return rc;
-  if (!x || !grad_out || !grad_weight) return AANET_EINVAL;
+  if (!x || !grad_out || !grad_weight || det < 0 || det > 2) return AANET_EINVAL;
   const BwdPlan pl = bwd_plan(a, AANET_WGRAD_WGS);
   const long nw = (long)co * (c / groups) * kh * kw;
   float *part = nullptr;
@@ -3478,13 +3482,13 @@ int conv_wgrad_impl(const float *x, const float *grad_out, float *grad_weight, f
   if (rc) return rc;
   if (det) {
     hipLaunchKernelGGL(det_weight_reduce_kernel, dim3(host_div_up(nw, 64)), dim3(256), 0, st,
-                       part, grad_weight, nw, pl.nsplit);
+                       part, grad_weight, nw, pl.nsplit, (int)(det == 2));
     rc = aanet_launch_status();
     if (rc) return rc;
   }
   if (grad_bias) {
     hipLaunchKernelGGL(bias_grad_kernel, dim3(co), dim3(1024), 0, st, grad_out, grad_bias, n, co,
-                       (long)a.Ho * a.Wo);
+                       (long)a.Ho * a.Wo, (int)(det == 2));
     rc = aanet_launch_status();
   }
   return rc;

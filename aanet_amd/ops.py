@@ -691,10 +691,12 @@ def conv2d_wgrad(x, grad_out, weight_shape, with_bias, stride=1, padding=0, dila
     Co, _, kh, kw = weight_shape
     if kh != kw:
         raise ValueError("square kernels only")
-    gw = x.new_zeros(tuple(weight_shape))
-    gb = x.new_zeros((Co,)) if with_bias else None
     if deterministic is None:
         deterministic = True
+    # the fixed-order form stores its results (mode 2): no zero fill; the atomic form adds
+    alloc = x.new_empty if deterministic else x.new_zeros
+    gw = alloc(tuple(weight_shape))
+    gb = alloc((Co,)) if with_bias else None
     ws, nbytes = None, 0
     if deterministic:
         nbytes = _lib.lib().aanet_conv2d_wgrad_workspace_size(N, C, H, W, Co, kh, kw, stride, padding,
@@ -703,7 +705,7 @@ def conv2d_wgrad(x, grad_out, weight_shape, with_bias, stride=1, padding=0, dila
             raise ValueError("aanet_conv2d_wgrad_workspace_size: invalid shape")
         ws = torch.empty((nbytes,), device=x.device, dtype=torch.uint8)
     call("aanet_conv2d_wgrad_f32", ptr(x), ptr(grad_out), ptr(gw), ptr(gb), N, C, H, W, Co, kh, kw,
-         stride, padding, dilation, groups, int(bool(deterministic)), ptr(ws), nbytes, stream_of(x))
+         stride, padding, dilation, groups, 2 if deterministic else 0, ptr(ws), nbytes, stream_of(x))
     return gw, gb
 
 

@@ -400,7 +400,8 @@ int aanet_mdcn_bwd_algo_f32(const float *x, const float *offset, const float *ma
  * grad_weight [co, c/groups, kh, kw] and grad_bias [co] (may be NULL) ACCUMULATE.
  * deterministic != 0: per-split partial sums reduced in a fixed order (bit-reproducible), with
  * `workspace` (device) of aanet_conv2d_wgrad_workspace_size(...) bytes; 0: float atomics, no
- * workspace.  The fixed-order form is also the faster one (round 5: 18 + 6 us against 36 us per
+ * workspace; 2: the fixed-order form that STORES grad_weight / grad_bias instead of adding to
+ * them (no zero fill needed).  The fixed-order form is also the faster one (round 5: 18 + 6 us against 36 us per
  * launch in the training step; the atomics of every pixel split hit the same weight elements),
  * and the Python layer calls it by default.  The data gradient is a forward conv on aanet_conv2d_fused_f32 (flipped,
  * transposed weight; zero-inserted grad_out for stride 2) -- aanet_amd/train.py. */

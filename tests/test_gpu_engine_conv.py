@@ -7,7 +7,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from aanet_amd import nets, ops, train
+from aanet_amd import _lib, nets, ops, train
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -145,3 +145,32 @@ def test_resize_bilinear_backward_matches_torch(hw, out):
     xa.grad = None
     ops.resize_bilinear(xa, out).backward(gy)
     assert torch.equal(again, xa.grad)
+
+
+def test_wgrad_modes_accumulate_or_store():
+    """aanet_conv2d_wgrad_f32 deterministic = 1 ADDS to grad_weight / grad_bias (the reference's
+    accumulate semantics), 2 STORES them (what ops.conv2d_wgrad uses: no zero fill), both with the
+    same fixed-order sums."""
+    shape = SHAPES[1]
+    N, C, H, W, Co, k, s, p, d, g, b = shape
+    x, w, _ = _case(shape, 3)
+    Ho = (H + 2 * p - d * (k - 1) - 1) // s + 1
+    Wo = (W + 2 * p - d * (k - 1) - 1) // s + 1
+    gy = torch.randn(N, Co, Ho, Wo, generator=torch.Generator().manual_seed(4)).to(DEV)
+    ref_w, ref_b = ops.conv2d_wgrad(x, gy, w.shape, True, s, p, d, g)
+    lib = _lib.lib()
+    nbytes = lib.aanet_conv2d_wgrad_workspace_size(N, C, H, W, Co, k, k, s, p, d, g)
+    ws = torch.empty((nbytes,), device=DEV, dtype=torch.uint8)
+    for mode, init in ((1, 0.5), (2, float("nan"))):
+        gw = torch.full(tuple(w.shape), init, device=DEV)
+        gb = torch.full((Co,), init, device=DEV)
+        ops.call("aanet_conv2d_wgrad_f32", ops.ptr(x), ops.ptr(gy), ops.ptr(gw), ops.ptr(gb), N, C, H,
+                 W, Co, k, k, s, p, d, g, mode, ops.ptr(ws), nbytes, ops.stream_of(x))
+        torch.cuda.synchronize()
+        if mode == 1:
+            assert torch.equal(gw, ref_w + 0.5) and torch.equal(gb, ref_b + 0.5)
+        else:
+            assert torch.equal(gw, ref_w) and torch.equal(gb, ref_b)
+    with pytest.raises(_lib.AanetError):
+        ops.call("aanet_conv2d_wgrad_f32", ops.ptr(x), ops.ptr(gy), ops.ptr(gw), ops.ptr(gb), N, C, H,
+                 W, Co, k, k, s, p, d, g, 3, ops.ptr(ws), nbytes, ops.stream_of(x))
