@@ -723,8 +723,8 @@ def conv2d_dgrad(grad_out, weight, input_hw, stride=1, padding=0, dilation=1, gr
         raise ValueError("padding > dilation*(k-1) has no engine data gradient")
     N, _, Ho, Wo = grad_out.shape
     H, W = input_hw
-    wt = (weight.view(groups, Co // groups, Cg, kh, kw).transpose(1, 2)
-          .reshape(groups * Cg, Co // groups, kh, kw).flip(-2, -1).contiguous())
+    wt = weight.view(groups, Co // groups, Cg, kh, kw).transpose(1, 2).reshape(groups * Cg, Co // groups, kh, kw)
+    wt = (wt.flip(-2, -1) if kh > 1 else wt).contiguous()  # a 1x1 flip is the identity: no launch
     if stride > 1:
         rh = H + 2 * padding - dilation * (kh - 1) - 1 - (Ho - 1) * stride
         rw = W + 2 * padding - dilation * (kw - 1) - 1 - (Wo - 1) * stride
