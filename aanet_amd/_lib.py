@@ -41,6 +41,7 @@ _SIGNATURES = {
     "aanet_resize_bilinear_f32": [_P, _P, _L] + [_I] * 4 + [_P],
     "aanet_conv2d_fused_f32": [_P] * 6 + [_I, _I, _P] + [_I] * 12 + [_P],
     "aanet_conv_weight_pack_f32": [_P, _P, _I, _I, _I, _I, _P],
+    "aanet_conv_weight_pack_dgrad_f32": [_P, _P, _I, _I, _I, _I, _I, _P],
     "aanet_conv_weight_pack_split_f32": [_P, _P, _I, _I, _I, _I, _I, _P],
     "aanet_conv2d_pw_f32": [_P] * 5 + [_I] + [_P] * 3 + [_I, _I, _P] + [_I] * 10 + [_P, _I, _P],
     "aanet_mdcn_pw_f32": [_P, _P, _L, _P, _L, _I, _F, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _P]

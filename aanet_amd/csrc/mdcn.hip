@@ -3056,6 +3056,36 @@ extern "C" int aanet_mdcn_window_fwd_supported(int c, int co, int kh, int kw, in
   return groups == 1 && dcn_tile_supported(c, co, co, kh, kw, stride, pad, dil, dg, 1, w);
 }
 
+// The data gradient's weight straight into the engine layout: wt[g*cg + i][j][k] =
+// w[g*(co/groups) + j][i][K-1-k] (per-group transpose, spatial flip), stored [k][co'][cg'] with
+// co' = groups*cg, cg' = co/groups -- what pack_weight_kernel makes of the transposed, flipped
+// copy, in one pass over w.
+__global__ void pack_weight_dgrad_kernel(const float *__restrict__ w, float *__restrict__ wp, int Co,
+                                         int Cg, int K, int groups) {
+  const int Cot = groups * Cg, Cgt = Co / groups;
+  const long total = (long)Cot * Cgt * K;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % Cgt);  // wt's input channel j (output order: [k][co'][cg'])
+    const long t = e / Cgt;
+    const int cot = (int)(t % Cot), k = (int)(t / Cot);
+    const int g = cot / Cg, i = cot - g * Cg;
+    wp[e] = w[((long)(g * Cgt + c) * Cg + i) * K + (K - 1 - k)];
+  }
+}
+
+extern "C" int aanet_conv_weight_pack_dgrad_f32(const float *weight, float *weight_packed, int co,
+                                                int cg, int kh, int kw, int groups,
+                                                aanet_stream_t stream) {
+  AANET_HOST_CHECK(weight && weight_packed && co > 0 && cg > 0 && kh > 0 && kw > 0 && groups > 0 &&
+                   co % groups == 0);
+  const long total = (long)co * cg * kh * kw;
+  hipLaunchKernelGGL(pack_weight_dgrad_kernel,
+                     dim3(host_div_up(total, 256) > 4096 ? 4096 : host_div_up(total, 256)), dim3(256),
+                     0, as_hip(stream), weight, weight_packed, co, cg, kh * kw, groups);
+  return aanet_launch_status();
+}
+
 extern "C" int aanet_conv_weight_pack_f32(const float *weight, float *weight_packed, int co,
                                           int cg, int kh, int kw, aanet_stream_t stream) {
   AANET_HOST_CHECK(weight && weight_packed && co > 0 && cg > 0 && kh > 0 && kw > 0);

@@ -723,15 +723,19 @@ def conv2d_dgrad(grad_out, weight, input_hw, stride=1, padding=0, dilation=1, gr
         raise ValueError("padding > dilation*(k-1) has no engine data gradient")
     N, _, Ho, Wo = grad_out.shape
     H, W = input_hw
-    wt = weight.view(groups, Co // groups, Cg, kh, kw).transpose(1, 2).reshape(groups * Cg, Co // groups, kh, kw)
-    wt = (wt.flip(-2, -1) if kh > 1 else wt).contiguous()  # a 1x1 flip is the identity: no launch
+    # the per-group transposed, flipped weight, packed for the engine in one launch
+    wt = weight.new_empty((groups * Cg, Co // groups, kh, kw))  # shape carrier only
+    wp = torch.empty((kh, kw, groups * Cg, Co // groups), device=weight.device, dtype=weight.dtype)
+    call("aanet_conv_weight_pack_dgrad_f32", ptr(weight.contiguous()), ptr(wp), Co, Cg, kh, kw, groups,
+         stream_of(weight))
     if stride > 1:
         rh = H + 2 * padding - dilation * (kh - 1) - 1 - (Ho - 1) * stride
         rw = W + 2 * padding - dilation * (kw - 1) - 1 - (Wo - 1) * stride
         dz = grad_out.new_zeros((N, Co, (Ho - 1) * stride + 1 + rh, (Wo - 1) * stride + 1 + rw))
         dz[:, :, : (Ho - 1) * stride + 1 : stride, : (Wo - 1) * stride + 1 : stride] = grad_out
         grad_out = dz
-    gx = conv2d_fused(grad_out.contiguous(), wt, padding=pad_t, dilation=dilation, groups=groups)
+    gx = conv2d_fused(grad_out.contiguous(), wt, padding=pad_t, dilation=dilation, groups=groups,
+                      packed_weight=wp)
     if tuple(gx.shape[2:]) != (H, W):
         raise RuntimeError(f"dgrad shape {tuple(gx.shape)} != input {(H, W)}")
     return gx

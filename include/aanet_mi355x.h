@@ -243,6 +243,13 @@ int aanet_mdcn_pw_f32(const float *x, const float *offset, long offset_batch_str
 int aanet_conv_weight_pack_f32(const float *weight, float *weight_packed, int co, int cg, int kh,
                                int kw, aanet_stream_t stream);
 
+/* The data gradient of a conv as a forward conv (train.EngineConv2dFunction): weight [co][cg][kh][kw]
+ * of a conv with `groups` -> the aanet_conv_weight_pack_f32 layout of its per-group transposed,
+ * spatially flipped weight ([groups*cg][co/groups][kh][kw], i.e. [kh][kw][groups*cg][co/groups])
+ * in one launch.  cuDNN's backward-data (the reference's training) has no such caller-side step. */
+int aanet_conv_weight_pack_dgrad_f32(const float *weight, float *weight_packed, int co, int cg,
+                                     int kh, int kw, int groups, aanet_stream_t stream);
+
 /* Weight buffer for the split-bf16 contraction (AANET_CONV_WEIGHTS_SPLIT): the
  * aanet_conv_weight_pack_f32 layout, then (at a 256-byte aligned offset) every weight split into
  * three bf16 pieces and laid out as MFMA operand fragments (mdcn.hip, split_frag_offset).

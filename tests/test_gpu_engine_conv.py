@@ -174,3 +174,18 @@ def test_wgrad_modes_accumulate_or_store():
     with pytest.raises(_lib.AanetError):
         ops.call("aanet_conv2d_wgrad_f32", ops.ptr(x), ops.ptr(gy), ops.ptr(gw), ops.ptr(gb), N, C, H,
                  W, Co, k, k, s, p, d, g, 3, ops.ptr(ws), nbytes, ops.stream_of(x))
+
+
+@pytest.mark.parametrize("co,cg,k,groups", [(32, 16, 3, 1), (54, 32, 3, 2), (16, 3, 7, 1), (64, 32, 1, 1),
+                                            (40, 70, 3, 1)])
+def test_dgrad_weight_pack_equals_transposed_flipped_pack(co, cg, k, groups):
+    """aanet_conv_weight_pack_dgrad_f32 (one launch) == pack_weight of the per-group transposed,
+    spatially flipped weight that ops.conv2d_dgrad used to build with two torch copies."""
+    w = torch.randn(co, cg, k, k, generator=torch.Generator().manual_seed(7)).to(DEV)
+    wt = (w.view(groups, co // groups, cg, k, k).transpose(1, 2)
+          .reshape(groups * cg, co // groups, k, k).flip(-2, -1).contiguous())
+    want = ops.pack_weight(wt)
+    got = torch.empty_like(want)
+    ops.call("aanet_conv_weight_pack_dgrad_f32", ops.ptr(w), ops.ptr(got), co, cg, k, k, groups,
+             ops.stream_of(w))
+    assert torch.equal(got, want)
