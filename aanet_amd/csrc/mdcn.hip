@@ -2840,6 +2840,8 @@ extern "C" int aanet_conv2d_fused_f32(const float *x, const float *weight, const
                                       int kw, int stride, int pad, int dil, int groups, int layout,
                                       aanet_stream_t stream) {
   if (act < 0 || act > 2) return AANET_EINVAL;
+  // the argument checks of launch_fwd, before any of the specialised kernels below is chosen
+  if (!x || !weight || !out || (post_scale && !post_shift)) return AANET_EINVAL;
   MdcnArgs a = make_args(x, nullptr, 0, nullptr, 0, 0, 1.f, weight, bias, post_scale, post_shift,
                          act, out, n, c, h, w, co, kh, kw, stride, pad, dil, groups, 1);
   a.residual = residual;

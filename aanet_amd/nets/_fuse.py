@@ -34,12 +34,17 @@ def _bn_tensors(bn):
 
 def clear_fold_caches(module):
     """Drop every folded-weight / BN-affine cache in `module`'s subtree (called on each
-    train()/eval() switch of the drop-in modules, see FoldCacheMixin)."""
+    train()/eval() switch of the drop-in modules, see FoldCacheMixin, and by Trainer.graph_step),
+    including the split-bf16 packs that ops._split_weight keeps on the weight tensors themselves:
+    writes through `.data` and HIP graph replays update a weight without bumping its _version."""
     for m in module.modules():
         for attr in ("_aanet_fold", "_aanet_fold_dense", "_aanet_affine", "_aanet_s2pack",
                      "_aanet_s2pack_k"):
             if attr in m.__dict__:
                 del m.__dict__[attr]
+        for p in m.parameters(recurse=False):
+            if "_aanet_split_pack" in p.__dict__:
+                del p.__dict__["_aanet_split_pack"]
 
 
 class FoldCacheMixin:

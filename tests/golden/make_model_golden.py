@@ -81,6 +81,86 @@ def checksum(sd):
     return np.float64(sum(float(v.double().abs().sum()) for v in sd.values()))
 
 
+# Near-tie fixtures (round 6, profiles/r06_raw_stages.txt): where the reference's own fp32 run
+# flips hundreds of pixels against its fp64 run, a single flip count is one draw of a
+# heavy-tailed distribution (the reference's own L1 flips range 0-151 over 27 runs whose images
+# differ by one rounding unit: profiles/r06_raw_lottery.txt).  For these the fixture also holds
+#   * the fp64 feature pyramid (fpn outputs, both images, stored as float32) and the reference's
+#     own fp32 normwise error on it, so the test checks the first stage directly;
+#   * the refinement run alone on the fp64 level-0 disparity (its own error, no inherited flips);
+#   * the ENVELOPE: the reference's fp32 pipeline re-run ENVELOPE_RUNS times with its feature
+#     pyramid carrying TWICE its own fp32 error (each tensor x (1 + u d), u uniform in [-1, 1],
+#     d = 3 e_ref: an extra normwise error of sqrt(3) e_ref on top of its own e_ref), per run and
+#     level: flips (|d - d64| > 0.05 px), p99 and max |d - d64|.
+NEAR_TIE = {"psmnet_aa_raw"}
+ENVELOPE_RUNS = 48
+FLIP = 0.05
+
+
+def near_tie_data(model, left, right, pyr, pyr64):
+    def nw(a, ref):
+        return float(np.linalg.norm(a - ref) / np.linalg.norm(ref))
+
+    feats = {}
+
+    def grab(tag):
+        return lambda mod, i, o: feats.setdefault(tag, []).append([t.detach().clone() for t in o])
+
+    out = {}
+    with torch.no_grad():
+        for tag, dt in (("64", torch.float64), ("32", torch.float32)):
+            h = model.fpn.register_forward_hook(grab(tag))
+            model.to(dt)(left.to(dt), right.to(dt))
+            h.remove()
+        errs = []
+        for img in range(2):
+            for s, (f32, f64) in enumerate(zip(feats["32"][img], feats["64"][img])):
+                out[f"feat64_{img}_{s}"] = f64.float().numpy()
+                errs.append(nw(f32.double().numpy(), f64.numpy()))
+        e_ref = np.array(errs)  # [img * 3 + scale]
+        out["feat_err32"] = e_ref
+        # the refinement alone on the fp64 level-0 disparity (fp64 run = the fixture's chain)
+        d0 = torch.from_numpy(pyr64[0].numpy())
+        model.double()
+        c64 = model.disparity_refinement(left.double(), right.double(), d0)
+        for i, c in enumerate(c64):
+            assert float((c - pyr64[i + 1]).abs().max()) < 1e-9
+        model.float()
+        c32 = model.disparity_refinement(left, right, d0.float())
+        out["cond32_stats"] = np.array([_err_stats(c.double().numpy(), r.numpy())
+                                        for c, r in zip(c32, c64)])
+        # the envelope
+        d64 = [d.numpy() for d in pyr64]
+        state = {}
+
+        def perturb(mod, i, o):
+            k = state["k"]
+            state["k"] += 1
+            res = []
+            for s, t in enumerate(o):
+                u = torch.rand(t.shape, generator=state["gen"], dtype=torch.float64) * 2 - 1
+                res.append((t.double() * (1 + u * 3 * e_ref[k * 3 + s])).float())
+            return res
+
+        h = model.fpn.register_forward_hook(perturb)
+        rows = []
+        for r in range(ENVELOPE_RUNS):
+            state.update(gen=torch.Generator().manual_seed(7000 + r), k=0)
+            p = model(left, right)
+            rows.append([v for d, ref in zip(p, d64) for v in _err_stats(d.double().numpy(), ref)])
+        h.remove()
+        out["envelope"] = np.array(rows)
+        out["envelope_delta"] = 3 * e_ref
+    print("    near-tie: feature err", np.round(e_ref, 8).tolist(), "envelope max per level "
+          "(flips, p99, max):", np.round(out["envelope"].max(0), 3).tolist())
+    return out
+
+
+def _err_stats(d, ref):
+    e = np.abs(d.astype(np.float64) - ref)
+    return [float((e > FLIP).sum()), float(np.percentile(e, 99)), float(e.max())]
+
+
 def main():
     load_reference()  # installs the stand-in `nets` package + nets.deform_conv
     aanet = importlib.import_module("nets.aanet")
@@ -137,6 +217,7 @@ def main():
             # the same model in float64: how far the reference's own fp32 result is from the
             # exact answer (the tests hold our fp32 result to the same distance)
             pyr64 = model.double()(left.double(), right.double())
+        extra = near_tie_data(model, left, right, pyr, pyr64) if tag in NEAR_TIE else {}
         save(f"model_{tag}", shape=np.array([B, H, W]), config=np.array(json.dumps(kw)),
              img_checksum=np.float64(float(left.double().sum() + right.double().abs().sum())),
              names=np.array([n for n, _ in names]),
@@ -144,7 +225,7 @@ def main():
              checksum=checksum(model.state_dict()), seed=seed, max_disp=max_disp,
              **({"scales": np.array(json.dumps(scales))} if scales else {}),
              **{f"disp{i}": d for i, d in enumerate(pyr)},
-             **{f"disp64_{i}": d for i, d in enumerate(pyr64)})
+             **{f"disp64_{i}": d for i, d in enumerate(pyr64)}, **extra)
         print(f"  {tag}: {len(names)} entries, pyramid " +
               ", ".join(f"{tuple(d.shape)} mean {d.mean():.2f}" for d in pyr))
 

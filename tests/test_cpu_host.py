@@ -51,6 +51,22 @@ def test_invalid_arguments_are_rejected_without_a_gpu():
         _lib.call("aanet_corr_volume_f32", None, None, None, 0, 1, 1, 1, 1, None)
 
 
+def test_conv_fused_null_arguments_rejected_before_the_direct_kernel():
+    """aanet_conv2d_fused_f32 on a few-channel shape (3 -> 32, 7x7 / 3: the direct VALU kernel of
+    small_conv.hip) with a null x / weight / out, or post_scale without post_shift, returns
+    AANET_EINVAL on the host instead of launching (the direct dispatch ran before the
+    engine's checks).  No GPU is touched: the checks come first."""
+    import ctypes as C
+    L = _lib.lib()
+    f = L.aanet_conv2d_fused_f32
+    buf = (C.c_float * 4)()
+    p = C.cast(buf, C.c_void_p)
+    shape = [1, 3, 48, 96, 32, 7, 7, 3, 2, 1, 1, 0, None]  # n c h w co kh kw s pad dil g layout st
+    for x, w, out, ps, sh in ((None, p, p, None, None), (p, None, p, None, None),
+                              (p, p, None, None, None), (p, p, p, p, None)):
+        assert f(x, w, None, ps, sh, None, 1, 0, out, *shape) == -1
+
+
 def test_descriptor_size_is_checked_without_a_gpu():
     """Descriptor structs carry struct_size (ABI version 4): a caller built against another
     header layout gets AANET_EABI before anything is read past the struct or launched (ADVICE r3:

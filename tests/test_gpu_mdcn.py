@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from aanet_amd import _lib, ops
+from aanet_amd import _lib, nets, ops
 from oracle import oracle
 
 pytestmark = pytest.mark.gpu
@@ -432,6 +432,36 @@ def test_split_weight_cache_follows_the_tensor_not_its_address():
         assert not torch.equal(p2, p1)
     w2.mul_(2.0)  # in place: new version, re-packed
     assert torch.equal(ops._split_weight(w2), ops.pack_weight_split(w2))
+
+
+def test_split_weight_cache_dropped_with_the_fold_caches():
+    """Writes through `.data` (and HIP graph replays: Trainer.graph_step) change a weight without
+    bumping its _version, so the pack kept on the tensor would go stale; clear_fold_caches (which
+    train()/eval() and graph_step call) drops it with the folded-weight caches.  The
+    sequence graph_step -> eager forward -> graph_step -> eager forward then runs the second eager
+    forward on the current weights: checked here on a DeformConv2d against algo='generic'."""
+    from aanet_amd.nets._fuse import clear_fold_caches
+    torch.manual_seed(0)
+    m = nets.DeformConv2d(64, 64).to(DEV)
+    with torch.no_grad():
+        m.deform_conv.weight.normal_(0, 0.05)
+        m.offset_conv.weight.normal_(0, 0.01)
+        m.offset_conv.bias.normal_(0, 0.5)
+    m.train()  # the reference op order: ModulatedDeformConv -> ops.mdcn_forward (window kernel)
+    x = torch.randn(1, 64, 12, 32, device=DEV)
+    w = m.deform_conv.weight
+    p1 = ops._split_weight(w).clone()
+    w.data.mul_(-0.5)  # no version bump: the kept pack is stale ...
+    assert torch.equal(ops._split_weight(w), p1)
+    clear_fold_caches(m)  # ... until the caches are dropped
+    assert torch.equal(ops._split_weight(w), ops.pack_weight_split(w))
+    with torch.no_grad():
+        off = m._offset_conv(x)
+        out = m(x)
+        om = off[:, 36:].sigmoid() * 2
+        ref = ops.mdcn_forward(x, off[:, :36].contiguous(), om.contiguous(), w, None, 1, 2, 2, 1, 2,
+                               algo="generic")
+    assert float((out - ref).abs().max()) <= 2e-5 * max(1.0, float(ref.abs().max()))
 
 
 WINDOW_FWD = [

@@ -70,8 +70,11 @@ def build(tag, fuse=True):
 STRICT = {"model_aanet", "model_aanet_inter", "model_aanetplus", "model_psmnet_aa"}
 FLIP = 0.05  # px: a near-tie soft-argmin flip
 # near-tie fixtures: the reference's own fp32 run flips hundreds of pixels against its fp64 run,
-# so which pixels flip, and by how much, is a rounding lottery.  There the flip COUNT is the
-# bound; the single largest flip (one sample) is only held to the disparity range.
+# and that count is one draw of a heavy-tailed distribution (its own level-1 flips range 0-151
+# over 27 runs whose images differ by one rounding unit, profiles/r06_raw_stages.txt E).  They
+# are checked stage by stage against data the fixture holds (make_model_golden.near_tie_data):
+# the feature pyramid against fp64, the refinement alone, and the pyramid against the envelope
+# of the reference's own pipeline with twice its own feature error (_check_near_tie).
 NEAR_TIE = {"model_psmnet_aa_raw"}
 
 
@@ -87,19 +90,12 @@ def test_full_model_vs_reference_golden(tag, fuse):
     be no further from it than the reference's own fp32 result, up to
       * flips (|d - d64| > 0.05 px): at most 2x the reference's count + 4;
       * mean over the pixels that neither run flips: at most 2x the reference's;
-      * p99 within 2x, max within 4x (NEAR_TIE fixtures: max within the disparity range, as
-        their largest flip is a single rounding-lottery sample);
+      * p99 within 2x, max within 4x;
     and the adaptive-aggregation models (STRICT) additionally max |d - d32| <= 1e-3 px against
     the reference's fp32 output.  model_psmnet_aa_raw is PSMNet-AA without the fixture
     conditioning: the reference's own fp32 run flips 3 / 29 / 697 pixels (up to 0.2 / 0.3 /
-    0.7 px) against its fp64 run there, so that fixture exercises the flip bounds (non-strict)."""
-    if tag in NEAR_TIE and not fuse:
-        # the reference-order path's aggregation logits are within 2x of the reference's own fp32
-        # normwise error here too (profiles/r04_psmnet_diag.txt: 1.6e-4 vs 7.5e-5), but on logits
-        # of +-1.5e4 with top-2 gaps down to 0.48 that error places its flips elsewhere (784 / 5647
-        # at levels 1 / 2 against the reference's 29 / 697; fused: 33 / 633, profiles/
-        # r05_raw_flips.txt).  The conditioned model_psmnet_aa holds this path to the strict bar.
-        pytest.skip("near-tie fixture: flip bounds are checked on the fused path")
+    0.7 px) against its fp64 run there: that fixture is checked stage by stage instead
+    (_check_near_tie), on both paths."""
     g, m, left, right = build(tag, fuse)
     # the plain convs of the reference-order run (those that are not ours) go through PyTorch's
     # native fp32 convolution (im2col + fp32 GEMM), not MIOpen: which MIOpen solver runs a conv
@@ -108,8 +104,14 @@ def test_full_model_vs_reference_golden(tag, fuse):
     # (bound 62) on boxes that picked them, and with MIOPEN_DEBUG_CONV_WINOGRAD=0 every time
     # (tools/diag_psmnet_flips.sh); TF32 proper gave 137.  A third-party algorithm choice is
     # not what this test measures, so it is taken out of the run.
+    feats = []
+    hook = m.fpn.register_forward_hook(lambda mod, i, o: feats.append([t.cpu() for t in o])) \
+        if tag in NEAR_TIE else None
     with torch.no_grad(), torch.backends.cudnn.flags(enabled=False, allow_tf32=False):
         pyr = m(left, right)
+    if hook is not None:
+        hook.remove()
+        return _check_near_tie(g, m, left, right, pyr, feats, fuse)
     n = len([k for k in g if k.startswith("disp") and not k.startswith("disp64")])
     assert len(pyr) == n
     report = []
@@ -132,15 +134,58 @@ def test_full_model_vs_reference_golden(tag, fuse):
         # p99 within 2x the reference's own fp32 distance; the max (a single near-tie flip, a
         # noisy one-sample statistic) within 4x
         for got, bound, k, slack in zip(e64[1:], sens[1:], (2, 4), (1e-4, 1e-3)):
-            if k == 4 and tag in NEAR_TIE:
-                assert got <= float(ref64.max()) + 1.0, (i, "max vs fp64", e64)
-                continue
             assert got <= k * bound + slack, (i, "vs fp64", e64, "ref fp32 vs fp64", sens)
         if tag in STRICT:
             assert e32[2] <= 1e-3, (i, e32)
     print(tag, "fused" if fuse else "ref-order", ["L%d vs32 mean/p99/max %.1e/%.1e/%.1e | "
           "vs64 %.1e/%.1e/%.1e | ref32-vs-64 %.1e/%.1e/%.1e" % ((i,) + a + b + c)
           for i, a, b, c in report])
+
+
+def _flip_stats(d, ref):
+    e = np.abs(np.asarray(d, np.float64) - ref)
+    return int((e > FLIP).sum()), float(np.percentile(e, 99)), float(e.max())
+
+
+def _check_near_tie(g, m, left, right, pyr, feats, fuse):
+    """A near-tie fixture (model_psmnet_aa_raw), stage by stage (profiles/r06_raw_stages.txt):
+      1. the feature pyramid, both images: normwise error against the reference's fp64 features
+         within 2x the reference's own fp32 error (+1e-7: the fp64 features are stored as float32);
+      2. the refinement alone, fed the fp64 level-0 disparity: flips <= 2x the reference's + 4,
+         p99 within 2x and max within 4x of the reference's own fp32 refinement of that input;
+      3. every pyramid level within the envelope of the reference's own fp32 pipeline when its
+         features carry twice its own error (48 seeded runs, make_model_golden.near_tie_data):
+         flips, p99 and max |d - d64| no larger than the largest of those runs (p99 / max with
+         the 1e-4 / 1e-3 px slack of the other fixtures' bounds).
+    Step 3 is where the single-draw bound of the other fixtures does not hold: every level-1/2
+    flip sits within 64 px of a level-0 flip, and the refinement alone flips nothing (step 2), so
+    the counts are the level-0 near-ties (fp64 top-2 logit gaps down to 0.48 on logits of
+    +-1.5e4) amplified; with 1.9x the reference's feature error -- the GPU fp32 conv accumulation,
+    ours and torch's alike -- the reference's own pipeline gives 2-8 / 3-888 / 15-6052 flips."""
+    tag = "fused" if fuse else "ref-order"
+    assert len(feats) == 2
+    e_ref = g["feat_err32"]
+    for img in range(2):
+        for s, t in enumerate(feats[img]):
+            ref = g[f"feat64_{img}_{s}"].astype(np.float64)
+            e = float(np.linalg.norm(t.numpy().astype(np.float64) - ref) / np.linalg.norm(ref))
+            assert e <= 2 * e_ref[img * 3 + s] + 1e-7, (tag, "features", img, s, e, e_ref[img * 3 + s])
+    d0 = torch.from_numpy(g["disp64_0"].astype(np.float32)).to(DEV)
+    with torch.no_grad(), torch.backends.cudnn.flags(enabled=False, allow_tf32=False):
+        cond = m.disparity_refinement(left, right, d0)
+    for i, (c, (f_ref, p99_ref, max_ref)) in enumerate(zip(cond, g["cond32_stats"])):
+        f, p99, mx = _flip_stats(c.cpu().numpy(), g[f"disp64_{i + 1}"])
+        assert f <= 2 * f_ref + 4 and p99 <= 2 * p99_ref + 1e-6 and mx <= 4 * max_ref + 1e-5, \
+            (tag, "refinement alone", i + 1, (f, p99, mx), tuple(g["cond32_stats"][i]))
+    env = g["envelope"].max(0)
+    report = []
+    for i, d in enumerate(pyr):
+        got = _flip_stats(d.cpu().numpy(), g[f"disp64_{i}"])
+        # (p99 / max with the slack of the single-draw bounds above: 1e-4 / 1e-3 px)
+        lim = tuple(float(v) + sl for v, sl in zip(env[3 * i:3 * i + 3], (0, 1e-4, 1e-3)))
+        report.append((i, got, lim))
+        assert all(a <= b for a, b in zip(got, lim)), (tag, "level", i, got, "envelope", lim)
+    print("near-tie", tag, "per level (flips, p99, max) vs envelope:", report)
 
 
 def test_aanetplus_c3_full_size_properties():
