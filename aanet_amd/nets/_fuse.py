@@ -10,6 +10,7 @@ import torch.nn as nn
 from .. import ops
 from .. import _lib
 from .._lib import is_nhwc
+from .._precision import CONV2D_TYPES
 
 
 def bn_scale_shift(bn):
@@ -201,7 +202,7 @@ def offset_conv_eval(x, conv):
 
 def s2_conv_ok(conv):
     """A conv of the CSA down chains that ops.conv3x3_s2 takes (3x3, stride 2, pad 1, plain)."""
-    return type(conv) is nn.Conv2d and engine_conv(conv) and _int(conv.kernel_size) == 3 and \
+    return engine_conv(conv) and _int(conv.kernel_size) == 3 and \
         _int(conv.stride) == 2 and _int(conv.padding) == 1 and _int(conv.dilation) == 1 and \
         conv.groups == 1 and conv.in_channels % 32 == 0 and conv.out_channels % 16 == 0 and \
         conv.out_channels <= 96
@@ -261,7 +262,7 @@ def act_name(m):
 
 def engine_conv(conv):
     """A conv the HIP implicit-GEMM engine runs (plain 2-D, zero padding, square parameters)."""
-    if type(conv) is not nn.Conv2d or conv.padding_mode != "zeros" or isinstance(conv.padding, str):
+    if type(conv) not in CONV2D_TYPES or conv.padding_mode != "zeros" or isinstance(conv.padding, str):
         return False
     return all(v[0] == v[1] for v in (conv.stride, conv.padding, conv.dilation, conv.kernel_size))
 

@@ -30,7 +30,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from ._precision import fp32_scope
+from ._precision import CONV2D_TYPES, PinnedConv2d, fp32_scope
 from .nets._fuse import clear_fold_caches
 
 # model.py:98-107: pyramid weights by pyramid length
@@ -138,7 +138,7 @@ class EngineConv2dFunction(torch.autograd.Function):
 
 
 def _engine_conv_ok(m):
-    if type(m) is not nn.Conv2d:
+    if type(m) not in (nn.Conv2d, PinnedConv2d):
         return False
     k, s, p, d = m.kernel_size, m.stride, m.padding, m.dilation
     return (m.padding_mode == "zeros" and not isinstance(p, str)
@@ -146,7 +146,7 @@ def _engine_conv_ok(m):
             and p[0] <= d[0] * (k[0] - 1))
 
 
-class EngineConv2d(nn.Conv2d):
+class EngineConv2d(PinnedConv2d):
     """nn.Conv2d whose training forward runs EngineConv2dFunction (use_engine_convs swaps a
     module's class to this one in place).  Same parameters, buffers and state-dict keys; being a
     module-level subclass, a whole-model torch.save / torch.load round-trips (a bound method
@@ -154,9 +154,12 @@ class EngineConv2d(nn.Conv2d):
 
     def forward(self, x):
         if x.dtype != torch.float32 or not x.is_cuda:  # the HIP engine takes fp32 device tensors
-            return nn.Conv2d.forward(self, x)
+            return PinnedConv2d.forward(self, x)
         return EngineConv2dFunction.apply(x, self.weight, self.bias, self.stride[0],
                                           self.padding[0], self.dilation[0], self.groups)
+
+
+CONV2D_TYPES.add(EngineConv2d)
 
 
 def use_engine_convs(model):
@@ -166,7 +169,7 @@ def use_engine_convs(model):
     DDP and the eval-mode folding of nets/_fuse.py see the same module."""
     n = 0
     for m in model.modules():
-        if type(m) is nn.Conv2d and _engine_conv_ok(m):
+        if _engine_conv_ok(m):
             m.__class__ = EngineConv2d
             m._aanet_engine = True
             n += 1

@@ -50,12 +50,9 @@ def test_trainer_steps_hot_path():
     assert 0 < d_off < 0.5 * d_base, (d_off, d_base)
 
 
-def test_trainer_backward_convs_run_fp32_under_global_tf32():
-    """ADVICE r4: with torch's global allow_tf32=True, the MIOpen conv backward of a Trainer step
-    runs with TF32 off (it reads the flag at backward time), and the weight gradient of such a
-    conv matches an fp64 recomputation at fp32 tolerance."""
-    m = _model(3)
-    conv = m.aggregation.fusions[0].branches[0][0].conv1    # a MIOpen nn.Conv2d in training
+def _conv_grad_vs_fp64(conv, run_step):
+    """Run `run_step()` with torch's global allow_tf32=True; return (the flags seen by conv's weight
+    hook, its weight gradient's max error against an fp64 recomputation / the gradient scale)."""
     seen, captured = [], {}
 
     def hook(g):
@@ -71,18 +68,91 @@ def test_trainer_backward_convs_run_fp32_under_global_tf32():
     prev = torch.backends.cudnn.allow_tf32
     torch.backends.cudnn.allow_tf32 = True
     try:
-        t = train.Trainer(m, lr=1e-3, accumulation_steps=2)   # no optimizer step yet
-        l, r, gt = _inputs(2, 4)
-        t.step(l, r, gt)
+        run_step()
         assert torch.backends.cudnn.allow_tf32 is True
     finally:
         torch.backends.cudnn.allow_tf32 = prev
-    assert seen == [False], seen
     x64, g64 = xin["x"].double(), gout["g"].double()
-    ref = torch.nn.grad.conv2d_weight(x64, conv.weight.shape, g64)
-    scale = torch.nn.grad.conv2d_weight(x64.abs(), conv.weight.shape, g64.abs()).max()
-    err = (captured["g"].double() - ref).abs().max() / scale
-    assert err <= 1e-5, float(err)
+    ref = torch.nn.grad.conv2d_weight(x64, conv.weight.shape, g64, conv.stride, conv.padding,
+                                      conv.dilation, conv.groups)
+    scale = torch.nn.grad.conv2d_weight(x64.abs(), conv.weight.shape, g64.abs(), conv.stride,
+                                        conv.padding, conv.dilation, conv.groups).max()
+    return seen, float((captured["g"].double() - ref).abs().max() / scale)
+
+
+def test_drop_in_backward_convs_fp32_without_trainer():
+    """the reference's own loop calls total_loss.backward() (model.py:137) with no
+    Trainer and no fp32_scope, under torch's default global allow_tf32=True.  The drop-in's MIOpen
+    convs are pinned (_precision.PinnedConv2d: aten convolution forward/backward with TF32 off), so
+    a conv weight gradient still matches fp64 at fp32 tolerance; and a transposed conv (AANet+'s
+    hourglass deconvolutions, Conv2x) against a float64 copy of the module."""
+    from aanet_amd import _precision
+    m = _model(3).train()
+    conv = m.aggregation.fusions[0].branches[0][0].conv1
+
+    def step():
+        l, r, gt = _inputs(2, 4)
+        total, _ = train.disparity_loss(m(l, r), gt, gt > 0)
+        total.backward()
+    seen, err = _conv_grad_vs_fp64(conv, step)
+    assert type(conv) is _precision.PinnedConv2d
+    assert err <= 1e-5, err
+
+    from aanet_amd.nets.feature import Conv2x
+    torch.manual_seed(1)
+    c = Conv2x(48, 32, deconv=True).to(DEV).train()
+    c64 = copy.deepcopy(c).cpu().double()
+    x = torch.randn(2, 48, 12, 16, device=DEV, requires_grad=True)
+    rem = torch.randn(2, 32, 24, 32, device=DEV)
+    g = torch.randn(2, 32, 24, 32, device=DEV)
+    prev = torch.backends.cudnn.allow_tf32
+    torch.backends.cudnn.allow_tf32 = True
+    try:
+        (c(x, rem) * g).sum().backward()
+    finally:
+        torch.backends.cudnn.allow_tf32 = prev
+    x64 = x.detach().cpu().double().requires_grad_()
+    (c64(x64, rem.cpu().double()) * g.cpu().double()).sum().backward()
+    assert type(c.conv1.conv) is _precision.PinnedConvTranspose2d
+    for (n, p), (_, p64) in zip(c.named_parameters(), c64.named_parameters()):
+        e = float((p.grad.cpu().double() - p64.grad).abs().max() / p64.grad.abs().max())
+        assert e <= 1e-5, (n, e)
+    e = float((x.grad.cpu().double() - x64.grad).abs().max() / x64.grad.abs().max())
+    assert e <= 1e-5, ("input", e)
+
+
+def test_trainer_backward_convs_run_fp32_under_global_tf32():
+    """ADVICE r4: with torch's global allow_tf32=True, the MIOpen conv backward of a Trainer step
+    runs with TF32 off, and the weight gradient of such a conv matches an fp64 recomputation at
+    fp32 tolerance.  engine_convs=False keeps the conv on MIOpen (with the engine
+    convs, the default on the GPU, this conv is an EngineConv2d -- the next test)."""
+    from aanet_amd import _precision
+    m = _model(3)
+    conv = m.aggregation.fusions[0].branches[0][0].conv1    # a MIOpen conv in training
+    t = train.Trainer(m, lr=1e-3, accumulation_steps=2, engine_convs=False)  # no optimizer step
+
+    def step():
+        l, r, gt = _inputs(2, 4)
+        t.step(l, r, gt)
+    seen, err = _conv_grad_vs_fp64(conv, step)
+    assert type(conv) is _precision.PinnedConv2d, type(conv)
+    assert seen == [False], seen
+    assert err <= 1e-5, err
+
+
+def test_trainer_engine_convs_wgrad_fp32():
+    """The Trainer's default on the GPU: the plain convs on the HIP engine (EngineConv2d, fp32
+    forward / dgrad / wgrad kernels whatever the TF32 flag) -- the same fp64 check."""
+    m = _model(3)
+    conv = m.aggregation.fusions[0].branches[0][0].conv1
+    t = train.Trainer(m, lr=1e-3, accumulation_steps=2)
+
+    def step():
+        l, r, gt = _inputs(2, 4)
+        t.step(l, r, gt)
+    _, err = _conv_grad_vs_fp64(conv, step)
+    assert type(conv) is train.EngineConv2d, type(conv)
+    assert err <= 1e-5, err
 
 
 def test_deterministic_training_step_is_bit_reproducible():
