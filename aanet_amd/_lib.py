@@ -4,6 +4,8 @@ This is the only way the Python package reaches the GPU: every op passes raw dev
 and torch's current HIP stream to an ``extern "C"`` entry point.  There is NO CPU fallback:
 if the library is missing or a tensor is not on a ROCm device, the call raises.
 """
+import contextlib
+import contextvars
 import ctypes
 import os
 
@@ -137,24 +139,42 @@ CONV_EXACT_F32 = 8  # AANET_CONV_EXACT_F32: exact f32 MFMA instead of the split-
 CONV_WEIGHTS_SPLIT = 16  # AANET_CONV_WEIGHTS_SPLIT: weight buffers carry bf16 piece fragments
 CONV_GENERIC_DCN = 32  # AANET_CONV_GENERIC_DCN: generic engine instead of the LDS-window DCN tail
 
-_exact_f32 = os.environ.get("AANET_EXACT_F32", "0") == "1"
+# The contraction arithmetic of the fused eval paths, per execution context (a ContextVar: each
+# thread / asyncio task has its own, and nothing is read from the process environment).
+_EXACT_F32 = contextvars.ContextVar("aanet_exact_f32", default=False)
+
+
+def exact_f32_enabled():
+    return _EXACT_F32.get()
 
 
 def set_exact_f32(on):
-    """Select the conv engine's contraction arithmetic for the fused eval paths: False (default)
-    = split-bf16 pieces with fp32 accumulation where the engine has the configuration (fp32-
-    accurate, include/aanet_mi355x.h AANET_CONV_EXACT_F32); True = exact f32 MFMA everywhere.
-    Returns the previous setting.  Env: AANET_EXACT_F32=1."""
-    global _exact_f32
-    prev, _exact_f32 = _exact_f32, bool(on)
+    """Select the conv engine's contraction arithmetic for the fused eval paths of the current
+    context: False (default) = split-bf16 pieces with fp32 accumulation where the engine has the
+    configuration (fp32-accurate, include/aanet_mi355x.h AANET_CONV_EXACT_F32); True = exact f32
+    MFMA everywhere.  Returns the previous setting (bench.py --exact-f32; `exact_f32` below is the
+    scoped form)."""
+    prev = _EXACT_F32.get()
+    _EXACT_F32.set(bool(on))
     return prev
+
+
+@contextlib.contextmanager
+def exact_f32(on=True):
+    """Scope: the enclosed fused eval calls run the exact f32 engine (on=True) or the split-bf16
+    contraction (on=False); the previous setting comes back on exit."""
+    token = _EXACT_F32.set(bool(on))
+    try:
+        yield
+    finally:
+        _EXACT_F32.reset(token)
 
 
 def conv_flags(*packed):
     """Contraction flags for a fused conv call whose packed weight buffers are `packed`: the split
     contraction when every buffer carries its pieces (ops.pack_weight_split) and exact mode is
     off, else the exact f32 engine."""
-    if _exact_f32:
+    if _EXACT_F32.get():
         return CONV_EXACT_F32
     if packed and all(getattr(w, "_aanet_split", False) for w in packed):
         return CONV_WEIGHTS_SPLIT

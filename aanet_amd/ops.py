@@ -251,7 +251,7 @@ def mdcn_forward(x, offset, mask, weight, bias=None, stride=1, padding=0, dilati
     Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
     if out is None:
         out = torch.empty((N, Co, Ho, Wo), device=x.device, dtype=x.dtype)
-    if algo == "auto" and not _lib._exact_f32 and \
+    if algo == "auto" and not _lib.exact_f32_enabled() and \
             window_fwd_ok(C, Co, kh, kw, stride, padding, dilation, groups, deformable_groups, W):
         wp = _split_weight(weight)
         K = kh * kw

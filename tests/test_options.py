@@ -46,3 +46,29 @@ def test_module_layer_reads_no_environment():
         if fn.endswith(".py"):
             src = open(os.path.join(root, fn)).read()
             assert "os.environ" not in src and "getenv" not in src, fn
+
+
+def test_exact_f32_is_a_scoped_context_setting_not_an_environment_switch():
+    """the split-bf16 / exact-f32 contraction choice is a per-context setting
+    (`_lib.exact_f32()` scope, `set_exact_f32`), never read from the process environment, and it
+    does not leak into other threads."""
+    import os
+    import subprocess
+    import sys
+    import threading
+
+    from aanet_amd import _lib
+    assert _lib.conv_flags() == 0 and not _lib.exact_f32_enabled()
+    with _lib.exact_f32():
+        assert _lib.conv_flags() == _lib.CONV_EXACT_F32
+        seen = []
+        t = threading.Thread(target=lambda: seen.append(_lib.exact_f32_enabled()))
+        t.start()
+        t.join()
+        assert seen == [False]
+    assert _lib.conv_flags() == 0
+    code = "from aanet_amd import _lib; print(_lib.exact_f32_enabled())"
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                         env={**os.environ, "AANET_EXACT_F32": "1"}, cwd=repo).stdout.strip()
+    assert out == "False"

@@ -9,6 +9,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from aanet_amd import _lib  # noqa: E402
 from tests.test_gpu_models import FLIP, build  # noqa: E402
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "model_psmnet_aa_raw"
@@ -24,5 +25,5 @@ for fuse in (True, False):
         e32 = np.abs(ours - g[f"disp{i}"])
         row.append(f"L{i} flips {int((e64 > FLIP).sum())} (ref {int((eref > FLIP).sum())}) "
                    f"max|d-d32| {e32.max():.2e} mean {e32.mean():.2e}")
-    print(tag, "fused" if fuse else "ref-order", os.environ.get("AANET_EXACT_F32", "0"), " | ".join(row),
+    print(tag, "fused" if fuse else "ref-order", "exact" if _lib.exact_f32_enabled() else "split", " | ".join(row),
           flush=True)
