@@ -333,14 +333,20 @@ def conv2d_fused(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1
                  out_nhwc=False):
     """Plain conv on the HIP implicit-GEMM engine: act(post_scale*(conv+bias)+post_shift+residual).
     weight gives the shape ([co][cg][kh][kw]); packed_weight (pack_weight(weight)) if given is
-    what the kernel reads.  x may be channels_last (NHWC staging); out_nhwc=True returns a
-    channels_last tensor (residual then channels_last too).  NHWC needs packed_weight and
-    32-channel groups (AANET_LAYOUT_*)."""
+    what the kernel reads, and then `weight` may be just that shape (a tuple).  x may be
+    channels_last (NHWC staging); out_nhwc=True returns a channels_last tensor (residual then
+    channels_last too).  NHWC needs packed_weight and 32-channel groups (AANET_LAYOUT_*)."""
+    if not torch.is_tensor(weight):
+        if packed_weight is None:
+            raise ValueError("a weight shape alone needs packed_weight")
+        weight_shape, weight = tuple(weight), None
+    else:
+        weight_shape = tuple(weight.shape)
     require_gpu(x, weight, bias, residual, post_scale, post_shift, packed_weight,
                 names=("input", "weight", "bias", "residual", "post_scale", "post_shift", "packed"),
                 nhwc_ok=(0, 3) if out_nhwc else (0,))
     N, C, H, W = x.shape
-    Co, _, kh, kw = weight.shape
+    Co, _, kh, kw = weight_shape
     Ho, Wo = _out_size(H, kh, stride, padding, dilation), _out_size(W, kw, stride, padding, dilation)
     if residual is not None and tuple(residual.shape) != (N, Co, Ho, Wo):
         raise ValueError("residual shape must match the output")
@@ -724,7 +730,6 @@ def conv2d_dgrad(grad_out, weight, input_hw, stride=1, padding=0, dilation=1, gr
     N, _, Ho, Wo = grad_out.shape
     H, W = input_hw
     # the per-group transposed, flipped weight, packed for the engine in one launch
-    wt = weight.new_empty((groups * Cg, Co // groups, kh, kw))  # shape carrier only
     wp = torch.empty((kh, kw, groups * Cg, Co // groups), device=weight.device, dtype=weight.dtype)
     call("aanet_conv_weight_pack_dgrad_f32", ptr(weight.contiguous()), ptr(wp), Co, Cg, kh, kw, groups,
          stream_of(weight))
@@ -734,8 +739,8 @@ def conv2d_dgrad(grad_out, weight, input_hw, stride=1, padding=0, dilation=1, gr
         dz = grad_out.new_zeros((N, Co, (Ho - 1) * stride + 1 + rh, (Wo - 1) * stride + 1 + rw))
         dz[:, :, : (Ho - 1) * stride + 1 : stride, : (Wo - 1) * stride + 1 : stride] = grad_out
         grad_out = dz
-    gx = conv2d_fused(grad_out.contiguous(), wt, padding=pad_t, dilation=dilation, groups=groups,
-                      packed_weight=wp)
+    gx = conv2d_fused(grad_out.contiguous(), (groups * Cg, Co // groups, kh, kw), padding=pad_t,
+                      dilation=dilation, groups=groups, packed_weight=wp)
     if tuple(gx.shape[2:]) != (H, W):
         raise RuntimeError(f"dgrad shape {tuple(gx.shape)} != input {(H, W)}")
     return gx
