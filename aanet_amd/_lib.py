@@ -144,6 +144,20 @@ CONV_GENERIC_DCN = 32  # AANET_CONV_GENERIC_DCN: generic engine instead of the L
 _EXACT_F32 = contextvars.ContextVar("aanet_exact_f32", default=False)
 
 
+_CACHE_FILLS = [0]
+
+
+def note_cache_fill():
+    """Counted by every eval-path cache (re)fill -- folded / packed weights, BN affines (nets/
+    _fuse.py, ops._split_weight): AdaptiveAggregation._run_chains must order the other chains
+    after the current stream when one happened (the fill's kernels run there)."""
+    _CACHE_FILLS[0] += 1
+
+
+def cache_fills():
+    return _CACHE_FILLS[0]
+
+
 def exact_f32_enabled():
     return _EXACT_F32.get()
 

@@ -40,7 +40,7 @@ def clear_fold_caches(module):
     writes through `.data` and HIP graph replays update a weight without bumping its _version."""
     for m in module.modules():
         for attr in ("_aanet_fold", "_aanet_fold_dense", "_aanet_affine", "_aanet_s2pack",
-                     "_aanet_s2pack_k"):
+                     "_aanet_s2pack_k", "_aanet_g3pack"):
             if attr in m.__dict__:
                 del m.__dict__[attr]
         for p in m.parameters(recurse=False):
@@ -82,6 +82,7 @@ def folded(conv, bn):
         if wp is None:
             wp = ops.pack_weight(w)
     conv._aanet_fold = (key, w, b, wp)
+    _lib.note_cache_fill()
     return w, b, wp
 
 
@@ -114,6 +115,7 @@ def folded_dense(conv, bn):
         wd = wd.contiguous()
         wp = ops.pack_weight_split(wd, 1)
     conv.__dict__["_aanet_fold_dense"] = (key, wd, b, wp)
+    _lib.note_cache_fill()
     return wd, b, wp
 
 
@@ -133,6 +135,7 @@ def s2_pack(owner, pairs):
         wsplit = ops.pack_conv3x3s2(w)
     val = None if wsplit is None else (wsplit, b)
     owner.__dict__["_aanet_s2pack"] = (key, val)
+    _lib.note_cache_fill()
     return val
 
 
@@ -157,6 +160,7 @@ def s2_pack_k(owner, pairs):
         wsplit = ops.pack_conv3x3s2(w)
     val = None if wsplit is None else (wsplit, b.contiguous())
     owner.__dict__["_aanet_s2pack_k"] = (key, val)
+    _lib.note_cache_fill()
     return val
 
 
@@ -167,8 +171,7 @@ def offset_conv_pack(conv):
     Round 4: the kernel is the halo form owning every group of its tile (conv_g3.hip): 94-95 vs
     102-103 us for the engine's halo form at C2 scale 0, step 3.636 vs 3.662 ms (same call,
     DESIGN.md 3), so it is the default; the round-3 direct form was slower than the engine."""
-    if type(conv) is not nn.Conv2d or \
-            not engine_conv(conv) or _int(conv.kernel_size) != 3 or _int(conv.stride) != 1 or \
+    if not engine_conv(conv) or _int(conv.kernel_size) != 3 or _int(conv.stride) != 1 or \
             _int(conv.padding) != _int(conv.dilation) or \
             (conv.in_channels // conv.groups) % 32 or (conv.out_channels // conv.groups) > 32:
         return None
@@ -182,6 +185,7 @@ def offset_conv_pack(conv):
         bias = b.contiguous() if b is not None else None
     val = None if wsplit is None else (wsplit, bias)
     conv.__dict__["_aanet_g3pack"] = (key, val)
+    _lib.note_cache_fill()
     return val
 
 
@@ -218,6 +222,7 @@ def bn_affine(bn):
         scale, shift = bn_scale_shift(bn)
         scale, shift = scale.contiguous(), shift.contiguous()
     bn._aanet_affine = (key, scale, shift)
+    _lib.note_cache_fill()
     return scale, shift
 
 

@@ -16,7 +16,7 @@ from .aggregation3d import (GCNetAggregation, PSMNetBasicAggregation, PSMNetHGAg
 from .cost import CostVolume, CostVolumePyramid
 from ._fuse import FoldCacheMixin
 from .estimation import DisparityEstimation
-from .options import set_options
+from .options import get_option, set_options
 from .feature import (FeaturePyramidNetwork, FeaturePyrmaid, GANetFeature, GCNetFeature,
                       PSMNetFeature, StereoNetFeature)
 from .refinement import HourglassRefinement, StereoDRNetRefinement, StereoNetRefinement
@@ -170,7 +170,8 @@ class AANet(FoldCacheMixin, nn.Module):
             # kernel's epilogue (AdaptiveAggregation._run)
             regress = (not self.aggregation.intermediate_supervision and not self.training and
                        self.disparity_estimation.match_similarity)
-            aggregation, disp = self.aggregation._run(cost_volume, regress=regress)
+            aggregation, disp = self.aggregation._run(
+                cost_volume, regress=regress, chains=get_option(self.aggregation, "batch_chains"))
         else:
             aggregation = self.aggregation(cost_volume)
         disparity_pyramid = [disp] if disp is not None else self.disparity_computation(aggregation)

@@ -14,7 +14,7 @@ import contextlib
 import torch
 import torch.nn as nn
 
-from .. import ops
+from .. import _lib, ops
 from ._fuse import FoldCacheMixin, conv_bn_act, folded, s2_conv_ok, s2_pack, s2_pack_k, use_fused
 from .deform import DeformSimpleBottleneck, SimpleBottleneck
 from .._precision import fp32_convs
@@ -471,16 +471,86 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
         """aggregation.py:452-464 (final 1x1 conv with bias on the HIP conv engine in eval)."""
         return self._run(cost_volume)[0]
 
-    def _run(self, cost_volume, regress=False):
+    def _run(self, cost_volume, regress=False, chains=1):
         """-> (aggregated cost volumes, disparity or None).  In eval on the fused path each
         fusion's scale-0 tail kernel also computes the next fusion's conv1 (post stage); with
         `regress` (the caller's DisparityEstimation is the plain similarity soft-argmin and there
         is one output scale) the last tail computes final_conv + the regression too, and the
-        cost-volume list is then None."""
+        cost-volume list is then None.  chains > 1 (the whole-model callers, option
+        batch_chains): the batch is split into that many chunks, each aggregated on its own
+        stream (_run_chains); the caller's list is then not mutated."""
         assert isinstance(cost_volume, list)
         fused = use_fused(self, cost_volume[0])
+        if chains > 1 and fused and cost_volume[0].is_cuda and cost_volume[0].shape[0] >= 2:
+            return self._run_chains(cost_volume, regress, min(chains, cost_volume[0].shape[0]))
+        return self._run_one(cost_volume, regress, fused)
+
+    def _run_chains(self, cost_volume, regress, k):
+        """Batch pipelining: the pairs are independent, so chunk c of the batch runs the whole
+        aggregation on its own stream -- chunk 0 on the current stream (with the concurrent-scale
+        side streams), chunk c >= 1 on side stream S - 1 + c with the one-stream schedule.  The
+        small, serially dependent kernels of one chunk (stride-2 heads, the coarse scales) then
+        run beside the large scale-0 tail kernels of another.  Every stream waits only for the
+        current stream and the current stream joins every stream (the only cross-stream edges
+        HIP graph capture takes).  Each pair's arithmetic is unchanged: bit-identical results."""
+        dev = cost_volume[0].device
+        main = torch.cuda.current_stream(dev)
+        B = cost_volume[0].shape[0]
+        bounds = [B * c // k for c in range(k + 1)]
+        chunks = [[t[bounds[c]:bounds[c + 1]] for t in cost_volume] for c in range(k)]
+        extra = side_streams(dev, max(self.num_scales - 1, 0) + k - 1)[max(self.num_scales - 1, 0):]
+        ready = _record(main)  # the cost volumes exist
+        strm = [main] + extra[:k - 1]
+        gens = [self._run_steps(chunks[0], regress, True)]
+        for c in range(1, k):
+            strm[c].wait_event(ready)
+            with torch.cuda.stream(strm[c]):
+                gens.append(self._run_steps(chunks[c], regress, True, concurrent=False))
+        # Issue the chunks fusion by fusion, round robin: the HIP graph executor launches the
+        # captured nodes in capture order, and chunk-by-chunk issue ran the chunks one after the
+        # other (profiles/r06_chains_timeline.txt, tools/step_big_kernels.py).  A step that (re)fills a weight cache (first
+        # call, new weights) ran those kernels on its own stream: the other streams catch up with
+        # it, through the current stream, before their next step.
+        results, live, behind = [None] * k, list(range(k)), set()
+        while live:
+            for c in list(live):
+                if c in behind:
+                    strm[c].wait_stream(main)
+                    behind.discard(c)
+                fills = _lib.cache_fills()
+                try:
+                    with torch.cuda.stream(strm[c]):
+                        next(gens[c])
+                except StopIteration as done:
+                    results[c] = done.value
+                    live.remove(c)
+                if _lib.cache_fills() != fills:
+                    if c:
+                        main.wait_stream(strm[c])
+                    behind = set(range(1, k)) - {c}
+        for c in range(1, k):
+            r = results[c]
+            for t in ([r[1]] if r[1] is not None else r[0]):
+                t.record_stream(main)  # allocated on a side stream, read on main below
+        for st in extra[:k - 1]:
+            main.wait_stream(st)
+        if results[0][1] is not None:
+            return None, torch.cat([r[1] for r in results])
+        return [torch.cat([r[0][i] for r in results]) for i in range(len(results[0][0]))], None
+
+    def _run_one(self, cost_volume, regress, fused, concurrent=True):
+        gen = self._run_steps(cost_volume, regress, fused, concurrent)
+        while True:
+            try:
+                next(gen)
+            except StopIteration as done:
+                return done.value
+
+    def _run_steps(self, cost_volume, regress, fused, concurrent=True):
+        """_run_one as a generator: one fusion per step (yields after each), the result as its
+        return value; the caller keeps the stream it started on current across steps."""
         streams = None
-        if fused and cost_volume[0].is_cuda and self.num_scales > 1 and \
+        if fused and cost_volume[0].is_cuda and self.num_scales > 1 and concurrent and \
                 get_option(self, "concurrent_scales"):
             dev = cost_volume[0].device
             main = torch.cuda.current_stream(dev)
@@ -504,6 +574,7 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
             pre = res["out"] if res is not None else None
             if res is not None and res.get("disp") is not None:
                 disp = res["disp"]
+            yield
         if streams is not None:
             for st in ss:
                 main.wait_stream(st)

@@ -14,7 +14,7 @@ from .aggregation import AdaptiveAggregation
 from .cost import CostVolume, CostVolumePyramid
 from ._fuse import FoldCacheMixin
 from .estimation import DisparityEstimation
-from .options import set_options
+from .options import get_option, set_options
 from .._precision import fp32_convs
 
 
@@ -65,7 +65,9 @@ class AANetHotPath(FoldCacheMixin, nn.Module):
     @fp32_convs
     def forward(self, left_feature, right_feature):
         cost_volume = self.cost_volume_construction(left_feature, right_feature)
-        aggregation, disp = self.aggregation._run(cost_volume, regress=self.regress_in_tail())
+        aggregation, disp = self.aggregation._run(
+            cost_volume, regress=self.regress_in_tail(),
+            chains=get_option(self.aggregation, "batch_chains"))
         if disp is not None:  # final_conv + soft-argmin ran in the last tail kernel's epilogue
             return [disp]
         return self.disparity_computation(aggregation)

@@ -18,6 +18,10 @@ summation order; tests/test_gpu_production.py, test_gpu_post.py, test_gpu_dense_
   s2_sums            True: output branches 1 and 2 are summed in the stride-2 kernels'
                      epilogues; False: separate aanet_csa_sum_f32 kernels.
                                                                       (AdaptiveAggregationModule)
+  batch_chains       k >= 1: the whole-model forwards (AANetHotPath, AANet) split the batch into
+                     k chunks, each aggregated on its own stream (batch pipelining: one chunk's
+                     small serial kernels beside another's large ones); 1: one chain.
+                     Bit-identical results.                           (AdaptiveAggregation)
   dense_grouped      True: 2-group convs with 16-channel groups (the scale-1 offset conv) run as
                      one block-diagonal ungrouped conv on the split-bf16 engine; False: the
                      grouped exact-f32 engine.                        (every nn.Conv2d)
@@ -25,7 +29,7 @@ summation order; tests/test_gpu_production.py, test_gpu_post.py, test_gpu_dense_
 import torch.nn as nn
 
 DEFAULTS = {"concurrent_scales": True, "post_fusion": "all", "s2_sums": True,
-            "dense_grouped": True}
+            "batch_chains": 1, "dense_grouped": True}
 _POST = ("all", "final", "none")
 
 
@@ -43,11 +47,15 @@ def set_options(module, **options):
         if name == "post_fusion":
             if value not in _POST:
                 raise ValueError(f"post_fusion must be one of {_POST}, got {value!r}")
+        elif name == "batch_chains":
+            if isinstance(value, bool) or not isinstance(value, int) or value < 1:
+                raise ValueError(f"batch_chains must be an int >= 1, got {value!r}")
         elif not isinstance(value, bool):
             raise ValueError(f"{name} must be a bool, got {value!r}")
     from .aggregation import AdaptiveAggregation, AdaptiveAggregationModule
     targets = {"concurrent_scales": AdaptiveAggregation, "post_fusion": AdaptiveAggregation,
-               "s2_sums": AdaptiveAggregationModule, "dense_grouped": nn.Conv2d}
+               "s2_sums": AdaptiveAggregationModule, "batch_chains": AdaptiveAggregation,
+               "dense_grouped": nn.Conv2d}
     for m in module.modules():
         for name, value in options.items():
             if isinstance(m, targets[name]):

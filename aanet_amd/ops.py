@@ -233,6 +233,7 @@ def _split_weight(weight):
     if not capturing:
         try:
             weight._aanet_split_pack = (key, wp)
+            _lib.note_cache_fill()
         except (AttributeError, RuntimeError):
             pass
     return wp

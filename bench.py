@@ -77,7 +77,19 @@ def parse():
                          "(tests/test_distributed.py); never a metric")
     ap.add_argument("--only", default=None,
                     help="profiling mode: run only one kernel family (corr|mdcn|regress|step)")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="eval schedule option of the model (aanet_amd/nets/options.py), e.g. "
+                         "side_heads=false; repeatable (A/B runs; recorded in config.options)")
     return ap.parse_args()
+
+
+def parse_options(items):
+    """--option NAME=VALUE list -> set_options kwargs (true/false -> bool)."""
+    out = {}
+    for it in items:
+        k, _, v = it.partition("=")
+        out[k] = {"true": True, "false": False}.get(v.lower(), int(v) if v.isdigit() else v)
+    return out
 
 
 def build_model(device, intermediate_supervision=False):
@@ -501,6 +513,9 @@ def main():
         dcn_sweep_main(args, device, rank)
         return
     model = build_model(device)
+    opts = parse_options(args.option)
+    if opts:
+        model.set_options(**opts)
     left, right = make_features(args.batch, rank, device, args.features)
 
     def step():
@@ -553,6 +568,7 @@ def main():
                 "global_batch": args.batch * world,
                 "parallelism": f"dp{world} (pairs sharded, no data-path collective)",
                 "hip_graph": graph is not None, "schedule": getattr(args, "schedule", None),
+                **({"options": parse_options(args.option)} if args.option else {}),
             },
             "roofline": {"kernel": dom_name, "bound": dom["bound"], "achieved": dom["achieved"],
                          "peak": dom["peak"], "unit": dom["unit"], "frac": dom["frac"],

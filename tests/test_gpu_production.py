@@ -241,6 +241,36 @@ def test_two_stream_schedule_graph_replay_and_single_stream_match():
                 assert torch.equal(a, b) and torch.equal(a, c)
 
 
+@pytest.mark.parametrize("chains", [2, 3])
+def test_batch_chains_bit_identical_eager_and_graph(chains):
+    """The batch-pipelined schedule (set_options(batch_chains=k): chunk c of the batch aggregated
+    on its own stream, every edge through the capturing stream) gives the one-chain result bit for
+    bit -- each pair's kernels and inputs are the same -- eagerly on the first (cache-filling) and
+    a later call, and in HIP graph replays.  B = 4 (the d64 case twice), so chunks are uneven at
+    k = 3."""
+    g, sd, m, left, right = _model("hotpath_d64")
+    left = [torch.cat([t, t.flip(0)]) for t in left]
+    right = [torch.cat([t, t.flip(0)]) for t in right]
+    with torch.no_grad():
+        one = [t.clone() for t in m(left, right)]
+        m.set_options(batch_chains=chains)
+        try:
+            from aanet_amd.nets._fuse import clear_fold_caches
+            clear_fold_caches(m)  # the first chained call refills every cache
+            for _ in range(2):
+                got = m(left, right)
+                assert all(torch.equal(a, b) for a, b in zip(one, got))
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                static = m(left, right)
+            for _ in range(3):
+                graph.replay()
+                torch.cuda.synchronize()
+                assert all(torch.equal(a, b) for a, b in zip(one, static))
+        finally:
+            m.set_options(batch_chains=1)
+
+
 def test_s2_sums_option_matches_separate_csa_sums():
     """The coarse branches' CSA sums in the stride-2 kernels' epilogues (s2_sums=True, default)
     against separate aanet_csa_sum_f32 kernels (s2_sums=False): the same terms in another fp32
