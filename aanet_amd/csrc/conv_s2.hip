@@ -83,23 +83,36 @@ __device__ __forceinline__ void for_steps(F &&f, std::integer_sequence<int, S...
   (f(std::integral_constant<int, S>{}), ...);
 }
 
-// epilogue: channel co = 16m + 4kr + r of pixel (y, x); rows of 16 pixels = 64-byte segments.
-// Branch-free in the (wave-uniform) term pointers and the (lane-varying) output choice: each pair
-// of co blocks issues all its term loads first (lanes / tensors without a term read x[0] and
-// discard it), then adds them with selects, then stores through a selected pointer.  Written with
-// per-value branches, the compiler waited for every term load in turn (48 serial round trips at
-// the C2 heads launch).  The arithmetic is the reference order: bias, identity, resized term, act.
+// epilogue: channel co = co_base + 16m + 4kr + r of pixel (y, x).  Every global access is a
+// buffer op on a per-image resource: a 32-bit lane offset (channel 4kr's plane + the pixel, or the
+// resize corner) formed once, and a wave-uniform plane offset per (m, r) in an SGPR, so no access
+// pays 64-bit address arithmetic (round 6: the 64-bit form was 1,963 of the kernel's 3,238 static
+// VALU at the C2 heads shape).  co_a is a multiple of 16, so a 16-channel block lies wholly in
+// output a (where the CSA terms apply) or wholly in output b: one wave-uniform branch per block.
+// The term loads of a block are all issued before its first use.  The arithmetic is the
+// reference order: bias, identity, resized term, act.
 template <int NCB>
 __device__ __forceinline__ void s2_epilogue(const S2Args &a, const f32x4 (&acc)[NCB], int n, int y, int x,
                                             int kr, int co_base, bool pv) {
   const int Ho = a.Ho, Wo = a.Wo;
   if (!pv) return;
-  const long P = (long)Ho * Wo, pix = (long)y * Wo + x;
-  const int cb = a.Co - a.co_a;
+  const int P = Ho * Wo, pix = y * Wo + x;
+  const int co_a = a.co_a, cb = a.Co - co_a;
   const bool hid = a.id != nullptr, hup = a.up != nullptr;
+  const int upa = a.up_h * a.up_w;
+  // per-image resources (num_records: that image's planes; the host checks the 2^31 bound)
+  const auto r_id = __builtin_amdgcn_make_buffer_rsrc((void *)(hid ? a.id + (long)n * co_a * P : a.x),
+                                                      (short)0, hid ? co_a * P * 4 : 0, 0x00020000);
+  const auto r_up = __builtin_amdgcn_make_buffer_rsrc((void *)(hup ? a.up + (long)n * co_a * upa : a.x),
+                                                      (short)0, hup ? co_a * upa * 4 : 0, 0x00020000);
+  const auto r_oa = __builtin_amdgcn_make_buffer_rsrc((void *)(co_a ? a.out[0] + (long)n * co_a * P : a.x),
+                                                      (short)0, co_a * P * 4, 0x00020000);
+  const auto r_ob = __builtin_amdgcn_make_buffer_rsrc((void *)(cb ? a.out[1] + (long)n * cb * P : a.x),
+                                                      (short)0, cb * P * 4, 0x00020000);
+  const int lo = (4 * kr * P + pix) * 4;  // channel 4kr's plane + this pixel
   // the resize stencil of this pixel (PyTorch upsample_bilinear2d, align_corners=False, as in
   // csa.hip's bilinear_resize): the same four offsets and weights for every channel plane
-  int o00 = 0, o01 = 0, o10 = 0, o11 = 0;
+  int lu[4] = {0, 0, 0, 0};
   float h0l = 0.f, h1l = 0.f, w0l = 0.f, w1l = 0.f;
   if (hup) {
     float hr = a.up_sh * ((float)y + 0.5f) - 0.5f;
@@ -110,73 +123,45 @@ __device__ __forceinline__ void s2_epilogue(const S2Args &a, const f32x4 (&acc)[
     const int h1p = h1 < a.up_h - 1 ? 1 : 0, w1p = w1 < a.up_w - 1 ? 1 : 0;
     h1l = hr - (float)h1, h0l = 1.f - h1l;
     w1l = wr - (float)w1, w0l = 1.f - w1l;
-    o00 = h1 * a.up_w + w1, o01 = o00 + w1p;
-    o10 = (h1 + h1p) * a.up_w + w1, o11 = o10 + w1p;
+    const int o00 = h1 * a.up_w + w1, o10 = (h1 + h1p) * a.up_w + w1;
+    const int lb = 4 * kr * upa;
+    lu[0] = (lb + o00) * 4;
+    lu[1] = (lb + o00 + w1p) * 4;
+    lu[2] = (lb + o10) * 4;
+    lu[3] = (lb + o10 + w1p) * 4;
   }
-  const long upa = (long)a.up_h * a.up_w;
-  constexpr int MB = NCB >= 2 ? 2 : 1;  // co blocks per batch of term loads
 #pragma unroll
-  for (int m0 = 0; m0 < NCB; m0 += MB) {
-    float tid[MB][4] = {}, tq[MB][4][4] = {};
-    if (hid) {  // wave-uniform: whole batches of loads, never one branch per value
+  for (int m = 0; m < NCB; ++m) {
+    const int cm = co_base + 16 * m;  // wave-uniform
+    const int c4 = cm + 4 * kr;
+    const f32x4 bs = a.bias ? *reinterpret_cast<const f32x4 *>(a.bias + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    if (cm < co_a) {
+      float tid[4] = {}, tq[4][4] = {};
+      if (hid) {
 #pragma unroll
-      for (int mm = 0; mm < MB; ++mm)
+        for (int r = 0; r < 4; ++r)
+          tid[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r_id, lo, (cm + r) * P * 4, 0));
+      }
+      if (hup) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int co = co_base + 16 * (m0 + mm) + 4 * kr + r;
-          const bool ina = co < a.co_a;
-          tid[mm][r] = *(ina ? a.id + ((long)n * a.co_a + co) * P + pix : a.x);
-        }
-    }
-    if (hup) {
+        for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int mm = 0; mm < MB; ++mm)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int co = co_base + 16 * (m0 + mm) + 4 * kr + r;
-          const bool ina = co < a.co_a;
-          const float *im = ina ? a.up + ((long)n * a.co_a + co) * upa : a.x;
-          tq[mm][r][0] = im[ina ? o00 : 0];
-          tq[mm][r][1] = im[ina ? o01 : 0];
-          tq[mm][r][2] = im[ina ? o10 : 0];
-          tq[mm][r][3] = im[ina ? o11 : 0];
-        }
-    }
-#pragma unroll
-    for (int mm = 0; mm < MB; ++mm) {
-      const int m = m0 + mm, c4 = co_base + 16 * m + 4 * kr;
-      const f32x4 bs = a.bias ? *reinterpret_cast<const f32x4 *>(a.bias + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
-      float res[4];
+          for (int q = 0; q < 4; ++q)
+            tq[r][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r_up, lu[q], (cm + r) * upa * 4, 0));
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = c4 + r;
-        const bool ina = co < a.co_a;
         float v = acc[m][r] + bs[r];
-        const float vi = v + tid[mm][r];
-        v = (hid && ina) ? vi : v;
-        const float vu = v + (h0l * (w0l * tq[mm][r][0] + w1l * tq[mm][r][1]) +
-                              h1l * (w0l * tq[mm][r][2] + w1l * tq[mm][r][3]));
-        v = (hup && ina) ? vu : v;
-        v = s2_act(v, ina ? a.act[0] : a.act[1]);
-        res[r] = v;
+        if (hid) v = v + tid[r];
+        if (hup) v = v + (h0l * (w0l * tq[r][0] + w1l * tq[r][1]) + h1l * (w0l * tq[r][2] + w1l * tq[r][3]));
+        v = s2_act(v, a.act[0]);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r_oa, lo, (cm + r) * P * 4, 0);
       }
-      // stores: a wave-uniform branch when the whole 16-channel block lies in one output (always
-      // for 16-multiple co_a), a per-lane pointer select otherwise
-      const int cm = co_base + 16 * m;
-      if (cm + 16 <= a.co_a) {
+    } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) a.out[0][((long)n * a.co_a + c4 + r) * P + pix] = res[r];
-      } else if (cm >= a.co_a) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) a.out[1][((long)n * cb + c4 + r - a.co_a) * P + pix] = res[r];
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int co = c4 + r;
-          float *dst = co < a.co_a ? a.out[0] + ((long)n * a.co_a + co) * P + pix
-                                   : a.out[1] + ((long)n * cb + co - a.co_a) * P + pix;
-          *dst = res[r];
-        }
+      for (int r = 0; r < 4; ++r) {
+        const float v = s2_act(acc[m][r] + bs[r], a.act[1]);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), r_ob, lo, (cm - co_a + r) * P * 4, 0);
       }
     }
   }
@@ -401,6 +386,8 @@ int aanet_conv3x3s2_terms_f32(const float *x, const void *wsplit, const float *b
   if ((co_a > 0 && !out_a) || (co_a < co && !out_b)) return AANET_EINVAL;
   if ((long)c * h * w * 4 >= (1L << 31) || (long)c2 * h * w * 4 >= (1L << 31)) return AANET_EUNSUPPORTED;
   const int ho = (h + 1) / 2, wo = (w + 1) / 2;
+  // the epilogue's block-uniform output choice and 32-bit buffer offsets
+  if (co_a % 16 || (long)co * ho * wo * 4 >= (1L << 31)) return AANET_EUNSUPPORTED;
   const bool has_terms = terms && (terms->identity || terms->up);
   if (has_terms && co_a == 0) return AANET_EINVAL;
   if (terms && terms->up && (terms->up_h <= 0 || terms->up_w <= 0)) return AANET_EINVAL;
