@@ -33,6 +33,16 @@ def side_streams(device, n):
     return ss[:n]
 
 
+_PREP_STREAMS = {}
+
+
+def prep_stream(device):
+    """The side stream of the deformable scale-0 conv1 + offset conv (option prep_stream)."""
+    if device not in _PREP_STREAMS:
+        _PREP_STREAMS[device] = torch.cuda.Stream(device=device)
+    return _PREP_STREAMS[device]
+
+
 def _record(stream):
     ev = torch.cuda.Event()
     ev.record(stream)
@@ -201,7 +211,7 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
             return self._down(heads[i], i, 0, start=1)
         return self._down(x[0], i, 0)
 
-    def _forward_eval(self, x, streams=None, keep=None, conv1_pre=None, post=None):
+    def _forward_eval(self, x, streams=None, keep=None, conv1_pre=None, post=None, sched=None):
         """Eval ISA + CSA.  The coarser scales run first, so that their exchange terms for output
         branch 0 exist when the scale-0 bottleneck runs: its tail kernel then writes both the
         block output and the cross-scale sum of branch 0 (aanet_csa_epilogue_t), which removes
@@ -224,7 +234,11 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
 
         conv1_pre: the scale-0 bottleneck's conv1 output, already computed by the previous
         module's tail kernel (its post stage); post: this module's scale-0 tail post stage (the
-        next module's conv1, or final_conv + regression), result in post["result"]."""
+        next module's conv1, or final_conv + regression), result in post["result"].
+        sched: state shared by the modules of one AdaptiveAggregation run.  With the prep_stream
+        option a deformable scale-0 block's conv1 + offset conv run on their own side stream as
+        soon as the previous module's scale-0 tail has written x[0] (sched["tail_ev"]), beside
+        that module's stride-2 heads, instead of after them on the current stream."""
         S = len(self.branches)
         nout = len(self.fuse_layers)
         if streams is None:
@@ -269,11 +283,18 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
         for b in range(self.num_blocks - 1):
             x[0] = self.branches[0][b](x[0])
         ok = csa_epilogue_ok(x[0], up0)
+        prep = None
+        if sched is not None and self.num_blocks == 1 and sched.get("tail_ev") is not None and \
+                get_option(self, "prep_stream"):
+            prep = (prep_stream(x[0].device), sched["tail_ev"], keep)
         x[0], csa0 = self.branches[0][self.num_blocks - 1].forward_csa(
             x[0], up0 if ok else None, before_tail=join,
-            conv1_out=conv1_pre if self.num_blocks == 1 else None, post=post if ok else None)
+            conv1_out=conv1_pre if self.num_blocks == 1 else None, post=post if ok else None,
+            prep=prep)
         if post is not None and not ok:
             post["result"] = None
+        if sched is not None:
+            sched["tail_ev"] = _record(main)  # x[0] / out[0] written: the next module's prep
         if post is not None and post.get("result") is not None:
             keep.extend(v for v in post["result"].values() if v is not None)
         keep.append(x[0])
@@ -352,13 +373,13 @@ class AdaptiveAggregationModule(FoldCacheMixin, nn.Module):
         return x_fused
 
     @fp32_convs
-    def forward(self, x, streams=None, keep=None, conv1_pre=None, post=None):
-        """aggregation.py:375-402.  streams / keep: the concurrent-scale schedule of
+    def forward(self, x, streams=None, keep=None, conv1_pre=None, post=None, sched=None):
+        """aggregation.py:375-402.  streams / keep / sched: the concurrent-scale schedule of
         AdaptiveAggregation (eval only, see _forward_eval); conv1_pre / post: the cross-module
         pointwise fusions of AdaptiveAggregation (eval only)."""
         assert len(self.branches) == len(x)
         if self.num_scales > 1 and use_fused(self, x[0]) and getattr(self, "aanet_fuse_csa", True):
-            return self._forward_eval(x, streams, keep, conv1_pre, post)
+            return self._forward_eval(x, streams, keep, conv1_pre, post, sched)
         if post is not None:
             post["result"] = None
         if streams is not None:  # reference op sequence: one stream
@@ -559,13 +580,15 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
             for st in ss:
                 st.wait_stream(main)  # the cost volumes are written on the current stream
             keep = list(cost_volume)
+            sched = {}
         pre, disp = None, None
         post_ok = fused and cost_volume[0].is_cuda and get_option(self, "post_fusion") != "none"
         for i in range(self.num_fusions):
             fusion = self.fusions[i]
             post = self._post_for(i, regress) if post_ok else None
             if streams is not None:
-                cost_volume = fusion(cost_volume, streams, keep, conv1_pre=pre, post=post)
+                cost_volume = fusion(cost_volume, streams, keep, conv1_pre=pre, post=post,
+                                     sched=sched)
             elif post_ok:
                 cost_volume = fusion(cost_volume, conv1_pre=pre, post=post)
             else:
@@ -578,6 +601,8 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
         if streams is not None:
             for st in ss:
                 main.wait_stream(st)
+            if dev in _PREP_STREAMS:
+                main.wait_stream(_PREP_STREAMS[dev])
             del keep
         if disp is not None:
             return None, disp

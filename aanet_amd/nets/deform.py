@@ -11,6 +11,8 @@ into the 1x1/3x3 convs, and the deformable conv2 -> bn2 -> ReLU done by ONE kern
 the offset_conv output in place (offset slice + 2*sigmoid(mask logits)) and applies BN+ReLU
 in its epilogue.
 """
+import contextlib
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -132,7 +134,8 @@ class _BottleneckBase(FoldCacheMixin, nn.Module):
         out = self.relu(out)
         return out
 
-    def _forward_fused(self, x, deform, conv1_out=None, csa_up=None, before_tail=None, post=None):
+    def _forward_fused(self, x, deform, conv1_out=None, csa_up=None, before_tail=None, post=None,
+                       prep=None):
         """conv1+bn1+relu, then conv2+bn2+relu -> conv3+bn3 (+identity) + relu as ONE HIP kernel
         (the conv3 GEMM runs in conv2's epilogue).  When the tail kernel takes the block, conv1
         writes its output channels-last (NHWC) so that conv2 / offset_conv / the DCN read each
@@ -143,7 +146,10 @@ class _BottleneckBase(FoldCacheMixin, nn.Module):
         before the tail kernel is launched (the stream join of the concurrent-scale schedule,
         AdaptiveAggregation: csa_up is produced on the side stream).  post (with csa_up): the
         tail kernel's post stage on the CSA output (ops._post_stage); its results are stored in
-        post["result"] (None when the kernel did not take the stage)."""
+        post["result"] (None when the kernel did not take the stage).  prep = (stream, event,
+        keep): the deformable block's conv1 and offset_conv run on that side stream once the
+        event (its input is written) has fired, beside whatever the current stream does before
+        the tail; the tail waits for them (the concurrent-scale schedule, AdaptiveAggregation)."""
         w3, b3, p3 = folded(self.conv3, self.bn3)
         width = self.conv1.weight.shape[0]
         c2 = self.conv2
@@ -156,14 +162,27 @@ class _BottleneckBase(FoldCacheMixin, nn.Module):
             pw = c2.groups == 1 and width <= 64 and w3.shape[0] <= 64 and \
                 c2.stride[0] == c2.stride[1] and c2.padding[0] == c2.padding[1]
             nhwc = pw and width % 32 == 0
-        if conv1_out is None:
-            out = conv_bn_act(x, self.conv1, self.bn1, "relu", out_nhwc=nhwc)
+        prep = prep if deform and self.conv2.modulation and pw else None
+        main = torch.cuda.current_stream(x.device) if prep is not None else None
+        if prep is not None:
+            prep[0].wait_event(prep[1])
+            ctx = torch.cuda.stream(prep[0])
         else:
-            out = conv1_out
+            ctx = contextlib.nullcontext()
+        with ctx:
+            if conv1_out is None:
+                out = conv_bn_act(x, self.conv1, self.bn1, "relu", out_nhwc=nhwc)
+            else:
+                out = conv1_out
+            # (the non-pw DCN path computes its offsets in forward_fused)
+            offset_mask = offset_conv_eval(out, c2.offset_conv) \
+                if deform and self.conv2.modulation and pw else None
+        if prep is not None:
+            main.wait_stream(prep[0])
+            prep[2].extend((out, offset_mask))  # written on the side stream, read below
         identity = (self.downsample(x) if self.downsample is not None else x).contiguous()
         if deform and self.conv2.modulation:
             dc = c2.deform_conv
-            offset_mask = offset_conv_eval(out, c2.offset_conv)
             ps, psh = bn_affine(self.bn2)
             _, _, wp = folded(dc, None)
             if pw:
@@ -190,12 +209,12 @@ class _BottleneckBase(FoldCacheMixin, nn.Module):
         out = conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity)
         return out if csa_up is None else (out, None)
 
-    def forward_csa(self, x, csa_up, before_tail=None, conv1_out=None, post=None):
+    def forward_csa(self, x, csa_up, before_tail=None, conv1_out=None, post=None, prep=None):
         """Eval-only: (block output, its output branch's CSA sum or None); see _forward_fused.
         conv1_out: this block's conv1 output, computed by the previous tail's post stage."""
         deform = isinstance(self, DeformSimpleBottleneck) or isinstance(self, DeformBottleneck)
         r = self._forward_fused(x, deform=deform, csa_up=None if csa_up is None else list(csa_up),
-                                before_tail=before_tail, conv1_out=conv1_out, post=post)
+                                before_tail=before_tail, conv1_out=conv1_out, post=post, prep=prep)
         return r if isinstance(r, tuple) else (r, None)
 
 

@@ -18,6 +18,9 @@ summation order; tests/test_gpu_production.py, test_gpu_post.py, test_gpu_dense_
   s2_sums            True: output branches 1 and 2 are summed in the stride-2 kernels'
                      epilogues; False: separate aanet_csa_sum_f32 kernels.
                                                                       (AdaptiveAggregationModule)
+  prep_stream        True: a deformable scale-0 block's conv1 + offset conv run on a side stream
+                     as soon as x[0] exists, beside the previous module's stride-2 heads;
+                     False: on the current stream after the heads.   (AdaptiveAggregationModule)
   batch_chains       k >= 1: the whole-model forwards (AANetHotPath, AANet) split the batch into
                      k chunks, each aggregated on its own stream (batch pipelining: one chunk's
                      small serial kernels beside another's large ones); 1: one chain.
@@ -29,7 +32,7 @@ summation order; tests/test_gpu_production.py, test_gpu_post.py, test_gpu_dense_
 import torch.nn as nn
 
 DEFAULTS = {"concurrent_scales": True, "post_fusion": "all", "s2_sums": True,
-            "batch_chains": 1, "dense_grouped": True}
+            "prep_stream": True, "batch_chains": 1, "dense_grouped": True}
 _POST = ("all", "final", "none")
 
 
@@ -54,7 +57,8 @@ def set_options(module, **options):
             raise ValueError(f"{name} must be a bool, got {value!r}")
     from .aggregation import AdaptiveAggregation, AdaptiveAggregationModule
     targets = {"concurrent_scales": AdaptiveAggregation, "post_fusion": AdaptiveAggregation,
-               "s2_sums": AdaptiveAggregationModule, "batch_chains": AdaptiveAggregation,
+               "s2_sums": AdaptiveAggregationModule, "prep_stream": AdaptiveAggregationModule,
+               "batch_chains": AdaptiveAggregation,
                "dense_grouped": nn.Conv2d}
     for m in module.modules():
         for name, value in options.items():

@@ -701,6 +701,12 @@ FULL_MODELS = {
                   no_intermediate_supervision=True),
     "aanetplus": dict(feature_type="ganet", feature_pyramid=True, refinement_type="hourglass",
                       no_intermediate_supervision=True),
+    # BASELINE configs[4] (C5): the 4-D concat cost volume (nets/cost.py:22-38) at 384x1248,
+    # D=192 (48 at the 1/4 feature scale): PSMNet features + the PSMNet hourglass 3-D aggregator,
+    # and PSMNet-AA (the same features, adaptive aggregation on the correlation pyramid)
+    "psmnet_hg": dict(feature_type="psmnet", feature_similarity="concat",
+                      aggregation_type="psmnet_hourglass", refinement_type=None),
+    "psmnet_aa": dict(feature_type="psmnet", feature_pyramid=True, no_intermediate_supervision=True),
 }
 
 

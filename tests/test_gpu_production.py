@@ -241,6 +241,26 @@ def test_two_stream_schedule_graph_replay_and_single_stream_match():
                 assert torch.equal(a, b) and torch.equal(a, c)
 
 
+def test_prep_stream_option_bit_identical():
+    """prep_stream (a deformable scale-0 block's conv1 + offset conv on their own side stream,
+    beside the previous module's stride-2 heads) only moves kernels between streams: the same
+    bits as prep_stream=False, eagerly and under HIP graph replay (run to run, three times)."""
+    g, sd, m, left, right = _model("hotpath_d64")
+    with torch.no_grad():
+        m.set_options(prep_stream=False)
+        ref = [t.clone() for t in m(left, right)]
+        m.set_options(prep_stream=True)
+        for _ in range(3):
+            assert all(torch.equal(a, b) for a, b in zip(ref, m(left, right)))
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            static = m(left, right)
+        for _ in range(3):
+            graph.replay()
+            torch.cuda.synchronize()
+            assert all(torch.equal(a, b) for a, b in zip(ref, static))
+
+
 @pytest.mark.parametrize("chains", [2, 3])
 def test_batch_chains_bit_identical_eager_and_graph(chains):
     """The batch-pipelined schedule (set_options(batch_chains=k): chunk c of the batch aggregated

@@ -14,11 +14,12 @@ def test_defaults_and_propagation():
     agg = m.aggregation
     for k, v in DEFAULTS.items():
         target = {"concurrent_scales": agg, "post_fusion": agg, "s2_sums": agg.fusions[0],
-                  "batch_chains": agg,
+                  "batch_chains": agg, "prep_stream": agg.fusions[4],
                   "dense_grouped": agg.fusions[5].branches[1][0].conv2.offset_conv}[k]
         assert get_option(target, k) == v
     assert m.set_options(concurrent_scales=False, post_fusion="final", s2_sums=False,
-                         dense_grouped=False, batch_chains=2) is m
+                         dense_grouped=False, batch_chains=2, prep_stream=False) is m
+    assert all(get_option(f, "prep_stream") is False for f in agg.fusions)
     assert get_option(agg, "batch_chains") == 2
     assert get_option(agg, "concurrent_scales") is False
     assert get_option(agg, "post_fusion") == "final"

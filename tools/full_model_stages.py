@@ -8,7 +8,7 @@ ConvTranspose2d / Conv3d / DeformConv2d in a reference-order pass (the fused pat
 forwards; the FLOPs are the same), 2 * MACs; bytes: every conv's input + output once (a lower
 bound on HBM traffic).  Each stage is priced against the roof its intensity puts it under:
 FLOP/byte above the ridge (416.7 TF/s split-bf16 / 8 TB/s = 52) -> MFMA (416.7 TF/s fp32-equiv),
-below -> HBM (8 TB/s).  Usage: python tools/full_model_stages.py [aanet|aanetplus] [--iters N]
+below -> HBM (8 TB/s).  Usage: python tools/full_model_stages.py [aanet|aanetplus|psmnet_aa|psmnet_hg] [--iters N]
 """
 import json
 import os
@@ -20,6 +20,7 @@ import torch.nn as nn
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 from aanet_amd.nets import AANet  # noqa: E402
+from aanet_amd.nets.aggregation import AdaptiveAggregation  # noqa: E402
 from aanet_amd.nets.deform import DeformConv2d  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("-") else "aanet"
@@ -61,6 +62,9 @@ def stages(m):
         st["cv"] = m.cost_volume_construction(st["lf"], st["rf"])
 
     def agg():
+        if not isinstance(m.aggregation, AdaptiveAggregation):  # 3-D aggregators (C5)
+            st["disp"] = m.disparity_computation(m.aggregation(st["cv"]))
+            return
         regress = (not m.aggregation.intermediate_supervision and not m.training and
                    m.disparity_estimation.match_similarity)
         a, d = m.aggregation._run(st["cv"], regress=regress)
@@ -84,8 +88,11 @@ def hook(mod, inp, out):
     if isinstance(mod, DeformConv2d):
         w = mod.deform_conv.weight
         macs = o.numel() * w.shape[1] * w.shape[2] * w.shape[3]
-    elif isinstance(mod, nn.ConvTranspose2d):
-        macs = x.numel() * mod.out_channels * mod.kernel_size[0] * mod.kernel_size[1] // mod.groups
+    elif isinstance(mod, nn.modules.conv._ConvTransposeNd):
+        k = 1
+        for v in mod.kernel_size:
+            k *= v
+        macs = x.numel() * (mod.out_channels // mod.groups) * k
     else:
         k = 1
         for v in mod.kernel_size:
@@ -97,7 +104,7 @@ def hook(mod, inp, out):
 
 handles = []
 for mod in model.modules():
-    if isinstance(mod, (nn.Conv2d, nn.ConvTranspose2d, nn.Conv3d, DeformConv2d)):
+    if isinstance(mod, (nn.modules.conv._ConvNd, DeformConv2d)):
         handles.append(mod.register_forward_hook(hook))
 for mod in model.modules():
     mod.aanet_fuse = False
