@@ -20,11 +20,15 @@ summation order; tests/test_gpu_production.py, test_gpu_post.py, test_gpu_dense_
                                                                       (AdaptiveAggregationModule)
   prep_stream        True: a deformable scale-0 block's conv1 + offset conv run on a side stream
                      as soon as x[0] exists, beside the previous module's stride-2 heads;
-                     False: on the current stream after the heads.   (AdaptiveAggregationModule)
+                     False (default): on the current stream after the heads.  Measured round 6:
+                     3.27 vs 3.22-3.23 ms (the heads slow down more than the prep gains;
+                     bit-identical either way).                       (AdaptiveAggregationModule)
   batch_chains       k >= 1: the whole-model forwards (AANetHotPath, AANet) split the batch into
                      k chunks, each aggregated on its own stream (batch pipelining: one chunk's
                      small serial kernels beside another's large ones); 1: one chain.
-                     Bit-identical results.                           (AdaptiveAggregation)
+                     Bit-identical results.  Measured round 6 (HIP graph): k = 2 / 3 / 4 3.34 /
+                     3.96 / 3.79 ms against 3.22 (profiles/r06_chains_timeline.txt).
+                                                                      (AdaptiveAggregation)
   dense_grouped      True: 2-group convs with 16-channel groups (the scale-1 offset conv) run as
                      one block-diagonal ungrouped conv on the split-bf16 engine; False: the
                      grouped exact-f32 engine.                        (every nn.Conv2d)
@@ -32,7 +36,7 @@ summation order; tests/test_gpu_production.py, test_gpu_post.py, test_gpu_dense_
 import torch.nn as nn
 
 DEFAULTS = {"concurrent_scales": True, "post_fusion": "all", "s2_sums": True,
-            "prep_stream": True, "batch_chains": 1, "dense_grouped": True}
+            "prep_stream": False, "batch_chains": 1, "dense_grouped": True}
 _POST = ("all", "final", "none")
 
 

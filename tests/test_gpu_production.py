@@ -250,6 +250,14 @@ def test_prep_stream_option_bit_identical():
         m.set_options(prep_stream=False)
         ref = [t.clone() for t in m(left, right)]
         m.set_options(prep_stream=True)
+        try:
+            _prep_runs(m, left, right, ref)
+        finally:
+            m.set_options(prep_stream=False)
+
+
+def _prep_runs(m, left, right, ref):
+    with torch.no_grad():
         for _ in range(3):
             assert all(torch.equal(a, b) for a, b in zip(ref, m(left, right)))
         graph = torch.cuda.CUDAGraph()
