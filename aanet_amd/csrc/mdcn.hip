@@ -1754,8 +1754,9 @@ __global__ __launch_bounds__(NT) void mdcn_bwd_data_nhwc_kernel(MdcnArgs a, cons
   }
 }
 
-// Window form of mdcn_bwd_data_nhwc_kernel (stride 1, <= 32 channels per deformable group,
-// K <= 9 taps, <= 64 output channels).  The workgroup owns an 8 x 8 output tile and one deformable group, and walks the
+// Window form of mdcn_bwd_data_nhwc_kernel (stride 1 or 2, <= 128 channels per deformable group,
+// K <= 9 taps, <= 128 output channels; round 6 added the feature extractor's stride-2, 64-channel
+// group, Co = 128 shapes).  The workgroup owns an 8 x 8 output tile and one deformable group, and walks the
 // group's channels in 16-channel slices: per slice it sums the grad_x corner contributions in an
 // LDS copy of the tile's input window (rows/cols [origin, origin + WR/WC): the corners of every
 // offset in [-R, R)), then adds the window to the global accumulator once -- one global add per
@@ -1794,7 +1795,7 @@ constexpr int WHC = 16;  // channels per window slice
 // conflict-free; the engine's CP = 80 left them 4- to 8-way conflicted
 constexpr int WCP = PT + 2;
 constexpr int WKMAX = 9; // taps the sP partial buffer holds
-constexpr int WCOMAX = 64;  // output channels (the W^T slice is prefetched in registers)
+constexpr int WCOMAX = 128;  // output channels (the W^T slice is prefetched in registers)
 constexpr int GW_COPIES = 8; // copies of the fused weight-gradient accumulator, summed afterwards
 template <int DET, int FUSEW = 0>
 __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, const float *__restrict__ xh,
@@ -1832,7 +1833,8 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
   // different XCDs: one copy per XCD keeps the atomics on one element from crossing them)
   const long gwc = (long)(blockIdx.x & (GW_COPIES - 1)) * K * Co * C;
   const float *xn = xh + (long)n * HW * C;
-  const int wy0 = ty0 - a.pad - R, wx0 = tx0 - a.pad - R;  // window origin (stride 1)
+  // window origin: the tile's first input row / column (stride s: 8 output pixels span 7s + 1)
+  const int wy0 = ty0 * a.stride - a.pad - R, wx0 = tx0 * a.stride - a.pad - R;
   const int nwin = WR * WCc * WHC;
   auto pix = [&](int pl) -> long {  // linear output pixel of tile pixel pl, or -1
     const int y = ty0 + (pl >> 3), x = tx0 + (pl & 7);
@@ -1938,24 +1940,28 @@ __global__ __launch_bounds__(NT, 2) void mdcn_bwd_data_win_kernel(MdcnArgs a, co
       }
       __syncthreads();
       if constexpr (FUSEW) {
-        // this tile's weight-gradient block: wave w = output channels 16w..16w+15, the slice's 16
-        // channels, K = the tile's 64 pixels; one float atomic per element into gwT[k][co][c]
-        f32x4 wacc = {0.f, 0.f, 0.f, 0.f};
-        for (int ks = 0; ks < PT / 4; ++ks) {
-          const float av = sG[(16 * wave + jj) * GP + 4 * ks + kr];
-          const float bv = sCol[jj * WCP + 4 * ks + kr];
-          wacc = mfma16x16x4(av, bv, wacc);
-        }
-        if (jj < rows) {
+        // this tile's weight-gradient block: wave w = output channels cbk + 16w .. + 15 for each
+        // 64-channel block cbk (Co <= 128, Co % 16 == 0: whole blocks), the slice's 16 channels,
+        // K = the tile's 64 pixels; one float atomic per element into gwT[k][co][c]
+        for (int cbk = 0; cbk < Co; cbk += 64) {
+          const int cw = cbk + 16 * wave;  // wave-uniform
+          if (cw >= Co) break;
+          f32x4 wacc = {0.f, 0.f, 0.f, 0.f};
+          for (int ks = 0; ks < PT / 4; ++ks) {
+            const float av = sG[(cw + jj) * GP + 4 * ks + kr];
+            const float bv = sCol[jj * WCP + 4 * ks + kr];
+            wacc = mfma16x16x4(av, bv, wacc);
+          }
+          if (jj < rows) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int co = 16 * wave + 4 * kr + r;
-            if (co >= Co) continue;
-            if (DET)  // int64 fixed point: the sum does not depend on the order of the tiles
-              atomicAdd(reinterpret_cast<unsigned long long *>(gwi) + gwc + ((long)k * Co + co) * C + cb0 + jj,
-                        (unsigned long long)__double2ll_rn((double)wacc[r] * wscale));
-            else
-              atomicAdd(gwT + gwc + ((long)k * Co + co) * C + cb0 + jj, wacc[r]);
+            for (int r = 0; r < 4; ++r) {
+              const int co = cw + 4 * kr + r;
+              if (DET)  // int64 fixed point: the sum does not depend on the order of the tiles
+                atomicAdd(reinterpret_cast<unsigned long long *>(gwi) + gwc + ((long)k * Co + co) * C + cb0 + jj,
+                          (unsigned long long)__double2ll_rn((double)wacc[r] * wscale));
+              else
+                atomicAdd(gwT + gwc + ((long)k * Co + co) * C + cb0 + jj, wacc[r]);
+            }
           }
         }
       }
@@ -3180,16 +3186,22 @@ struct DetLayout {
 
 bool bwd_nhwc_reads(const MdcnArgs &a);
 // the window form's LDS (mdcn_bwd_impl), fused weight gradient, and whether a shape takes it
+// the window of an 8 x 8 output tile: 7 * stride + 1 input rows / columns under the taps' reach,
+// plus the R = 2 margin on both sides (offsets in [-2, 2) stay inside)
+int win_rows(int kh, int dil, int stride) { return 7 * stride + 1 + (kh - 1) * dil + 4; }
 size_t win_smem(const MdcnArgs &a) {
   const int GPW = round_pitch(PT, 2), WTP = round_pitch(a.Co, 2);
-  const int WR = 8 + (a.kh - 1) * a.dil + 4, WCw = 8 + (a.kw - 1) * a.dil + 4;
+  const int WR = win_rows(a.kh, a.dil, a.stride), WCw = win_rows(a.kw, a.dil, a.stride);
   return sizeof(float) * ((size_t)a.Co * GPW + (size_t)WHC * WTP + (size_t)WHC * WCP + (size_t)PT * 16 +
                           (size_t)3 * WKMAX * PT + (size_t)WHC * WCP) +
          (size_t)WR * WCw * WHC * 8;
 }
+// round 6: stride 2, up to 128 channels per deformable group (the 16-channel slices' offset /
+// mask partials accumulate in sP in slice order) and up to 128 output channels (the fused weight
+// gradient loops over 64-channel blocks): the feature extractor's DCNs (nets/resnet.py:133-134)
 bool win_shape_ok(const MdcnArgs &a) {
-  return bwd_nhwc_reads(a) && a.stride == 1 && a.C / a.dg <= 2 * WHC && a.kh * a.kw <= WKMAX &&
-         a.Co <= WCOMAX && win_smem(a) <= 160 * 1024;
+  return bwd_nhwc_reads(a) && (a.stride == 1 || a.stride == 2) && a.C / a.dg <= 8 * WHC &&
+         a.kh * a.kw <= WKMAX && a.Co <= WCOMAX && a.Co % 16 == 0 && win_smem(a) <= 160 * 1024;
 }
 
 // The deterministic backward runs over the batch in chunks of images whose int64 grad_x
@@ -3274,12 +3286,12 @@ int mdcn_bwd_core(const float *x, const float *offset, const float *mask, const 
   }
   const bool nr = nhs && bwd_nhwc_reads(a);  // channels-last reads too
   const int GP = round_pitch(PT, 16), WTP = round_pitch(co, 2);
-  // window form of grad_x (stride 1, <= 32 channels per deformable group, channels-last reads,
+  // window form of grad_x (stride 1 / 2, <= 128 channels per deformable group, channels-last reads,
   // <= 9 taps, <= 64 output channels): 8x8 tile per workgroup in 16-channel slices, int64
   // fixed-point LDS window.
   // AUTO takes it in both modes; GLOBAL / WINDOW force one form (tests, A/B).
   const int R = 2;
-  const int WR = 8 + (kh - 1) * dil + 2 * R, WCw = 8 + (kw - 1) * dil + 2 * R;
+  const int WR = win_rows(kh, dil, stride), WCw = win_rows(kw, dil, stride);
   const bool fusew = true;  // the weight gradient rides in the window kernel (both modes)
   // gOut tile pitch of the window kernel: 80 (= 16 mod 32) keeps the colg reads (rows kr,
   // columns jj) conflict-free; the fused weight gradient also reads it transposed (rows jj), which

@@ -630,13 +630,14 @@ DCN_BWD_ALGOS = {"auto": 0, "global": 1, "window": 2}  # AANET_DCN_BWD_* (includ
 def window_bwd_ok(C, Co, kh, kw, stride, dilation, deformable_groups):
     """Whether AANET_DCN_BWD_WINDOW takes a DCN backward shape (mdcn.hip win_shape_ok; the full
     list of include/aanet_mi355x.h).  The LDS term: gOut tile, W^T slice, sampling / partial
-    buffers, sampled columns and the int64 window of (8 + (k-1) dil + 4)^2 positions x 16
+    buffers, sampled columns and the int64 window of (7 s + 1 + (k-1) dil + 4)^2 positions x 16
     channels, within the CU's 160 KiB."""
     cpg = C // deformable_groups
-    if stride != 1 or cpg > 32 or C % 4 or cpg % 4 or kh * kw > 9 or Co > 64:
+    if stride not in (1, 2) or cpg > 128 or C % 4 or cpg % 4 or kh * kw > 9 or Co > 128 or Co % 16:
         return False
     pitch = lambda v: v + (2 - v % 32) % 32  # noqa: E731  (mdcn.hip round_pitch(v, 2))
-    wr, wc = 8 + (kh - 1) * dilation + 4, 8 + (kw - 1) * dilation + 4
+    # mdcn.hip win_rows: 7 * stride + 1 rows under an 8-pixel tile + the taps' reach + 2 x 2
+    wr, wc = 7 * stride + 1 + (kh - 1) * dilation + 4, 7 * stride + 1 + (kw - 1) * dilation + 4
     smem = 4 * (Co * pitch(64) + 16 * pitch(Co) + 16 * 66 + 64 * 16 + 3 * 9 * 64 + 16 * 66) \
         + wr * wc * 16 * 8
     return smem <= 160 * 1024

@@ -361,9 +361,9 @@ int aanet_mdcn_bwd_ws_f32(const float *x, const float *offset, const float *mask
  *     depend on atomic ordering. The fixed-point scale is a power of two chosen on the device from
  *     max_{c,k} sum_co |W| * max|grad_out| * max|mask|, so there is no host synchronisation.
  *   - grad_weight: partial sums reduced in a fixed order -- per split of the weight kernel, or,
- *     when the window form applies (stride 1, <= 32 channels per deformable group, <= 9 taps,
- *     <= 64 output channels, C and C/dg multiples of 4), one partial per 8x8 output tile of the
- *     window kernel, summed over 64 chunks of consecutive tiles and then over the chunks.
+ *     when the window form applies (stride 1 or 2, <= 128 channels per deformable group, <= 9
+ *     taps, <= 128 output channels in multiples of 16, C and C/dg multiples of 4), int64
+ *     fixed-point sums of every 8x8 output tile's weight-gradient block (order-free).
  * `workspace` (device, caller-owned) must hold aanet_mdcn_bwd_det_workspace_size(...) bytes; with
  * the window form that includes tiles * co * c * kh * kw floats of tile partials
  * (tiles = n * ceil(ho / 8) * ceil(wo / 8)).
@@ -385,8 +385,9 @@ enum {
   AANET_DCN_BWD_GLOBAL = 1, /* one global atomic per (pixel, tap, corner, channel) contribution,
                                the reference's col2im pattern (kernel.cu:635-693), into an NHWC
                                accumulator */
-  AANET_DCN_BWD_WINDOW = 2  /* stride 1, <= 32 channels per deformable group, C and C/dg
-                               divisible by 4, <= 9 taps, Co <= 64, and the window's LDS
+  AANET_DCN_BWD_WINDOW = 2  /* stride 1 or 2, <= 128 channels per deformable group, C and C/dg
+                               divisible by 4, <= 9 taps, Co <= 128 and a multiple of 16, and the
+                               window's LDS
                                (grows with the dilation) within the CU's 160 KiB: each
                                (8x8 output tile, 16-channel slice) sums its
                                contributions in an int64 fixed-point LDS window and adds the

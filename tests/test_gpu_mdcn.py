@@ -337,6 +337,29 @@ def test_mdcn_backward_c4_agg_s0_vs_oracle(form):
         assert err.max() <= 1e-4 * scale + 1e-6, f"{form} {name}: max err {err.max():.3g} (scale {scale:.3g})"
 
 
+@pytest.mark.parametrize("shape", ["feat_s1", "feat_s2"])
+@pytest.mark.parametrize("det", [False, True])
+def test_mdcn_backward_c4_feature_dcn_window_vs_oracle(shape, det):
+    """SURVEY C4 at the feature extractor's DCN shapes (nets/resnet.py:133-134: 128 channels, two
+    deformable groups of 64, Co = 128, dil 2; stride 1 at 32x104 and stride 2 from 64x208), one
+    image at full size: the window form (round 6: 64-channel groups in four 16-channel slices,
+    Co = 128 in two 64-channel weight-gradient blocks, the stride-2 window) against the oracle,
+    float and fixed-point."""
+    N, C, Co, k, p, d, dg = 1, 128, 128, 3, 2, 2, 2
+    H, W, s = (32, 104, 1) if shape == "feat_s1" else (64, 208, 2)
+    assert ops.window_bwd_ok(C, Co, k, k, s, d, dg)
+    x, off, msk, w, b = make_case(13, N, C, H, W, Co, k, s, p, d, dg, off_scale=0.7)
+    Ho, Wo = off.shape[2:]
+    go = np.random.default_rng(14).standard_normal((N, Co, Ho, Wo)).astype(np.float32)
+    got = ops.mdcn_backward(g2t(x), g2t(off), g2t(msk), g2t(w), g2t(go), True, s, p, d, 1, dg,
+                            deterministic=det, algo="window")
+    ref = oracle.mdcn_backward(x, off, msk, w, go, True, s, p, d, 1, dg)
+    for name, gt, r in zip(("grad_input", "grad_offset", "grad_mask", "grad_weight", "grad_bias"), got, ref):
+        err = np.abs(t2n(gt) - r)
+        scale = np.abs(r).max() + 1e-12
+        assert err.max() <= 1e-4 * scale + 1e-6, f"{shape} det={det} {name}: max err {err.max():.3g}"
+
+
 @pytest.mark.parametrize("det", [False, True])
 @pytest.mark.parametrize("bad", [np.inf, np.nan])
 def test_mdcn_backward_nonfinite_grad_out_propagates(det, bad):
