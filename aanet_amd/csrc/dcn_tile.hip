@@ -72,6 +72,12 @@ __device__ __forceinline__ f32x4 mfma_split6(const bf16x8 (&A)[3], const bf16x8 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0], B[0], t, 0, 0, 0);
 }
 
+// the resource of an optional tensor's image planes: an absent tensor gets 0 records (its loads
+// return 0, its stores are dropped), on any valid base
+__device__ __forceinline__ brsrc_t opt_rsrc(const float *p, const float *any, long img, long bytes) {
+  return buf_rsrc(p ? p + img : any, p ? bytes : 0);
+}
+
 // branch-free in the wave-uniform act (selects, not scalar branches that split the epilogue
 // into per-value basic blocks); same values as relu / leaky(0.2) / identity
 __device__ __forceinline__ float act_f(float v, int act) {
@@ -445,17 +451,23 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   const int Co2 = a.Co2;
   f32x4 er[EPT];
   float eb[EPT];
-  long eo[EPT];
+  unsigned eo[EPT];  // byte offset of the item in image n's [Co2][H][W] planes
   bool eok[EPT];
   const bool res = a.residual && !(dbg & 16), csa = a.csa_out && !(dbg & 16);
+  // buffer resources over image n's planes (SGPRs) and 32-bit byte offsets per item (round 6: a
+  // 64-bit plane product and pointer per access, as the conv engine's epilogue had before round 5)
+  const long img2 = (long)n * Co2 * P, img_b = (long)Co2 * P * 4;
+  const brsrc_t ro = opt_rsrc(a.out, a.x, img2, img_b);
+  const brsrc_t rcs = opt_rsrc(a.csa_out, a.x, img2, img_b);
+  const brsrc_t rre = opt_rsrc(a.residual, a.x, img2, img_b);
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
     const int e = tid + NT * i, co2 = e >> 5, qi = e & 31, yy = y0 + (qi >> 2), xx = x0 + 4 * (qi & 3);
     eok[i] = co2 < Co2 && yy < H && xx < W;
-    eo[i] = ((long)(n * Co2 + co2) * H + yy) * W + xx;
+    eo[i] = 4u * (unsigned)(co2 * P + yy * W + xx);
     if (!eok[i]) continue;
     eb[i] = a.tail_b ? a.tail_b[co2] : 0.f;
-    if (res) er[i] = *reinterpret_cast<const f32x4 *>(a.residual + eo[i]);
+    if (res) er[i] = buf_ld4(rre, eo[i]);
   }
 
   // ---- tail: BN2 + act -> conv3 (pointwise, split-bf16) ----------------------------------------
@@ -531,38 +543,45 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   // CSA source rows, segment start and row weights are computed once per thread (round 5: per
   // item and term, in both passes, before)
   const int qit = tid & 31, yyt = y0 + (qit >> 2), xxt = x0 + 4 * (qit & 3);
-  int urow0[2] = {0, 0}, urow1[2] = {0, 0}, us0[2] = {0, 0};
+  unsigned urow0[2] = {0u, 0u}, urow1[2] = {0u, 0u}, uhw[2] = {0u, 0u};
+  int us0[2] = {0, 0}, uiw[2] = {4, 4};
   float uh0[2] = {1.f, 1.f}, uh1[2] = {0.f, 0.f};
+  brsrc_t ru[2] = {ro, ro};
+  bool sfast = true;
   if (csa) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       if (j >= a.num_up) break;
       const int ih = a.up_h[j], iw = a.up_w[j], r = a.up_r[j];
+      ru[j] = buf_rsrc(a.up[j] + (long)n * Co2 * ih * iw, (long)Co2 * ih * iw * 4);
+      uhw[j] = 4u * (unsigned)(ih * iw);
+      uiw[j] = iw;
       // PyTorch's area_pixel_compute_scale (ih / H) and source row, align_corners=False
       float hr = ((float)ih / (float)H) * ((float)yyt + 0.5f) - 0.5f;
       hr = hr < 0.f ? 0.f : hr;
       const int h1 = (int)hr, h1p = h1 < ih - 1 ? 1 : 0;
-      urow0[j] = h1 * iw;
-      urow1[j] = (h1 + h1p) * iw;
+      urow0[j] = 4u * (unsigned)(h1 * iw);
+      urow1[j] = 4u * (unsigned)((h1 + h1p) * iw);
       us0[j] = r == 2 ? 2 * (xxt >> 2) - 1 : (xxt >> 2) - 1;
+      sfast = sfast && us0[j] >= 0 && us0[j] + 3 <= iw - 1;
       uh1[j] = hr - (float)h1;
       uh0[j] = 1.f - uh1[j];
     }
   }
+  // the image-edge quads read clamped columns: a wave with one takes the per-column loads
+  const bool wfast = __all(sfast || !(yyt < H && xxt < W));
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
     const int e = tid + NT * i, co2 = e >> 5, qi = e & 31;
     ev[i] = *reinterpret_cast<const f32x4 *>(sO + co2 * OP + (qi >> 2) * 16 + 4 * (qi & 3));
     if (!eok[i]) continue;
     if (csa) {
-      const long plane = (long)n * Co2 + co2;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         if (j >= a.num_up) break;
-        const int iw = a.up_w[j];
-        const float *im = a.up[j] + plane * (a.up_h[j] * iw);
-        eu[i][j][0] = load_seg(im + urow0[j], iw, us0[j]);
-        eu[i][j][1] = load_seg(im + urow1[j], iw, us0[j]);
+        const unsigned pl = (unsigned)co2 * uhw[j];
+        eu[i][j][0] = buf_seg(ru[j], pl + urow0[j], us0[j], uiw[j], wfast);
+        eu[i][j][1] = buf_seg(ru[j], pl + urow1[j], us0[j], uiw[j], wfast);
       }
     }
   }
@@ -582,7 +601,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   for (int i = 0; i < EPT; ++i) {
     if (!eok[i]) continue;
     if (dbg & 16) {  // no epilogue traffic (keeps the work alive)
-      if (ev[i][0] == 12345.f) a.out[eo[i]] = ev[i][1];
+      if (ev[i][0] == 12345.f) buf_st4(ro, eo[i], ev[i]);
       continue;
     }
     const int e = tid + NT * i, qi = e & 31;
@@ -593,7 +612,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       if (res) t += er[i][u];
       v[u] = act_f(t, a.tail_act);
     }
-    if (!post || !a.post_skip) *reinterpret_cast<f32x4 *>(a.out + eo[i]) = v;
+    if (!post || !a.post_skip) buf_st4(ro, eo[i], v);
     if (csa) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -602,7 +621,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) v[u] = act_f(v[u], a.csa_act);
-      if (!post || !a.post_skip) *reinterpret_cast<f32x4 *>(a.csa_out + eo[i]) = v;
+      if (!post || !a.post_skip) buf_st4(rcs, eo[i], v);
     }
     if (post)  // the branch output back into the item's own slot: the post stage's B operand
       *reinterpret_cast<f32x4 *>(sO + (e >> 5) * OP + (qi >> 2) * 16 + 4 * (qi & 3)) = v;

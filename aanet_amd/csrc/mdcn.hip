@@ -3302,7 +3302,13 @@ int mdcn_bwd_core(const float *x, const float *offset, const float *mask, const 
                        (size_t)WR * WCw * WHC * 8;
   const bool win_ok = nr && win_shape_ok(a) && smem3 <= 160 * 1024;
   if (algo == AANET_DCN_BWD_WINDOW && !win_ok) return AANET_EUNSUPPORTED;
-  const bool use_win = win_ok && (algo == AANET_DCN_BWD_WINDOW || algo == AANET_DCN_BWD_AUTO);
+  // AUTO takes the window form where it measured faster: the aggregation's shapes (stride 1,
+  // <= 32 channels per group, Co <= 64).  At the feature extractor's shapes (64-channel groups,
+  // Co = 128, one workgroup per CU for its LDS) it measured slower in float mode (C4 feat_s1 /
+  // feat_s2 990 / 1089 us vs 853 / 856 us global) and mixed in fixed point (983 vs 1046 us at
+  // stride 1, 1177 vs 1073 at stride 2; CHANGELOG.md round 6): WINDOW selects it there.
+  const bool win_auto = a.stride == 1 && a.C / a.dg <= 2 * WHC && a.Co <= 64;
+  const bool use_win = win_ok && (algo == AANET_DCN_BWD_WINDOW || (algo == AANET_DCN_BWD_AUTO && win_auto));
   float *xh = nhs ? reinterpret_cast<float *>(wb + L.xh) : nullptr;
   float *wt = nhs ? reinterpret_cast<float *>(wb + L.wt) : nullptr;
   long long *gxi = det ? reinterpret_cast<long long *>(wb + L.gxi) : nullptr;

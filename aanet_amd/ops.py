@@ -648,11 +648,11 @@ def mdcn_backward(x, offset, mask, weight, grad_out, with_bias, stride, padding,
     """deform_conv_cuda.cpp:571-685 -> (gX, gOffset, gMask, gW, gB or None).
 
     Default: aanet_mdcn_bwd_algo_f32 with the caller-owned workspace; algo "auto" takes the
-    LDS-window form of grad_x where it applies (window_bwd_ok: stride 1, <= 32 channels per
-    deformable group, C and C/dg divisible by 4, <= 9 taps, Co <= 64, and the window's LDS within
-    160 KiB; int64 fixed-point window in both modes) and the global-atomic
-    form otherwise; "window" / "global" force one form (AANET_EUNSUPPORTED if the window form
-    does not apply).  nchw_scatter=True: the workspace-free aanet_mdcn_bwd_f32 (global atomics in NCHW).
+    LDS-window form of grad_x where it measured faster (stride 1, <= 32 channels per deformable
+    group, Co <= 64: the aggregation's DCNs; int64 fixed-point window in both modes) and the
+    global-atomic form otherwise; "window" / "global" force one form ("window" also takes the
+    feature extractor's stride-2, 64-channel-group, Co = 128 shapes -- window_bwd_ok --
+    AANET_EUNSUPPORTED where it does not apply).  nchw_scatter=True: the workspace-free aanet_mdcn_bwd_f32 (global atomics in NCHW).
 
     deterministic (default: torch.are_deterministic_algorithms_enabled()): the bit-reproducible
     form (fixed-point grad_x accumulation, ordered grad_W reduction) instead of float atomics."""

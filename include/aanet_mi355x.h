@@ -381,7 +381,9 @@ int aanet_mdcn_bwd_det_f32(const float *x, const float *offset, const float *mas
  * AANET_DCN_BWD_AUTO).  deterministic: 0 = float atomics (workspace of
  * aanet_mdcn_bwd_ws_workspace_size bytes), 1 = fixed point (aanet_mdcn_bwd_det_workspace_size). */
 enum {
-  AANET_DCN_BWD_AUTO = 0,   /* the window form where it applies, else global (both modes) */
+  AANET_DCN_BWD_AUTO = 0,   /* the window form where it measured faster (stride 1, <= 32
+                               channels per deformable group, Co <= 64: the aggregation's DCNs),
+                               else global (both modes) */
   AANET_DCN_BWD_GLOBAL = 1, /* one global atomic per (pixel, tap, corner, channel) contribution,
                                the reference's col2im pattern (kernel.cu:635-693), into an NHWC
                                accumulator */
