@@ -14,6 +14,7 @@
 // floor / bilinear follow kernel.cu:467-497 with fp contraction disabled, so im2col values
 // and sampling indices equal the CPU oracle's bit for bit (tests/test_gpu_mdcn.py).
 #include "common.h"
+#include "dcn_small.h"
 #include "dcn_tile.h"
 #include "pointwise.h"
 #include "small_conv.h"
@@ -2497,6 +2498,35 @@ MdcnArgs make_args(const float *x, const float *offset, long off_bs, const float
   return a;
 }
 
+// DcnSmallArgs of the op-level form (no tail) from the engine's arguments
+DcnSmallArgs small_args(const MdcnArgs &a, const float *weight, int packed) {
+  DcnSmallArgs t{};
+  t.x = a.x;
+  t.offset = a.offset;
+  t.off_bs = a.off_bs;
+  t.mask = a.mask;
+  t.mask_bs = a.mask_bs;
+  t.mask_logits = a.mask_logits;
+  t.mask_scale = a.mask_scale;
+  t.w = weight;
+  t.packed = packed;
+  t.bias = a.bias;
+  t.post_scale = a.post_scale;
+  t.post_shift = a.post_shift;
+  t.act = a.act;
+  t.out = a.out;
+  t.N = a.N;
+  t.C = a.C;
+  t.H = a.H;
+  t.W = a.W;
+  t.Co = a.Co;
+  t.Co2 = a.Co;
+  t.pad = a.pad;
+  t.dil = a.dil;
+  t.dg = a.dg;
+  return t;
+}
+
 template <int MODE, int CO_T, int PTT, int FULL, int CFG>
 void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
   const dim3 blk(FNT);
@@ -2836,6 +2866,12 @@ extern "C" int aanet_mdcn_fwd_f32(const float *x, const float *offset, const flo
                                   int dil, int groups, int dg, aanet_stream_t stream) {
   MdcnArgs a = make_args(x, offset, -1, mask, -1, 0, 1.f, weight, bias, nullptr, nullptr, 0, out,
                          n, c, h, w, co, kh, kw, stride, pad, dil, groups, dg);
+  // 16 channels in two 8-channel groups (the aggregation's coarsest scale): direct fp32 form
+  if (!check_shapes(a) && groups == 1 && a.Ho == h && a.Wo == w &&
+      dcn_small_supported(c, co, 0, kh, kw, stride, pad, dil, dg, groups)) {
+    const int rc = dcn_small_launch(small_args(a, weight, 0), as_hip(stream));
+    if (rc != AANET_EUNSUPPORTED) return rc;
+  }
   return launch_fwd<1>(a, 0, as_hip(stream));
 }
 
@@ -3007,6 +3043,18 @@ extern "C" int aanet_mdcn_pw_f32(const float *x, const float *offset, long offse
     if (rc2 != AANET_EUNSUPPORTED) return rc2;
   }
   if (a.post) return AANET_EUNSUPPORTED;  // the generic engine has no post stage
+  // the coarsest scale's 16-channel block (two 8-channel groups): direct fp32 form (dcn_small.hip)
+  if (!generic && layout == 0 && !a.csa_out && a.Ho == h && a.Wo == w &&
+      dcn_small_supported(c, co, co2, kh, kw, stride, pad, dil, dg, 1)) {
+    DcnSmallArgs t = small_args(a, weight_packed, 1);
+    t.tail_w = pw_weight_packed;
+    t.tail_b = pw_bias;
+    t.tail_act = pw_act;
+    t.residual = residual;
+    t.Co2 = co2;
+    const int rc2 = dcn_small_launch(t, as_hip(stream));
+    if (rc2 != AANET_EUNSUPPORTED) return rc2;
+  }
   return launch_fwd<1>(a, 1, as_hip(stream));
 }
 
@@ -3054,6 +3102,11 @@ extern "C" int aanet_mdcn_fwd_fused_f32(const float *x, const float *offset,
     t.x_nchw = a.layout == 0;
     t.plain = 1;
     const int rc = dcn_tile_launch(t, as_hip(stream));
+    if (rc != AANET_EUNSUPPORTED) return rc;
+  }
+  if (!generic && a.layout == 0 && groups == 1 && a.Ho == h && a.Wo == w &&
+      dcn_small_supported(c, co, 0, kh, kw, stride, pad, dil, dg, groups)) {
+    const int rc = dcn_small_launch(small_args(a, weight, weight_packed), as_hip(stream));
     if (rc != AANET_EUNSUPPORTED) return rc;
   }
   return launch_fwd<1>(a, weight_packed, as_hip(stream));

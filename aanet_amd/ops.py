@@ -239,13 +239,21 @@ def _split_weight(weight):
     return wp
 
 
+def direct_fwd_ok(C, Co, kh, kw, stride, padding, dilation, groups, deformable_groups):
+    """Whether the DCN forward entry points take the direct few-channel kernel (dcn_small.hip
+    dcn_small_supported: 16 channels in two 8-channel groups, Co = 16, 3x3, stride 1, pad = dil)."""
+    return (C, Co, kh, kw, stride, groups, deformable_groups) == (16, 16, 3, 3, 1, 1, 2) and \
+        padding == dilation >= 1
+
+
 def mdcn_forward(x, offset, mask, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
                  deformable_groups=1, out=None, algo="auto"):
     """deform_conv_cuda.cpp:490-569 -> [N, Co, Ho, Wo].
 
     algo "auto": the aggregation's DCN shapes (window_fwd_ok) run the LDS-window kernel on the
     split-bf16 contraction (weights packed by pack_weight_split, cached per weight version),
-    the rest the generic engine (aanet_mdcn_fwd_f32); "generic" forces the latter."""
+    the rest aanet_mdcn_fwd_f32 (16 channels in two groups: the direct kernel, dcn_small.hip;
+    else the generic engine); "generic" forces the generic engine (AANET_CONV_GENERIC_DCN)."""
     require_gpu(x, offset, mask, weight, bias, names=("input", "offset", "mask", "weight", "bias"))
     N, C, H, W = x.shape
     Co, _, kh, kw = weight.shape
@@ -260,6 +268,13 @@ def mdcn_forward(x, offset, mask, weight, bias=None, stride=1, padding=0, dilati
              ptr(mask), deformable_groups * K * Ho * Wo, 0, 1.0, ptr(wp), 1, ptr(bias), None, None,
              0, ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation, groups,
              deformable_groups, _lib.CONV_WEIGHTS_SPLIT, stream_of(x))
+        return out
+    if algo == "generic":
+        K = kh * kw
+        call("aanet_mdcn_fwd_fused_f32", ptr(x), ptr(offset), 2 * deformable_groups * K * Ho * Wo,
+             ptr(mask), deformable_groups * K * Ho * Wo, 0, 1.0, ptr(weight), 0, ptr(bias), None,
+             None, 0, ptr(out), N, C, H, W, Co, kh, kw, stride, padding, dilation, groups,
+             deformable_groups, _lib.CONV_GENERIC_DCN, stream_of(x))
         return out
     call("aanet_mdcn_fwd_f32", ptr(x), ptr(offset), ptr(mask), ptr(weight), ptr(bias), ptr(out),
          N, C, H, W, Co, kh, kw, stride, padding, dilation, groups, deformable_groups, stream_of(x))

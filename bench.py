@@ -30,6 +30,7 @@ sys.path.insert(0, REPO)
 
 METRIC = "stereo-pairs/s @384x1248 D=64 fp32, 1/2/4/8 MI355X; EPE vs ref"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+STORE_CEILING_GBS = 6490.0  # measured store-only ceiling (profiles/r06_write_ceiling.txt: hipMemsetAsync)
 FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 = f32 vector rate
 BF16_DENSE_PEAK_TF = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 L2_GATHER_GBPS = 17800.0     # MI355X_MICROARCH.md "Indexed rows": L2-served gather, 16.8-18.8 TB/s
@@ -166,6 +167,27 @@ def time_events(fn, iters, stream, warm_ms=30.0):
     return start.elapsed_time(end) / iters  # ms
 
 
+def time_graph(fn, iters, stream, reps=3):
+    """Per-launch device time of fn with the host out of the loop: `iters` calls captured in one
+    HIP graph, replayed `reps` times between HIP events (for launches shorter than their Python
+    call, which time_events would measure instead).  fn must not allocate per call."""
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=stream):
+        for _ in range(iters):
+            fn()
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    g.replay()
+    torch.cuda.synchronize()
+    start.record(stream)
+    for _ in range(reps):
+        g.replay()
+    end.record(stream)
+    torch.cuda.synchronize()
+    return start.elapsed_time(end) / (iters * reps)
+
+
 def kernel_rooflines(model, left, right, batch, iters):
     """Per-kernel average duration (HIP events on the launch stream) and roofline fractions."""
     from aanet_amd import ops
@@ -280,6 +302,11 @@ def kernel_rooflines(model, left, right, batch, iters):
     res["concat_volume_c5"] = dict(bound="hbm", ms=ms, algo=cc_bytes, unit="GB/s",
                                    achieved=cc_bytes / ms / 1e6, peak=HBM_PEAK_GBS,
                                    pairs=Bc, bytes_per_pair=cc_bytes / Bc, in_step=False)
+    # 92% of its bytes are stores: priced also against the store ceiling measured on this part
+    # (tools/write_ceiling.hip, profiles/r06_write_ceiling.txt: hipMemsetAsync 6.49 TB/s, the best
+    # kernel store pattern 6.19 TB/s), which is what a write-bound kernel can reach
+    res["concat_volume_c5"]["store_ceiling_GBps"] = STORE_CEILING_GBS
+    res["concat_volume_c5"]["frac_of_store_ceiling"] = cc_bytes / ms / 1e6 / STORE_CEILING_GBS
     del lc, rc
     for v in res.values():
         v["frac"] = v["achieved"] / v["peak"]
@@ -577,7 +604,8 @@ def main():
                          "peak_basis": peak_basis(dom),
                          **({"gather": dom["gather"]} if "gather" in dom else {})},
             "kernels": {k: {kk: v[kk] for kk in ("bound", "ms", "achieved", "unit", "frac", "gather",
-                                                 "pairs", "bytes_per_pair")
+                                                 "pairs", "bytes_per_pair", "store_ceiling_GBps",
+                                                 "frac_of_store_ceiling")
                             if kk in v}
                         for k, v in roof.items()},
             # EPE vs ref: mean / max |dd| of every rank's pair 0 against the CPU oracle
@@ -636,10 +664,13 @@ DCN_SHAPES = [("agg_s0", 64, 128, 416, 1), ("agg_s1", 32, 64, 208, 1), ("agg_s2"
 
 def dcn_sweep_main(args, device, rank):
     """C4 microbench: the modulated DCN op (ops.mdcn_forward = the reference's
-    modulated_deform_conv_cuda_forward: the LDS-window kernel for the aggregation shapes,
-    `fwd_generic_us` the generic engine of aanet_mdcn_fwd_f32; aanet_mdcn_bwd_f32 / _det_f32 =
+    modulated_deform_conv_cuda_forward: the LDS-window kernel for the aggregation's scale-0/1
+    shapes, the direct kernel (dcn_small.hip) for scale 2, `fwd_generic_us` the generic
+    implicit-GEMM engine; aanet_mdcn_bwd_f32 / _det_f32 =
     ..._backward) per shape,
     B=--batch, offsets N(0, 0.5^2) (fractional, some out of the image), mask U(0, 1).
+    Forward times are per-launch device times from HIP-graph replays (`fwd_eager_call_us`: the
+    eager per-call time, host launch overhead included); backward times are eager.
     Flops: forward 2*B*Ho*Wo*Co*C*9 (the MFMA contraction; bilinear lerps excluded); backward
     counts dgrad + wgrad contractions (2x the forward).  One JSON line per shape on rank 0, then
     the num_scales 1 / 3 aggregation totals."""
@@ -670,12 +701,21 @@ def dcn_sweep_main(args, device, rank):
         bwd_glob = lambda: ops.mdcn_backward(x, off, mask, w, go, False, stride, pad, dil, 1, dg,  # noqa: E731
                                              deterministic=False, algo="global")
         flops = 2.0 * B * Ho * Wo * C * C * k * k
-        ms_f, ms_fg, ms_b, ms_d, ms_g = (time_events(f, iters, stream)
-                                         for f in (fwd, fwd_gen, bwd, bwd_det, bwd_glob))
+        ms_b, ms_d, ms_g = (time_events(f, iters, stream) for f in (bwd, bwd_det, bwd_glob))
+        # forwards write into `out`: timed as graph replays (device time; the 16-channel scale's
+        # launch is shorter than its Python call), with the eager per-call time beside them
+        ms_fh = time_events(fwd, iters, stream)
+        side = torch.cuda.Stream(device)
+        side.wait_stream(stream)
+        with torch.cuda.stream(side):
+            ms_f, ms_fg = (time_graph(f, iters, side) for f in (fwd, fwd_gen))
+        stream.wait_stream(side)
         line = {"bench": "dcn_sweep (C4)", "shape": name, "input": [B, C, H, W], "stride": stride,
                 "deformable_groups": dg, "dilation": dil, "fwd_us": ms_f * 1e3,
                 "fwd_window": ops.window_fwd_ok(C, C, k, k, stride, pad, dil, 1, dg, W),
-                "fwd_generic_us": ms_fg * 1e3, "bwd_us": ms_b * 1e3,
+                "fwd_direct": ops.direct_fwd_ok(C, C, k, k, stride, pad, dil, 1, dg),
+                "fwd_generic_us": ms_fg * 1e3, "fwd_eager_call_us": ms_fh * 1e3,
+                "bwd_us": ms_b * 1e3,
                 "bwd_det_us": ms_d * 1e3, "bwd_global_atomic_us": ms_g * 1e3,
                 "fwd_tflops": flops / ms_f / 1e9, "bwd_tflops": 2 * flops / ms_b / 1e9,
                 "fwd_frac_f32_mfma": flops / ms_f / 1e9 / FP32_MFMA_PEAK_TF,
