@@ -1,0 +1,71 @@
+// deconv.hip -- output assembly of the 2-D transposed convs of the hourglasses (GANetFeature and
+// HourglassRefinement: Conv2x(deconv=True) = ConvTranspose2d(k = 4, stride 2, padding 1) + BN +
+// ReLU, then torch.cat with the skip; nets/feature.py:342-376, nets/refinement.py:109-197).
+//
+// A stride-2 transposed conv is four ordinary convs, one per output phase (a, b) = (Y % 2, X % 2):
+// out[c][2y+a][2x+b] = sum_ci sum_{ty,tx in 0,1} in[ci][y+a-1+ty][x+b-1+tx] W[ci][c][3-a-2ty][3-b-2tx].
+// The host (ops.deconv2x) runs them as ONE 2x2, pad-1 conv on the implicit-GEMM engine with 4*co
+// outputs (phase channel 4c + 2a + b; BN folded, ReLU in its epilogue), whose output element
+// [4c+2a+b][y+a][x+b] is out[c][2y+a][2x+b].  This kernel scatters those phase planes into the
+// 2x resolution output and appends the skip tensor's channels after them (the concat), so the
+// transposed conv costs one engine launch and one memory-bound pass -- instead of MIOpen's
+// transposed-conv solvers (backward-data GEMM + col2im + layout transposes) and a torch.cat.
+#include "common.h"
+
+namespace {
+
+// one thread per 4 output columns (a quad) of one output row of one channel
+__global__ __launch_bounds__(256) void deconv2x_assemble_kernel(const float *__restrict__ ph,
+                                                                const float *__restrict__ rem,
+                                                                float *__restrict__ out, int n,
+                                                                int co, int cr, int h, int w) {
+  const int W2 = 2 * w, H2 = 2 * h, qpr = (W2 + 3) / 4, ct = co + cr;
+  const long total = (long)n * ct * H2 * qpr;
+  const long ph_plane = (long)(h + 1) * (w + 1), o_plane = (long)H2 * W2;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int q = (int)(e % qpr);
+    long r = e / qpr;
+    const int Y = (int)(r % H2);
+    r /= H2;
+    const int c = (int)(r % ct), img = (int)(r / ct);
+    const int X0 = 4 * q;
+    float *dst = out + ((long)img * ct + c) * o_plane + (long)Y * W2;
+    float v[4];
+    if (c < co) {
+      // columns X0 + u: phase b = u & 1, input column x = (X0 + u) >> 1, conv column x + b
+      const int a = Y & 1, y = Y >> 1;
+      const float *p0 = ph + ((long)img * 4 * co + 4 * c + 2 * a) * ph_plane + (long)(y + a) * (w + 1);
+      const float *p1 = p0 + ph_plane;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int X = X0 + u, x = X >> 1;
+        v[u] = X < W2 ? ((u & 1) ? p1[x + 1] : p0[x]) : 0.f;
+      }
+    } else {
+      const float *src = rem + ((long)img * cr + (c - co)) * o_plane + (long)Y * W2;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = X0 + u < W2 ? src[X0 + u] : 0.f;
+    }
+    if ((W2 & 3) == 0) {
+      *reinterpret_cast<f32x4 *>(dst + X0) = f32x4{v[0], v[1], v[2], v[3]};
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (X0 + u < W2) dst[X0 + u] = v[u];
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int aanet_deconv2x_assemble_f32(const float *ph, const float *rem, float *out, int n,
+                                           int co, int cr, int h, int w, aanet_stream_t stream) {
+  if (n < 0 || co < 0 || cr < 0 || h < 0 || w < 0) return AANET_EINVAL;
+  const long total = (long)n * (co + cr) * 2 * h * ((2 * w + 3) / 4);
+  if (total == 0) return AANET_OK;
+  if (!out || (co && !ph) || (cr && !rem)) return AANET_EINVAL;
+  const long blocks = host_div_up(total, 256);
+  hipLaunchKernelGGL(deconv2x_assemble_kernel, dim3((unsigned)(blocks > 65536 ? 65536 : blocks)),
+                     dim3(256), 0, as_hip(stream), ph, rem, out, n, co, cr, h, w);
+  return aanet_launch_status();
+}

@@ -470,17 +470,31 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   const int wc0 = __builtin_amdgcn_readfirstlane((wave / WP) * NCB);  // first co block of the wave
   const int wp0 = __builtin_amdgcn_readfirstlane((wave % WP) * NPB);  // first px block of the wave
   const long P = (long)a.Ho * a.Wo;
-  static_assert(!HALO || (MODE == 0 && PREC == 1 && HALO <= 2 && PTT == 128 && (LAYOUT & 1)),
+  static_assert(!HALO || (MODE == 0 && PREC == 1 && (HALO <= 2 || HALO == 4) && PTT == 128 && (LAYOUT & 1)),
                 "halo configuration");
+  // HALO 4: the phase-strided halo tile.  A 3x3 conv of dilation D (= pad, stride 1) is D x D
+  // independent dilation-1 convs, one per phase (pixels y % D = pa, x % D = pb): the tile is
+  // 8 x 16 outputs of one phase, its halo the (8+2) x (16+2) phase positions around them, so
+  // dilations 4 / 8 (nets/refinement.py:60-106) stage 1.4 positions per output instead of the
+  // (8+2D)(16+2D)/128 of a plain halo or the nine of im2col.  NHWC in and out only.
+  constexpr bool PH = HALO == 4;
+  static_assert(!PH || (LAYOUT == 3 && !TAIL && !POST), "phase-strided halo: NHWC in/out, no tail");
   constexpr int TRH = 8;  // output rows of a halo tile (16 columns)
-  const int htx = HALO ? (a.Wo + 15) / 16 : 1;
-  const int ntiles = HALO ? htx * ((a.Ho + TRH - 1) / TRH) : (int)((P + PTT - 1) / PTT);
+  const int pd = PH ? a.dil : 1;                       // phase stride
+  const int hWo = PH ? (a.Wo + pd - 1) / pd : a.Wo;    // (largest) phase image size
+  const int hHo = PH ? (a.Ho + pd - 1) / pd : a.Ho;
+  const int htx = HALO ? (hWo + 15) / 16 : 1;
+  const int hty = HALO ? (hHo + TRH - 1) / TRH : 1;
+  const int ntiles = HALO ? pd * pd * htx * hty : (int)((P + PTT - 1) / PTT);
   // XCD-aware remap of the pixel-tile index (bijective for any grid size)
   const int nwg = gridDim.x, b0 = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, xcd = b0 & 7;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b0 >> 3);
-  const int n = bid / ntiles, tile = bid % ntiles;
-  const int hy0 = HALO ? (tile / htx) * TRH : 0, hx0 = HALO ? (tile % htx) * 16 : 0;  // HALO tile origin
+  const int n = bid / ntiles, tile0 = bid % ntiles;
+  const int ph = PH ? tile0 / (htx * hty) : 0, tile = PH ? tile0 - ph * (htx * hty) : tile0;
+  const int pa = PH ? ph / pd : 0, pb = PH ? ph - pa * pd : 0;  // the tile's phase
+  // HALO tile origin (phase coordinates for HALO 4: image row pa + pd * y)
+  const int hy0 = HALO ? (tile / htx) * TRH : 0, hx0 = HALO ? (tile % htx) * 16 : 0;
   const int Cg = a.C / a.groups, Cog = a.Co / a.groups, K = a.kh * a.kw, cpg = a.C / a.dg;
   const int ncot = (Cog + CO_T - 1) / CO_T;
   const int gc = blockIdx.y / ncot, cot = blockIdx.y % ncot;
@@ -893,7 +907,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   if constexpr (HALO) {
     // stride 1, dilation = padding = d (the round-3 stride-2 NCHW form, HALO 3, was removed in
     // round 4: faster alone, slower in the two-stream step)
-    constexpr int d = HALO;  // tap spacing in the halo
+    constexpr int d = PH ? 1 : HALO;  // tap spacing in the halo
     constexpr int hw = 16 + 2 * d, npos = (8 + 2 * d) * hw;
     const int hy = hy0 - d, hx = hx0 - d;
     constexpr int HIT = (npos * 8 + FNT - 1) / FNT;  // halo quads per thread (NHWC)
@@ -909,8 +923,9 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
       for (int i = 0; i < HIT; ++i) {
         const int e = t + FNT * i, pos = e >> 3;
         const int yy = hy + pos / hw, xx = hx + pos % hw;
-        const bool ok = pos < npos && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
-        const int off = ok ? ((yy * a.W + xx) * a.C + 4 * (e & 7)) * 4 : img_bytes;  // zero padding: OOB
+        const int iy = PH ? pa + pd * yy : yy, ix = PH ? pb + pd * xx : xx;  // image position
+        const bool ok = pos < npos && yy >= 0 && iy < a.H && xx >= 0 && ix < a.W;
+        const int off = ok ? ((iy * a.W + ix) * a.C + 4 * (e & 7)) * 4 : img_bytes;  // zero padding: OOB
         hv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, soff, 0));
       }
     };
@@ -1144,7 +1159,8 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   // output pixel of tile-local index px (flattened, -1 outside the image); quad q = px 4q..4q+3
   auto pix = [&](int px) -> long {
     if constexpr (HALO) {
-      const int y = hy0 + (px >> 4), x = hx0 + (px & 15);
+      int y = hy0 + (px >> 4), x = hx0 + (px & 15);
+      if constexpr (PH) y = pa + pd * y, x = pb + pd * x;
       return (y < a.Ho && x < a.Wo) ? (long)y * a.Wo + x : -1;
     } else {
       return p0 + px < P ? p0 + px : -1;
@@ -2532,6 +2548,11 @@ void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
   const dim3 blk(FNT);
   if constexpr (FULL && CFG == 0 && CO_T >= 32) {  // split-bf16 contraction (PREC 1)
     if constexpr (MODE == 0 && PTT == 128) {
+      if (a.split && packed && a.halo == 4) {  // phase-strided halo tile (dilation > 2)
+        if (a.layout == 3)
+          hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, 128, 1, 0, 1, 1, 3, CFG, 1, 4>), grid, blk, 0, st, a);
+        return;
+      }
       if (a.split && packed && a.halo == 1) {  // 3x3 stride-1 halo-tile form (NHWC input), HALO = dil
         if (a.dil == 1) {
           if (a.tail_w && a.post && CO_T == 64)
@@ -2646,13 +2667,21 @@ int launch_fwd(const MdcnArgs &a_in, int packed, hipStream_t st) {
   if (full_cfg(a, MODE, co_t) == 1) ptt = 128;  // 16-channel chunks are staged 4 per thread
   a.halo = MODE == 0 && a.split && packed && (a.layout & 1) && a.kh == 3 && a.kw == 3 &&
            a.stride == 1 && a.pad == a.dil && a.dil <= 2 && co_t >= 32 && full_cfg(a, 0, co_t) == 0;
+  // dilations > 2 (the refinement's dilated blocks): the phase-strided halo tile (HALO 4),
+  // NHWC in and out, no tail
+  if (!a.halo && MODE == 0 && a.split && packed && a.layout == 3 && a.kh == 3 && a.kw == 3 &&
+      a.stride == 1 && a.pad == a.dil && a.dil > 2 && co_t >= 32 && !a.tail_w && !a.csa_out &&
+      !a.post && full_cfg(a, 0, co_t) == 0)
+    a.halo = 4;
   if (a.halo) ptt = 128;
   // post stage (aanet_post_stage_t): the HALO 1 tail with the CSA epilogue, 64 -> 64 channels,
   // NHWC output only; anything else is left to the caller before any launch
   if (a.post && (MODE != 0 || !a.csa_out || !a.halo || a.dil != 1 || co_t != 64 || a.Co2 != 64 ||
                  a.post->disp || !a.post->out_nhwc || a.post->skip_outputs || !a.split || !packed))
     return AANET_EUNSUPPORTED;
-  dim3 grid((unsigned)(a.halo ? (long)a.N * host_div_up(a.Wo, 16) * host_div_up(a.Ho, 8)
+  const int hd = a.halo == 4 ? a.dil : 1;  // phase stride (HALO 4)
+  dim3 grid((unsigned)(a.halo ? (long)a.N * hd * hd * host_div_up(host_div_up(a.Wo, hd), 16) *
+                                    host_div_up(host_div_up(a.Ho, hd), 8)
                               : a.N * host_div_up(P, ptt)),
             (unsigned)(a.groups * ncot));
   if (ptt == 128) {

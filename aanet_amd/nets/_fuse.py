@@ -86,6 +86,47 @@ def folded(conv, bn):
     return w, b, wp
 
 
+def deconv2x_ok(conv):
+    """A transposed conv the phase form takes (ops.deconv2x): 2-D, 4x4, stride 2, padding 1, no
+    output padding / groups / dilation (the hourglasses' Conv2x deconvs)."""
+    return isinstance(conv, nn.ConvTranspose2d) and conv.kernel_size == (4, 4) and \
+        conv.stride == (2, 2) and conv.padding == (1, 1) and conv.output_padding == (0, 0) and \
+        conv.groups == 1 and conv.dilation == (1, 1) and conv.padding_mode == "zeros"
+
+
+def folded_deconv(conv, bn):
+    """(phase weight [4co][ci][2][2], bias [4co], packed weight) of a deconv2x_ok transposed conv
+    followed by eval BN (bn may be None), cached on the conv like folded()."""
+    tensors = (conv.weight, conv.bias) + (_bn_tensors(bn) if bn is not None else ())
+    key = _key(*tensors)
+    cache = getattr(conv, "_aanet_fold", None)
+    if cache is not None and cache[0] == key:
+        return cache[1], cache[2], cache[3]
+    with torch.no_grad():
+        co = conv.out_channels
+        if bn is None:
+            scale, shift = None, conv.bias if conv.bias is not None else conv.weight.new_zeros(co)
+        else:
+            scale, shift = bn_scale_shift(bn)
+            if conv.bias is not None:
+                shift = conv.bias * scale + shift
+        w = ops.deconv2x_phase_weight(conv.weight, scale)
+        b = shift.repeat_interleave(4).contiguous()
+    wp = ops.pack_weight_split(w)
+    if wp is None:
+        wp = ops.pack_weight(w)
+    conv._aanet_fold = (key, w, b, wp)
+    _lib.note_cache_fill()
+    return w, b, wp
+
+
+def deconv_bn_act(x, conv, bn=None, act=None, rem=None):
+    """act(BN(conv_transpose(x))) [+ the concat with rem] as the engine phase conv + one assembly
+    pass (ops.deconv2x)."""
+    w, b, wp = folded_deconv(conv, bn)
+    return ops.deconv2x(x, w, b, act, packed_weight=wp, rem=rem)
+
+
 def dense_grouped_ok(conv, x):
     """A 2-group conv whose groups are narrower than the split-bf16 engine's 32-channel K chunk
     (the scale-1 offset_conv: 32 -> 54, two 16-channel groups) but whose full input is a multiple

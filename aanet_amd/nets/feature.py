@@ -11,7 +11,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ._fuse import FusedSequential, conv_bn_act, engine_conv, use_fused
+from ._fuse import FusedSequential, conv_bn_act, deconv2x_ok, deconv_bn_act, engine_conv, use_fused
 from .deform import DeformConv2d
 from .._precision import fp32_convs
 
@@ -249,11 +249,18 @@ class BasicConv(nn.Module):
             self.bn = nn.BatchNorm2d(out_channels)
         self.conv = conv_t(in_channels, out_channels, bias=False, **kwargs)
 
+    def fused_deconv(self, x):
+        """Eval fast path of a 2-D 4x4 stride-2 transposed conv (ops.deconv2x), or None."""
+        return use_fused(self, x) and deconv2x_ok(self.conv)
+
     @fp32_convs
     def forward(self, x):
         if use_fused(self, x) and engine_conv(self.conv):
             return conv_bn_act(x, self.conv, self.bn if self.use_bn else None,
                                "relu" if self.relu else None)
+        if self.fused_deconv(x):
+            return deconv_bn_act(x, self.conv, self.bn if self.use_bn else None,
+                                 "relu" if self.relu else None)
         x = self.conv(x)
         if self.use_bn:
             x = self.bn(x)
@@ -282,6 +289,12 @@ class Conv2x(nn.Module):
 
     @fp32_convs
     def forward(self, x, rem):
+        c1 = self.conv1
+        if self.concat and c1.fused_deconv(x) and rem.shape[2:] == (2 * x.shape[2], 2 * x.shape[3]):
+            # transposed conv + BN + ReLU and the concat: one engine launch + one assembly pass
+            x = deconv_bn_act(x, c1.conv, c1.bn if c1.use_bn else None,
+                              "relu" if c1.relu else None, rem=rem)
+            return self.conv2(x)
         x = self.conv1(x)
         assert x.size() == rem.size()
         x = torch.cat((x, rem), 1) if self.concat else x + rem

@@ -506,6 +506,47 @@ def mdcn_pw(x, offset_mask, weight, packed_weight, bias, post_scale, post_shift,
     return (out, csa_out) if post is None else (out, csa_out, pres if ran else None)
 
 
+_DECONV_TAP = ((3, 1), (2, 0))  # [phase][2x2 tap] -> 4x4 transposed-conv tap (deconv.hip)
+
+
+def deconv2x_phase_weight(weight, scale=None):
+    """ConvTranspose2d(k=4, s=2, p=1) weight [ci][co][4][4] (times a per-output-channel scale,
+    e.g. a folded BN) -> the [4co][ci][2][2] weight of the equivalent 2x2 pad-1 conv whose output
+    channel 4c + 2a + b is the phase (a, b) of output channel c (deconv.hip)."""
+    ci, co = weight.shape[:2]
+    if tuple(weight.shape[2:]) != (4, 4):
+        raise ValueError("deconv2x: 4x4 kernels only")
+    w = weight if scale is None else weight * scale.view(1, -1, 1, 1)
+    idx = torch.tensor(_DECONV_TAP, device=weight.device)
+    g = w.permute(1, 0, 2, 3)[:, :, idx]          # [co][ci][a][ty][kx]
+    g = g[:, :, :, :, idx]                         # [co][ci][a][ty][b][tx]
+    return g.permute(0, 2, 4, 1, 3, 5).reshape(4 * co, ci, 2, 2).contiguous()
+
+
+def deconv2x(x, phase_weight, bias=None, act=None, packed_weight=None, rem=None):
+    """act(ConvTranspose2d(k=4, stride 2, padding 1)(x) + bias) [, rem concatenated after its
+    channels] -> [N, co (+ cr), 2H, 2W]: the 2x2 pad-1 phase conv on the HIP engine (weights from
+    deconv2x_phase_weight, bias repeated per phase), then aanet_deconv2x_assemble_f32 (phase
+    scatter + the concat).  nets/feature.py:342-376 (Conv2x with deconv=True)."""
+    require_gpu(x, phase_weight, bias, packed_weight, rem,
+                names=("input", "weight", "bias", "packed", "rem"))
+    N, C, H, W = x.shape
+    co = phase_weight.shape[0] // 4
+    ph = conv2d_fused(x.contiguous(), phase_weight, bias, 1, 1, 1, 1, act,
+                      packed_weight=packed_weight)
+    cr = 0
+    if rem is not None:
+        rem = rem.contiguous()
+        if tuple(rem.shape[0:1]) + tuple(rem.shape[2:]) != (N, 2 * H, 2 * W):
+            raise ValueError(f"deconv2x: rem {tuple(rem.shape)} does not match the output "
+                             f"{(N, co, 2 * H, 2 * W)}")
+        cr = rem.shape[1]
+    out = torch.empty((N, co + cr, 2 * H, 2 * W), device=x.device, dtype=x.dtype)
+    call("aanet_deconv2x_assemble_f32", ptr(ph), ptr(rem), ptr(out), N, co, cr, H, W,
+         stream_of(x))
+    return out
+
+
 def pack_conv3x3s2(weight):
     """Pre-split A fragments of a [co][c][3][3] weight for conv3x3_s2 (aanet_conv3x3s2_pack_f32;
     co % 16 == 0, co <= 96, c % 32 == 0), or None when the shape is outside the kernel."""

@@ -322,6 +322,15 @@ int aanet_conv3x3s2_terms_f32(const float *x, const void *wsplit, const float *b
                               float *out_b, int act_b, const aanet_s2_terms_t *terms,
                               aanet_stream_t stream);
 
+/* ConvTranspose2d(k = 4, stride 2, padding 1) assembly (nets/feature.py:342-376 Conv2x(deconv=True),
+ * used by GANetFeature and HourglassRefinement, refinement.py:109-197): the transposed conv runs as
+ * one 2x2, pad-1 conv with 4*co phase outputs (ph [n][4co][h+1][w+1], channel 4c + 2a + b; the
+ * Python layer's ops.deconv2x); this writes out [n][co + cr][2h][2w] with
+ * out[c][2y+a][2x+b] = ph[4c+2a+b][y+a][x+b] for c < co and the skip tensor rem [n][cr][2h][2w]
+ * as channels co .. co+cr-1 (the torch.cat of Conv2x.forward; cr = 0: no skip, rem may be NULL). */
+int aanet_deconv2x_assemble_f32(const float *ph, const float *rem, float *out, int n, int co, int cr,
+                                int h, int w, aanet_stream_t stream);
+
 /* F.interpolate(x, size=(out_h, out_w), mode='bilinear', align_corners=False) on [planes, in_h,
  * in_w] -> y [planes, out_h, out_w] (aggregation.py:395-396 in training; the loss's upsampling,
  * model.py:115-117): one thread per output element, the reference kernel's stencil and order. */

@@ -272,3 +272,22 @@ def test_pinned_convs_match_torch_autograd(is_3d):
     assert torch.allclose(x.grad, x2.grad, atol=1e-5) and torch.allclose(rem.grad, rem2.grad, atol=1e-5)
     for (n, p), (_, p2) in zip(m.named_parameters(), ref.named_parameters()):
         assert torch.allclose(p.grad, p2.grad, atol=1e-4, rtol=1e-5), n
+
+
+@pytest.mark.parametrize("ci,co,h,w", [(8, 4, 5, 7), (3, 6, 1, 1), (16, 8, 4, 9)])
+def test_deconv2x_phase_weight_is_the_transposed_conv(ci, co, h, w):
+    """ops.deconv2x's decomposition on the CPU: the 2x2 pad-1 conv with the phase weight
+    (deconv2x_phase_weight), its output [4c+2a+b][y+a][x+b] scattered to [c][2y+a][2x+b] (what
+    aanet_deconv2x_assemble_f32 does), equals ConvTranspose2d(k=4, s=2, p=1) in fp64."""
+    g = torch.Generator().manual_seed(ci * 100 + co)
+    x = torch.randn(2, ci, h, w, generator=g, dtype=torch.float64)
+    wt = torch.randn(ci, co, 4, 4, generator=g, dtype=torch.float64)
+    scale = torch.rand(co, generator=g, dtype=torch.float64) + 0.5
+    ref = torch.nn.functional.conv_transpose2d(x, wt * scale.view(1, -1, 1, 1), stride=2, padding=1)
+    ph = torch.nn.functional.conv2d(x, ops.deconv2x_phase_weight(wt, scale), padding=1)
+    assert ph.shape == (2, 4 * co, h + 1, w + 1)
+    out = torch.empty_like(ref)
+    for a in (0, 1):
+        for b in (0, 1):
+            out[:, :, a::2, b::2] = ph[:, 2 * a + b::4, a:a + h, b:b + w]
+    assert torch.allclose(out, ref, rtol=0, atol=1e-12)

@@ -367,3 +367,39 @@ def test_tail_csa_epilogue_rejects_non_integer_ratio():
     with pytest.raises(Exception):
         ops.conv2d_pw(x, w2, ops.pack_weight(w2), None, None, None, "relu", ops.pack_weight(w3),
                       None, None, "relu", 1, 1, 1, csa_up=[torch.randn(N, C, 3, 9, device=DEV)])
+
+
+# ------------------------------------------- dilation > 2: phase-strided halo tiles (HALO 4)
+PHASE_CASES = [
+    # N, C, H, W, Co, dil   (3x3, stride 1, pad = dil; the refinement's dilated BasicBlocks)
+    (2, 32, 40, 104, 32, 4),     # StereoDRNet dilation 4 (nets/refinement.py:60-106)
+    (1, 32, 48, 160, 32, 8),     # dilation 8
+    (1, 32, 19, 37, 32, 3),      # ragged phases: H, W not multiples of the dilation
+    (1, 64, 21, 70, 64, 4),      # 64 channels (two K chunks), 64-channel tile
+    (1, 32, 5, 9, 32, 8),        # image smaller than one dilation step in both directions
+]
+
+
+@pytest.mark.parametrize("case", PHASE_CASES)
+@pytest.mark.parametrize("residual", [False, True])
+def test_conv2d_dilated_phase_halo_vs_torch(case, residual):
+    """Split-bf16 3x3 convs of dilation > 2, NHWC in and out (the form the refinement's dilated
+    blocks run): the D x D phase-strided halo tiles against torch CPU in fp64, at fp32 accuracy."""
+    N, C, H, W, Co, d = case
+    gen = torch.Generator().manual_seed(31 + d + C)
+    x = torch.randn(N, C, H, W, generator=gen, dtype=torch.float64)
+    w = torch.randn(Co, C, 3, 3, generator=gen, dtype=torch.float64) / (C * 9) ** 0.5
+    b = torch.randn(Co, generator=gen, dtype=torch.float64)
+    res = torch.randn(N, Co, H, W, generator=gen, dtype=torch.float64) if residual else None
+    ref = F.conv2d(x, w, b, 1, d, d) + (res if residual else 0)
+    ref = F.relu(ref)
+    xd = x.float().to(DEV).contiguous(memory_format=torch.channels_last)
+    wd = w.float().to(DEV)
+    wp = ops.pack_weight_split(wd)
+    assert wp is not None
+    rd = res.float().to(DEV).contiguous(memory_format=torch.channels_last) if residual else None
+    got = ops.conv2d_fused(xd, wd, b.float().to(DEV), 1, d, d, 1, "relu", rd, packed_weight=wp,
+                           out_nhwc=True)
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    err = (got.cpu().double() - ref).abs().max().item()
+    assert err <= 2e-5 * (1 + ref.abs().max().item()), err
