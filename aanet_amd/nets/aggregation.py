@@ -502,6 +502,8 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
         stream (_run_chains); the caller's list is then not mutated."""
         assert isinstance(cost_volume, list)
         fused = use_fused(self, cost_volume[0])
+        if self._pipeline_ok(cost_volume, fused):
+            return self._run_pipelined(cost_volume)
         if chains > 1 and fused and cost_volume[0].is_cuda and cost_volume[0].shape[0] >= 2:
             return self._run_chains(cost_volume, regress, min(chains, cost_volume[0].shape[0]))
         return self._run_one(cost_volume, regress, fused)
@@ -558,6 +560,106 @@ class AdaptiveAggregation(FoldCacheMixin, nn.Module):
         if results[0][1] is not None:
             return None, torch.cat([r[1] for r in results])
         return [torch.cat([r[0][i] for r in results]) for i in range(len(results[0][0]))], None
+
+    def _pipeline_ok(self, cost_volume, fused):
+        """Whether the cross-module pipelined schedule (option `pipeline`, _run_pipelined) takes
+        this aggregation: eval fast path on the GPU, three scales, one block per branch, and the
+        stride-2 sums (heads kernel + branch-2 conv) for every module with three outputs."""
+        if not (fused and cost_volume[0].is_cuda and self.num_scales == 3 and
+                get_option(self, "pipeline") and len(cost_volume) == 3 and
+                csa_epilogue_ok(cost_volume[0], cost_volume[1:])):
+            return False
+        for f in self.fusions:
+            if f.num_blocks != 1 or (len(f.fuse_layers) == 3 and not f._s2_sums_ok(cost_volume)):
+                return False
+            if len(f.fuse_layers) not in (1, 3):
+                return False
+        return True
+
+    def _run_pipelined(self, cost_volume):
+        """Cross-module pipelined eval schedule (option `pipeline`).  Module m's scale-0 block
+        T(m) needs only the previous module's scale-0 CSA sum, so it runs on side stream F while
+        the current stream runs the previous module's stride-2 heads H(m-1) and this module's
+        coarse blocks (scale 1 here, scale 2 on side stream B); the scale-0 CSA sum S(m) (one
+        aanet_csa_sum_f32) follows on F once both are done:
+            F:    S(m-1) -> T(m) ---------------------(wait chains(m))-> S(m) -> T(m+1) ...
+            main: (wait T(m-1)) H(m-1) -> scale-1 block + up terms (m) -> (wait T(m)) H(m) ...
+            B:    (wait H(m-1)) scale-2 block + up terms (m)
+        so the heads and the small, serially dependent coarse kernels overlap the large scale-0
+        tails instead of running between them.  Every cross-stream edge goes through the current
+        stream (side streams wait only for it; it waits for them), which HIP graph capture needs.
+        Same arithmetic per term as the default schedule except that branch 0's sum is the
+        separate aanet_csa_sum_f32 kernel instead of the tail kernel's CSA epilogue, and conv1
+        of each scale-0 block is its own launch.  (A fused sum + conv1 kernel measured 192 us
+        alone against 45 + 55 us for the two.)"""
+        dev = cost_volume[0].device
+        main = torch.cuda.current_stream(dev)
+        F, B = side_streams(dev, 2)
+        ready = _record(main)
+        F.wait_event(ready)
+        B.wait_event(ready)
+        keep = list(cost_volume)
+        x0, x1, x2 = cost_volume
+        y0 = None          # the scale-0 block's conv1 output, from the previous S
+        nf = self.num_fusions
+
+        def block0(fu):
+            with torch.cuda.stream(F):
+                out = fu.branches[0][0].forward_csa(x0, None, conv1_out=y0)[0] if y0 is not None \
+                    else fu.branches[0](x0)
+            return out, _record(F)
+
+        out0, ev_t = block0(self.fusions[0])       # T(0)
+        for m, fu in enumerate(self.fusions):
+            nout = len(fu.fuse_layers)
+            with torch.cuda.stream(B):      # scale 2: block + its up terms
+                y2 = fu.branches[2](x2)
+                t02 = fu._exchange_up([None, None, y2], 0, 2)
+                t12 = fu._exchange_up([None, None, y2], 1, 2) if nout > 1 else None
+            ev_b = _record(B)
+            y1 = fu.branches[1](x1)         # scale 1 on the current stream
+            t01 = fu._exchange_up([None, y1], 0, 1)
+            main.wait_event(ev_b)
+            main.wait_event(ev_t)
+            keep.extend(t for t in (out0, y1, y2, t01, t02, t12) if t is not None)
+            # S(m): branch 0's sum, then the next block's conv1 (both alone on the GPU)
+            x0 = ops.csa_sum([out0, t01.contiguous(), t02.contiguous()], act="leaky")
+            keep.append(x0)
+            nxt = self._pipeline_conv(m + 1) if m + 1 < nf else None
+            y0 = conv_bn_act(x0, nxt.conv1, nxt.bn1, "relu", out_nhwc=True) if nxt is not None \
+                else None
+            if y0 is not None:
+                keep.append(y0)
+            h_in = out0
+            if m + 1 < nf:
+                # T(m + 1) is captured BEFORE H(m): the HIP graph executor launches nodes in
+                # capture order, and T(m + 1) captured after H(m) and the coarse blocks ran after
+                # them (no overlap)
+                F.wait_event(_record(main))
+                out0, ev_t = block0(self.fusions[m + 1])
+            if nout == 3:                   # H(m): branches 1 and 2, beside T(m + 1)
+                x1, hb = fu._heads_sum1(h_in, y1, t12)
+                x2 = fu._branch2_sum(hb, y1, y2)
+                keep.extend((x1, hb, x2))
+                B.wait_event(_record(main))
+            else:
+                x1 = x2 = None
+        out = [conv_bn_act(x0, self.final_conv[0])]
+        if len(self.final_conv) > 1:
+            out += [conv_bn_act(t, c) for t, c in zip((x1, x2), self.final_conv[1:])]
+        main.wait_stream(F)
+        main.wait_stream(B)
+        del keep
+        return out, None
+
+    def _pipeline_conv(self, i):
+        """Fusion i's scale-0 block when its conv1 can run ahead of the block (the pipelined
+        schedule computes it right after the previous module's branch-0 sum, on the current
+        stream, channels-last as the tail kernels read it), or None."""
+        blk = self.fusions[i].branches[0][0]
+        if self.fusions[i].num_blocks != 1 or blk.conv1.weight.shape[0] % 32:
+            return None
+        return blk
 
     def _run_one(self, cost_volume, regress, fused, concurrent=True):
         gen = self._run_steps(cost_volume, regress, fused, concurrent)

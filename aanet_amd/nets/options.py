@@ -29,6 +29,14 @@ summation order; tests/test_gpu_production.py, test_gpu_post.py, test_gpu_dense_
                      Bit-identical results.  Measured round 6 (HIP graph): k = 2 / 3 / 4 3.34 /
                      3.96 / 3.79 ms against 3.22 (profiles/r06_chains_timeline.txt).
                                                                       (AdaptiveAggregation)
+  pipeline           True: the cross-module pipelined schedule (AdaptiveAggregation.
+                     _run_pipelined): each module's scale-0 block on a side stream beside the
+                     previous module's stride-2 heads and this module's coarse blocks, branch 0's
+                     sum + the next conv1 as their own kernels.  Within fp32 summation order of
+                     the default.  Measured round 6 (HIP graph): 3.30 vs 3.15 ms -- the scale-0
+                     tail beside the heads and coarse blocks slows from 220 to 305 us, i.e. the
+                     step is throughput-bound, and the separate sum + conv1 cost 118 us a module
+                     (profiles/r06_pipeline_timeline.txt).                (AdaptiveAggregation)
   dense_grouped      True: 2-group convs with 16-channel groups (the scale-1 offset conv) run as
                      one block-diagonal ungrouped conv on the split-bf16 engine; False: the
                      grouped exact-f32 engine.                        (every nn.Conv2d)
@@ -36,7 +44,7 @@ summation order; tests/test_gpu_production.py, test_gpu_post.py, test_gpu_dense_
 import torch.nn as nn
 
 DEFAULTS = {"concurrent_scales": True, "post_fusion": "all", "s2_sums": True,
-            "prep_stream": False, "batch_chains": 1, "dense_grouped": True}
+            "prep_stream": False, "batch_chains": 1, "dense_grouped": True, "pipeline": False}
 _POST = ("all", "final", "none")
 
 
@@ -62,7 +70,7 @@ def set_options(module, **options):
     from .aggregation import AdaptiveAggregation, AdaptiveAggregationModule
     targets = {"concurrent_scales": AdaptiveAggregation, "post_fusion": AdaptiveAggregation,
                "s2_sums": AdaptiveAggregationModule, "prep_stream": AdaptiveAggregationModule,
-               "batch_chains": AdaptiveAggregation,
+               "batch_chains": AdaptiveAggregation, "pipeline": AdaptiveAggregation,
                "dense_grouped": nn.Conv2d}
     for m in module.modules():
         for name, value in options.items():

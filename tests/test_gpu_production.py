@@ -269,6 +269,27 @@ def _prep_runs(m, left, right, ref):
             assert all(torch.equal(a, b) for a, b in zip(ref, static))
 
 
+def test_pipeline_option_matches_default_eager_and_graph():
+    """The cross-module pipelined schedule (set_options(pipeline=True): each scale-0 block on a
+    side stream beside the previous module's heads and the coarse blocks, branch 0's sum as its
+    own kernel) computes the same terms: within fp32 summation order of the default schedule and
+    the reference fixture, bit-reproducible run to run, and the HIP-graph replay equal to the
+    eager result bit for bit."""
+    g, sd, m, left, right = _model("hotpath_d64")
+    with torch.no_grad():
+        ref = m(left, right)[0].clone()
+        m.set_options(pipeline=True)
+        try:
+            assert m.aggregation._pipeline_ok(
+                m.cost_volume_construction(left, right), True)
+            got = [t.clone() for t in m(left, right)]
+            assert np.abs(got[0].cpu().numpy() - g["disp0"]).max() <= DISP_TOL
+            assert (got[0] - ref).abs().max().item() <= DISP_TOL
+            _prep_runs(m, left, right, got)
+        finally:
+            m.set_options(pipeline=False)
+
+
 @pytest.mark.parametrize("chains", [2, 3])
 def test_batch_chains_bit_identical_eager_and_graph(chains):
     """The batch-pipelined schedule (set_options(batch_chains=k): chunk c of the batch aggregated

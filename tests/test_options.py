@@ -14,11 +14,13 @@ def test_defaults_and_propagation():
     agg = m.aggregation
     for k, v in DEFAULTS.items():
         target = {"concurrent_scales": agg, "post_fusion": agg, "s2_sums": agg.fusions[0],
-                  "batch_chains": agg, "prep_stream": agg.fusions[4],
+                  "batch_chains": agg, "prep_stream": agg.fusions[4], "pipeline": agg,
                   "dense_grouped": agg.fusions[5].branches[1][0].conv2.offset_conv}[k]
         assert get_option(target, k) == v
     assert m.set_options(concurrent_scales=False, post_fusion="final", s2_sums=False,
-                         dense_grouped=False, batch_chains=2, prep_stream=False) is m
+                         dense_grouped=False, batch_chains=2, prep_stream=False,
+                         pipeline=True) is m
+    assert get_option(agg, "pipeline") is True
     assert all(get_option(f, "prep_stream") is False for f in agg.fusions)
     assert get_option(agg, "batch_chains") == 2
     assert get_option(agg, "concurrent_scales") is False
@@ -38,7 +40,7 @@ def test_full_model_and_module_function():
 
 @pytest.mark.parametrize("kw", [{"concurrent": True}, {"post_fusion": "0"},
                                 {"s2_sums": 1}, {"dense_grouped": "no"},
-                                {"batch_chains": 0}, {"batch_chains": True}])
+                                {"batch_chains": 0}, {"batch_chains": True}, {"pipeline": 1}])
 def test_rejects_unknown(kw):
     with pytest.raises(ValueError):
         nets.AANetHotPath(16).set_options(**kw)

@@ -4,7 +4,9 @@ launch per step).  For the median-length step of the last N it prints every kern
 duration, queue, workgroups, a short name; then the intervals in which exactly ONE kernel runs
 (the serial stretches of the schedule) grouped by kernel, and the idle gaps.
 
-Usage: python tools/step_timeline.py TRACE_kernel_trace.csv [N]"""
+Usage: python tools/step_timeline.py TRACE_kernel_trace.csv [N] [MARK]
+(MARK: the kernel-name substring that delimits steps; default the last tail's post-stage form,
+"corr_pyramid" for schedules without it)"""
 import collections
 import csv
 import re
@@ -13,10 +15,12 @@ import sys
 path = sys.argv[1]
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-mark = "dcn_tile_kernel<2, 32, true"
+mark = sys.argv[3] if len(sys.argv) > 3 else "dcn_tile_kernel<2, 32, true"
 idx = [i for i, r in enumerate(rows) if mark in r["Kernel_Name"]]
-idx = idx[-(N + 1):]
-steps = [(idx[k], idx[k + 1]) for k in range(len(idx) - 1)]
+# consecutive marks at least 1 ms apart delimit whole steps (not a kernel-only timing loop)
+gaps = [(idx[k], idx[k + 1]) for k in range(len(idx) - 1)
+        if int(rows[idx[k + 1]]["Start_Timestamp"]) - int(rows[idx[k]]["Start_Timestamp"]) > 1_000_000]
+steps = gaps[-N:]
 lens = [int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"]) for a, b in steps]
 order = sorted(range(len(steps)), key=lambda k: lens[k])
 a, b = steps[order[len(order) // 2]]
