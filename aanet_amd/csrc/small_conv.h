@@ -13,6 +13,14 @@ struct DirectArgs {
   int N, C, H, W, Co, Ho, Wo, pad;
 };
 
+// refine_stem_kernel (aanet_refine_stem_f32)
+struct StemArgs {
+  const float *warped, *left, *disp;   // [N][3][H][W], [N][3][H][W], [N][1][H][W]
+  const float *w1, *b1, *w2, *b2;      // [16][6][3][3], [16], [16][1][3][3], [16] (BN folded)
+  float *out;                          // [N][H][W][32]
+  int act, N, H, W;
+};
+
 // AANET_OK, AANET_EUNSUPPORTED (no instance for the shape: the caller runs the engine), or a
 // positive hipError_t.  y = act(post_scale*(conv + bias) + post_shift + residual).
 int conv_direct_launch(const DirectArgs &a, int k, int stride, int dil, hipStream_t st);

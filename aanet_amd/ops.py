@@ -547,6 +547,23 @@ def deconv2x(x, phase_weight, bias=None, act=None, packed_weight=None, rem=None)
     return out
 
 
+def refine_stem(warped, left, disp, w1, b1, w2, b2, act="leaky"):
+    """torch.cat((act(conv1(cat(warped - left, left))), act(conv2(disp))), 1) as one channels-last
+    [N, 32, H, W] tensor (aanet_refine_stem_f32; nets/refinement.py:92-99 with BN folded into
+    w1/b1, w2/b2)."""
+    require_gpu(warped, left, disp, w1, b1, w2, b2)
+    N, _, H, W = left.shape
+    if tuple(warped.shape) != (N, 3, H, W) or tuple(disp.shape) != (N, 1, H, W) or \
+            tuple(w1.shape) != (16, 6, 3, 3) or tuple(w2.shape) != (16, 1, 3, 3):
+        raise ValueError("refine_stem: unexpected shapes")
+    out = torch.empty((N, 32, H, W), device=left.device, dtype=left.dtype,
+                      memory_format=torch.channels_last)
+    call("aanet_refine_stem_f32", ptr(warped.contiguous()), ptr(left.contiguous()),
+         ptr(disp.contiguous()), ptr(w1.contiguous()), ptr(b1), ptr(w2.contiguous()), ptr(b2),
+         ACT[act], ptr(out), N, H, W, stream_of(left))
+    return out
+
+
 def pack_conv3x3s2(weight):
     """Pre-split A fragments of a [co][c][3][3] weight for conv3x3_s2 (aanet_conv3x3s2_pack_f32;
     co % 16 == 0, co <= 96, c % 32 == 0), or None when the shape is outside the kernel."""

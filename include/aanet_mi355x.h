@@ -331,6 +331,16 @@ int aanet_conv3x3s2_terms_f32(const float *x, const void *wsplit, const float *b
 int aanet_deconv2x_assemble_f32(const float *ph, const float *rem, float *out, int n, int co, int cr,
                                 int h, int w, aanet_stream_t stream);
 
+/* The warp-error stem of StereoDRNet / Hourglass refinement (nets/refinement.py:92-99, 148-155):
+ *   out_nhwc[n][y][x][0:16]  = act(conv3x3([warped - left, left]; w1) + b1)   (conv1, 6 -> 16)
+ *   out_nhwc[n][y][x][16:32] = act(conv3x3(disp; w2) + b2)                    (conv2, 1 -> 16)
+ * i.e. torch.cat((conv1(cat(warped - left, left)), conv2(disp)), 1) written channels-last.
+ * warped, left: [n][3][h][w]; disp: [n][1][h][w]; w1: [16][6][3][3], w2: [16][1][3][3] with the
+ * BatchNorms folded by the caller; pad 1, stride 1. */
+int aanet_refine_stem_f32(const float *warped, const float *left, const float *disp,
+                          const float *w1, const float *b1, const float *w2, const float *b2,
+                          int act, float *out_nhwc, int n, int h, int w, aanet_stream_t stream);
+
 /* F.interpolate(x, size=(out_h, out_w), mode='bilinear', align_corners=False) on [planes, in_h,
  * in_w] -> y [planes, out_h, out_w] (aggregation.py:395-396 in training; the loss's upsampling,
  * model.py:115-117): one thread per output element, the reference kernel's stencil and order. */

@@ -403,3 +403,36 @@ def test_conv2d_dilated_phase_halo_vs_torch(case, residual):
     assert got.is_contiguous(memory_format=torch.channels_last)
     err = (got.cpu().double() - ref).abs().max().item()
     assert err <= 2e-5 * (1 + ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("H,W", [(96, 312), (13, 37)])
+def test_refine_stem_matches_separate_convs(H, W):
+    """aanet_refine_stem_f32 (the StereoDRNet / Hourglass refinement stem, nets/refinement.py:
+    92-99: conv1 on [warped - left, left] and conv2 on the disparity, concatenated) against the
+    same convs run one by one on the HIP direct kernel + torch.cat: identical values (same
+    per-channel arithmetic), channels-last; and within fp32 of torch CPU."""
+    from aanet_amd.nets.refinement import StereoDRNetRefinement
+    torch.manual_seed(5)
+    m = StereoDRNetRefinement()
+    with torch.no_grad():
+        for seq in (m.conv1, m.conv2):
+            seq[1].running_mean.normal_(0, 0.1)
+            seq[1].running_var.uniform_(0.5, 1.5)
+    m = m.to(DEV).eval()
+    g = torch.Generator(device=DEV).manual_seed(6)
+    warped = torch.randn(2, 3, H, W, device=DEV, generator=g)
+    left = torch.randn(2, 3, H, W, device=DEV, generator=g)
+    disp = torch.rand(2, 1, H, W, device=DEV, generator=g) * 40
+    from aanet_amd.nets._fuse import folded
+    with torch.no_grad():
+        w1, b1, _ = folded(m.conv1[0], m.conv1[1])
+        w2, b2, _ = folded(m.conv2[0], m.conv2[1])
+        got = ops.refine_stem(warped, left, disp, w1, b1, w2, b2)
+        ref = torch.cat((m.conv1(torch.cat((warped - left, left), 1)), m.conv2(disp)), 1)
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(got, ref)
+    cpu = torch.cat((F.leaky_relu(F.conv2d(torch.cat((warped - left, left), 1).cpu().double(),
+                                           w1.cpu().double(), b1.cpu().double(), padding=1), 0.2),
+                     F.leaky_relu(F.conv2d(disp.cpu().double(), w2.cpu().double(),
+                                           b2.cpu().double(), padding=1), 0.2)), 1)
+    assert (got.cpu().double() - cpu).abs().max().item() <= 1e-5 * (1 + cpu.abs().max().item())
