@@ -2959,7 +2959,8 @@ extern "C" int aanet_conv2d_fused_f32(const float *x, const float *weight, const
     p.Co = co;
     p.in_nhwc = a.layout & 1;
     p.out_nhwc = a.layout >> 1;
-    return pw_conv_launch(p, as_hip(stream));
+    const int rc = pw_conv_launch(p, as_hip(stream));
+    if (rc != AANET_EUNSUPPORTED) return rc;
   }
   return launch_fwd<0>(a, weight_packed, as_hip(stream));
 }

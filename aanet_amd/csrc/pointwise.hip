@@ -34,12 +34,12 @@ __device__ __forceinline__ float pw_act(float v, int act) {
 template <int NB, int ONH>
 __device__ __forceinline__ void pw_store(const PwArgs &a, const f32x4 (&acc)[NB],
                                          const float (&eb)[NB][4], int t, int half, int kr, int n,
-                                         int p) {
+                                         int p, int co_base = 0) {
   const int T = a.N * a.P, P = a.P, Co = a.Co;
   if (t >= T) return;
 #pragma unroll
   for (int m = 0; m < NB; ++m) {
-    const int c0 = 16 * (NB * half + m) + 4 * kr;
+    const int c0 = co_base + 16 * (NB * half + m) + 4 * kr;
     if (c0 >= Co) continue;
     f32x4 y;
 #pragma unroll
@@ -58,13 +58,20 @@ __device__ __forceinline__ void pw_store(const PwArgs &a, const f32x4 (&acc)[NB]
       for (int r = 0; r < 4; ++r) y[r] = pw_act(y[r], a.act);
       *reinterpret_cast<f32x4 *>(a.out + o) = y;
     } else {
+      // every residual load before the first store: out may alias residual for the compiler, so
+      // a load issued after a store waited for it -- one memory round trip per channel (the
+      // bottleneck conv3 with its identity ran 3.4x the time of the plain conv)
+      float rv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (a.residual) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (c0 + r < Co) rv[r] = a.residual[((long)n * Co + c0 + r) * P + p];
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         if (c0 + r >= Co) break;
         const long o = ((long)n * Co + c0 + r) * P + p;
-        float s = y[r];
-        if (a.residual) s += a.residual[o];
-        a.out[o] = pw_act(s, a.act);
+        a.out[o] = pw_act(a.residual ? y[r] + rv[r] : y[r], a.act);
       }
     }
   }
@@ -282,7 +289,10 @@ __global__ __launch_bounds__(256) void pw_conv_nchw_s_kernel(PwArgs a) {
   const int b0 = blockIdx.x * per, b1 = min(nblk, b0 + per);
   if (b0 >= b1) return;  // workgroup-uniform
 
-  const bf16x8 *fr = static_cast<const bf16x8 *>(a.wsplit);
+  // output channels [64 t, 64 t + 64) (Co > 64: one co tile per grid row, the input re-staged
+  // per tile); the split weight fragments of tile t follow tile t - 1's
+  const int cot = blockIdx.y, co_base = 64 * cot;
+  const bf16x8 *fr = static_cast<const bf16x8 *>(a.wsplit) + (long)cot * NCC * 4 * 3 * 64;
   bf16x8 A[NCC][3];
 #pragma unroll
   for (int cc = 0; cc < NCC; ++cc)
@@ -291,7 +301,7 @@ __global__ __launch_bounds__(256) void pw_conv_nchw_s_kernel(PwArgs a) {
   float eb[1][4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int co = 16 * cb + 4 * kr + r;
+    const int co = co_base + 16 * cb + 4 * kr + r;
     eb[0][r] = (a.bias && co < Co) ? a.bias[co] : 0.f;
   }
 
@@ -350,7 +360,7 @@ __global__ __launch_bounds__(256) void pw_conv_nchw_s_kernel(PwArgs a) {
         pp -= P;
         ++nn;
       }
-      pw_store<1, ONH>(a, acc, eb, b * BP + off, cb, kr, nn, pp);
+      pw_store<1, ONH>(a, acc, eb, b * BP + off, cb, kr, nn, pp, co_base);
     }
     if (b + 1 < b1) {
       stage(buf ^ 1);
@@ -408,13 +418,35 @@ void launch_ci(const PwArgs &a, hipStream_t st) {
 int pw_conv_supported(int c, int co, int kh, int kw, int stride, int pad, int groups, long np,
                       int out_nhwc, int p) {
   return kh == 1 && kw == 1 && stride == 1 && pad == 0 && groups == 1 && (c == 32 || c == 64) &&
-         co >= 1 && co <= 64 && np + 16 < 0x7fffffffL && (!out_nhwc || co % 4 == 0) && p >= 1;
+         co >= 1 && (co <= 64 || (co <= 512 && co % 64 == 0)) && np + 16 < 0x7fffffffL &&
+         (!out_nhwc || co % 4 == 0) && p >= 1;
 }
 
 int pw_conv_launch(const PwArgs &a, hipStream_t st) {
   if (!a.x || !a.wsplit || !a.out || (a.post_scale && !a.post_shift)) return AANET_EINVAL;
   if (!pw_conv_supported(a.C, a.Co, 1, 1, 1, 0, 1, (long)a.N * a.P, a.out_nhwc, a.P))
     return AANET_EUNSUPPORTED;
+  if (a.Co > 64) {
+    // Co = 128 .. 512 (the feature extractors' expansions): 64-channel tiles over grid rows, NCHW
+    // input only (the channels-last kernel keeps its weights for all of Co in registers)
+    if (a.in_nhwc) return AANET_EUNSUPPORTED;
+    const long nblk = ((long)a.N * a.P + 63) / 64;
+    long g = (nblk + 3) / 4;
+    if (g > 1024) g = 1024;
+    const dim3 grid((unsigned)g, (unsigned)(a.Co / 64)), blk(256);
+    if (a.C == 32) {
+      if (a.out_nhwc)
+        hipLaunchKernelGGL((pw_conv_nchw_s_kernel<32, 4, 1>), grid, blk, 0, st, a);
+      else
+        hipLaunchKernelGGL((pw_conv_nchw_s_kernel<32, 4, 0>), grid, blk, 0, st, a);
+    } else {
+      if (a.out_nhwc)
+        hipLaunchKernelGGL((pw_conv_nchw_s_kernel<64, 4, 1>), grid, blk, 0, st, a);
+      else
+        hipLaunchKernelGGL((pw_conv_nchw_s_kernel<64, 4, 0>), grid, blk, 0, st, a);
+    }
+    return aanet_launch_status();
+  }
   if (a.C == 32)
     launch_ci<32>(a, st);
   else

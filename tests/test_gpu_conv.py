@@ -436,3 +436,28 @@ def test_refine_stem_matches_separate_convs(H, W):
                      F.leaky_relu(F.conv2d(disp.cpu().double(), w2.cpu().double(),
                                            b2.cpu().double(), padding=1), 0.2)), 1)
     assert (got.cpu().double() - cpu).abs().max().item() <= 1e-5 * (1 + cpu.abs().max().item())
+
+
+@pytest.mark.parametrize("C,Co,H,W", [(32, 128, 24, 52), (64, 256, 16, 26), (64, 512, 8, 13),
+                                      (32, 192, 5, 7)])
+@pytest.mark.parametrize("out_nhwc", [False, True])
+def test_pointwise_wide_outputs_vs_torch(C, Co, H, W, out_nhwc):
+    """1x1 convs with Co = 128 .. 512 (the ResNet bottlenecks' expansions, nets/resnet.py) on the
+    streaming pointwise kernel, one 64-channel tile per grid row: against torch CPU in fp64 with
+    bias, residual and activation, NCHW and channels-last output."""
+    g = torch.Generator().manual_seed(C + Co + H)
+    x = torch.randn(2, C, H, W, generator=g, dtype=torch.float64)
+    w = torch.randn(Co, C, 1, 1, generator=g, dtype=torch.float64) / C ** 0.5
+    b = torch.randn(Co, generator=g, dtype=torch.float64)
+    res = torch.randn(2, Co, H, W, generator=g, dtype=torch.float64)
+    ref = F.relu(F.conv2d(x, w, b) + res)
+    wd = w.float().to(DEV)
+    wp = ops.pack_weight_split(wd)
+    assert wp is not None
+    rd = res.float().to(DEV)
+    if out_nhwc:
+        rd = rd.contiguous(memory_format=torch.channels_last)
+    got = ops.conv2d_fused(x.float().to(DEV), wd, b.float().to(DEV), act="relu", residual=rd,
+                           packed_weight=wp, out_nhwc=out_nhwc)
+    err = (got.cpu().double() - ref).abs().max().item()
+    assert err <= 2e-5 * (1 + ref.abs().max().item()), err
