@@ -123,25 +123,29 @@ __device__ __forceinline__ TapState tap_state(float oh, float ow, float ml, int 
   return s;
 }
 
-// CG = channels per deformable group (two groups): 32 (scale 0: C = 64) or 16 (scale 1: C = 32).
+// CG = channels per deformable group (two groups): 32 (scale 0: C = 64), 16 (scale 1: C = 32) or
+// 64 (the feature extractor's DCNs, C = 128, op-level PLAIN form only: each group spans two
+// 32-channel phases, which recompute its sampling state; one workgroup per CU for the LDS).
 // A chunk is one tap of a 32-channel K slice ("phase"): with CG = 32 a phase is one group, with
 // CG = 16 it holds both groups (lane groups kr = 0, 1 carry group 0's channels, kr = 2, 3 group 1's).
 // XN: x is NCHW (the op-level forward, ModulatedDeformConvFunction) instead of channels-last.
 // PLAIN: no bottleneck tail -- out = act(post_scale * (DCN + bias) + post_shift), NCHW.
 template <int DIL, int CG, bool POST, bool XN = false, bool PLAIN = false>
-__global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
+__global__ __launch_bounds__(NT, CG == 64 ? 2 : 4) void dcn_tile_kernel(DcnTileArgs a) {
   constexpr int CT = 2 * CG;             // channels = Co = Co2
   constexpr int NPH = CT / 32;           // phases
   constexpr int NCH = NPH * K;           // chunks
   constexpr int NCO = CT / 16;           // 16-row co blocks
   constexpr int ABUF = NCO * 3 * 1024;   // one chunk's A fragments: NCO blocks x 3 pieces x 64 lanes x 16 B
-  constexpr int TPP = CG == 32 ? 4 : 2;  // taps per sampling pass (x groups per pass = 4 lane groups)
+  static_assert(CG != 64 || PLAIN, "64-channel groups: op-level form only");
+  constexpr bool WG = CG >= 32;          // a phase is (part of) ONE group: lane groups = 4 taps
+  constexpr int TPP = WG ? 4 : 2;        // taps per sampling pass (x groups per pass = 4 lane groups)
   constexpr int MG = DIL + RW;                     // window margin around the tile
   constexpr int WR = TR + 2 * MG, WC = TC + 2 * MG;
   constexpr int NPOS = (WR * WC + 63) / 64 * 64;   // positions per quad plane (multiple of 64)
   constexpr int NWI = NPOS / 64;                   // window quads staged per thread (8*NPOS/512)
   constexpr int WIN = 8 * NPOS * 16;               // window bytes: [8 channel quads][NPOS][16 B]
-  static_assert(WIN >= CT * OP * 4, "epilogue tile must fit the window");
+  static_assert(WIN >= (CT < 64 ? CT : 64) * OP * 4, "epilogue tile must fit the window");
   // Three LDS objects: the compiler orders a ds_read after an outstanding LDS-DMA only when they
   // may alias, so the DMA of tap c+1's weights into one A slot never holds reads of the window or
   // of the other slot.
@@ -229,22 +233,26 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   auto issue_a = [&](int c, char *dst) {
     if (dbg & 64) return;
     const int g = c / K, k = c - K * (c / K);
+    // the split pack is 64-row-tile major: blocks 4t .. 4t+3 of chunk (k, g) at tile t's copy
     const char *src = wsp + (long)((k * ncc + g) * 12) * 1024 + lane * 16;
+    const long tile = (long)K * ncc * 12 * 1024;
     for (int pc = wave; pc < 3 * NCO; pc += 8)
-      __builtin_amdgcn_global_load_lds((const void *)(src + pc * 1024), (lds_void *)(dst + pc * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void *)(src + (pc / 12) * tile + (pc % 12) * 1024),
+                                       (lds_void *)(dst + pc * 1024), 16, 0, 0);
   };
 
   // ---- sampling state: lane group kr computes (tap, group) pt(kr) of this lane's pixel: tap
   // t0 + kr of the phase's group (CG = 32), or tap t0 + (kr & 1) of group kr >> 1 (CG = 16)
-  const int pt = CG == 32 ? kr : (kr & 1);
-  const int lgrp = CG == 32 ? 0 : (kr >> 1);  // this lane's group within the phase
+  const int pt = WG ? kr : (kr & 1);
+  const int lgrp = WG ? 0 : (kr >> 1);  // this lane's group within the phase
+  constexpr int PPG = CG == 64 ? 2 : 1;  // phases per group
   float poh = 0.f, pow_ = 0.f, pml = 0.f;  // prefetched offsets / mask of the next pass
   // All three byte offsets are formed before the first load, in 32-bit 24-bit-multiply form: as
   // (plane * P * 4 + p4) the compiler chose v_mad_u64_u32 with a 64-bit addend register pair whose
   // high half was the destination of the offset load just issued, i.e. an s_waitcnt vmcnt(0) (a
   // full memory round trip) in every sampling pass.  Plane indices are < 2 * 2 * 9, P * 4 < 2^24.
   auto load_pass = [&](int g, int t0) {
-    const int t = min(t0 + pt, K - 1), gr = CG == 32 ? g : (kr >> 1);
+    const int t = min(t0 + pt, K - 1), gr = WG ? g / PPG : (kr >> 1);
     const unsigned P4 = (unsigned)P * 4u;
     const int o_h = (int)__umul24((unsigned)(gr * 2 * K + 2 * t), P4) + p4;
     const int o_w = o_h + (int)P4;
@@ -300,7 +308,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       if (s.pos < 0) {
         // global gather of this lane's corners (blended here, so no load is pending at the join)
 #pragma clang fp contract(off)
-        const int oplane = ((CG == 32 ? g : lgrp) * 2 * K + 2 * k) * P * 4;
+        const int oplane = ((WG ? g / PPG : lgrp) * 2 * K + 2 * k) * P * 4;
         const float oh = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, p4 + oplane, 0, 0));
         const float ow = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(offr, p4 + oplane + P * 4, 0, 0));
         const int i = k / 3, j = k - 3 * (k / 3);
@@ -347,8 +355,8 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       // the next phase's window and first offsets: issued once this chunk's corners are blended
       // (their registers free) and before its MFMAs, so the load latency overlaps the MFMA run
       __builtin_amdgcn_sched_barrier(0);
-      load_window(1);
-      load_pass(1, 0);
+      load_window(g + 1);
+      load_pass(g + 1, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
     const char *ab = sAc + lane * 16;
@@ -370,7 +378,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
   // front of it; issued after the DMA, that wait exposed the DMA's whole L2 latency every chunk.
   float pf_win = 0.f, pf_res = 0.f;
   auto step = [&](int c, const char *cur, char *nxt) {
-    const int g = c >= K ? 1 : 0, k = c - K * g, t0 = k - k % TPP;
+    const int g = c / K, k = c - K * g, t0 = k - k % TPP;
     TapState s;
     if (k == 0) {  // group start: its window (loaded in the chunk before) and pass-0 states
       if (g == 1) asm volatile("" ::"v"(pf_win));
@@ -402,7 +410,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
       const int yy = min(y0 + (tid & 7), H - 1), co2 = min(tid >> 3, a.Co2 - 1);
       pf_res = a.residual[((long)(n * a.Co2 + co2) * H + yy) * W + x0];
     }
-    tap(g, k, cur, s, NPH == 2 && c == K - 1);
+    tap(g, k, cur, s, g + 1 < NPH && k == K - 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of A(c+1) landed ...
     if (!(dbg & 8)) __syncthreads();                 // ... and every other wave's
   };
@@ -423,24 +431,29 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
     // ---- op-level DCN: act(post_scale * (acc + bias) + post_shift) -> LDS [co][px] -> NCHW rows
     // (the window is free: every wave passed the last chunk's barrier)
     float *sO = reinterpret_cast<float *>(sWin);
+    constexpr int CH = CT < 64 ? CT : 64;  // channels per pass through the LDS tile
 #pragma unroll
-    for (int m = 0; m < NCO; ++m) {
-      const int co = 16 * m + 4 * kr;
-      const f32x4 bs = a.bias ? *reinterpret_cast<const f32x4 *>(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 sc = a.post_scale ? *reinterpret_cast<const f32x4 *>(a.post_scale + co) : f32x4{1.f, 1.f, 1.f, 1.f};
-      const f32x4 sh = a.post_scale ? *reinterpret_cast<const f32x4 *>(a.post_shift + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int h0 = 0; h0 < CT; h0 += CH) {
+      if (h0) __syncthreads();  // the previous pass's rows are stored
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        sO[(co + r) * OP + wave * 16 + jj] = act_f((acc[m][r] + bs[r]) * sc[r] + sh[r], a.act);
-    }
-    __syncthreads();
-    constexpr int EPP = CT * TR * (TC / 4) / NT;  // 4-pixel items per thread
+      for (int m = h0 / 16; m < (h0 + CH) / 16; ++m) {
+        const int co = 16 * m + 4 * kr;
+        const f32x4 bs = a.bias ? *reinterpret_cast<const f32x4 *>(a.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 sc = a.post_scale ? *reinterpret_cast<const f32x4 *>(a.post_scale + co) : f32x4{1.f, 1.f, 1.f, 1.f};
+        const f32x4 sh = a.post_scale ? *reinterpret_cast<const f32x4 *>(a.post_shift + co) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < EPP; ++i) {
-      const int e = tid + NT * i, co = e >> 5, qi = e & 31, yy = y0 + (qi >> 2), xx = x0 + 4 * (qi & 3);
-      if (yy < H && xx < W)
-        *reinterpret_cast<f32x4 *>(a.out + ((long)(n * CT + co) * H + yy) * W + xx) =
-            *reinterpret_cast<const f32x4 *>(sO + co * OP + (qi >> 2) * 16 + 4 * (qi & 3));
+        for (int r = 0; r < 4; ++r)
+          sO[(co - h0 + r) * OP + wave * 16 + jj] = act_f((acc[m][r] + bs[r]) * sc[r] + sh[r], a.act);
+      }
+      __syncthreads();
+      constexpr int EPP = CH * TR * (TC / 4) / NT;  // 4-pixel items per thread
+#pragma unroll
+      for (int i = 0; i < EPP; ++i) {
+        const int e = tid + NT * i, co = e >> 5, qi = e & 31, yy = y0 + (qi >> 2), xx = x0 + 4 * (qi & 3);
+        if (yy < H && xx < W)
+          *reinterpret_cast<f32x4 *>(a.out + ((long)(n * CT + h0 + co) * H + yy) * W + xx) =
+              *reinterpret_cast<const f32x4 *>(sO + co * OP + (qi >> 2) * 16 + 4 * (qi & 3));
+      }
     }
     return;
   }
@@ -725,7 +738,7 @@ __global__ __launch_bounds__(NT, 4) void dcn_tile_kernel(DcnTileArgs a) {
 
 int dcn_tile_supported(int c, int co, int co2, int kh, int kw, int stride, int pad, int dil,
                        int dg, int groups, int w) {
-  return (c == 64 || c == 32) && co == c && co2 == c && kh == 3 && kw == 3 &&
+  return (c == 64 || c == 32 || c == 128) && co == c && co2 == c && kh == 3 && kw == 3 &&
          stride == 1 && pad == dil && dil == 2 && dg == 2 && groups == 1 && w % 4 == 0;
 }
 
@@ -765,8 +778,13 @@ int dcn_tile_launch(const DcnTileArgs &a, hipStream_t stream) {
   b.dbg = dbg;
   if (a.post_wsplit && a.C != 64) return AANET_EUNSUPPORTED;
   const dim3 grid((unsigned)(a.N * tiles));
+  if (a.C == 128 && !a.plain) return AANET_EUNSUPPORTED;  // 64-channel groups: op-level form only
   if (a.plain) {
-    if (a.C == 64 && a.x_nchw)
+    if (a.C == 128 && a.x_nchw)
+      hipLaunchKernelGGL((dcn_tile_kernel<2, 64, false, true, true>), grid, dim3(NT), 0, stream, b);
+    else if (a.C == 128)
+      hipLaunchKernelGGL((dcn_tile_kernel<2, 64, false, false, true>), grid, dim3(NT), 0, stream, b);
+    else if (a.C == 64 && a.x_nchw)
       hipLaunchKernelGGL((dcn_tile_kernel<2, 32, false, true, true>), grid, dim3(NT), 0, stream, b);
     else if (a.C == 64)
       hipLaunchKernelGGL((dcn_tile_kernel<2, 32, false, false, true>), grid, dim3(NT), 0, stream, b);

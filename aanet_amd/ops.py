@@ -212,8 +212,8 @@ class DispWarpFunction(Function):
 def window_fwd_ok(C, Co, kh, kw, stride, padding, dilation, groups, deformable_groups, W):
     """Whether the LDS-window DCN kernel takes an op-level forward shape
     (aanet_mdcn_window_fwd_supported): the aggregation's deformable convs -- 3x3, stride 1,
-    padding = dilation = 2, one conv group, two deformable groups of 32 or 16 channels
-    (C = Co = 64 or 32), W % 4 == 0."""
+    padding = dilation = 2, one conv group, two deformable groups of 64, 32 or 16 channels
+    (C = Co = 128, 64 or 32), W % 4 == 0."""
     return bool(_lib.lib().aanet_mdcn_window_fwd_supported(C, Co, kh, kw, stride, padding, dilation,
                                                            groups, deformable_groups, W))
 

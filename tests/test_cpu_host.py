@@ -224,9 +224,11 @@ def test_mdcn_backward_workspace_sizes():
 def test_window_fwd_support_query_without_a_gpu():
     """aanet_mdcn_window_fwd_supported (the op-level DCN forward's window dispatch) takes exactly
     the aggregation's deformable convs: 3x3, stride 1, pad = dil = 2, one conv group, two
-    deformable groups, C = Co in {32, 64}, W % 4 == 0 (nets/deform.py:216-226)."""
+    deformable groups, C = Co in {32, 64, 128}, W % 4 == 0 (nets/deform.py:216-226; 128 channels:
+    SURVEY C4's feat_s1 shape)."""
     ok = ops.window_fwd_ok
     assert ok(64, 64, 3, 3, 1, 2, 2, 1, 2, 416) and ok(32, 32, 3, 3, 1, 2, 2, 1, 2, 208)
+    assert ok(128, 128, 3, 3, 1, 2, 2, 1, 2, 104)
     assert not ok(16, 16, 3, 3, 1, 2, 2, 1, 2, 104)      # scale 2: 8 channels per group
     assert not ok(128, 128, 3, 3, 1, 1, 1, 1, 2, 104)    # feature DCN
     assert not ok(64, 64, 3, 3, 2, 2, 2, 1, 2, 416)      # stride 2

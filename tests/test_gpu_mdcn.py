@@ -493,6 +493,8 @@ WINDOW_FWD = [
     (1, 64, 13, 36, 3.0),
     (2, 32, 9, 28, 0.7),
     (1, 32, 21, 20, 3.0),
+    (2, 128, 16, 52, 0.7),  # 64-channel groups (SURVEY C4 feat_s1 shape class): 4 phases, 8 co blocks
+    (1, 128, 13, 36, 3.0),
 ]
 
 
