@@ -56,7 +56,67 @@ __global__ __launch_bounds__(256) void deconv2x_assemble_kernel(const float *__r
   }
 }
 
+// Channels-last form: the assembled [n][2h][2w][co + cr] tensor, for a consumer conv that stages
+// NHWC input (the Conv2x conv2 3x3 on the engine's halo tile).  A workgroup takes 32 output
+// columns of one output row and every channel: the phase / skip rows are read along x (two or
+// one contiguous segments per channel) into LDS [channel][column], then each column's channel
+// vector is written as contiguous 16-byte quads (the 32 columns' vectors are one contiguous run).
+constexpr int AC = 32;  // output columns per workgroup
+__global__ __launch_bounds__(256) void deconv2x_assemble_nhwc_kernel(const float *__restrict__ ph,
+                                                                     const float *__restrict__ rem,
+                                                                     float *__restrict__ out, int co,
+                                                                     int cr, int h, int w) {
+  extern __shared__ float s[];  // [ct][AC + 1]
+  const int W2 = 2 * w, H2 = 2 * h, ct = co + cr;
+  const int X0 = blockIdx.x * AC, Y = blockIdx.y, img = blockIdx.z;
+  const int a = Y & 1, y = Y >> 1;
+  const long ph_plane = (long)(h + 1) * (w + 1), o_plane = (long)H2 * W2;
+  const int ncol = min(AC, W2 - X0);
+  for (int e = threadIdx.x; e < ct * AC; e += 256) {
+    const int c = e / AC, u = e % AC, X = X0 + u;
+    float v = 0.f;
+    if (u < ncol) {
+      if (c < co) {
+        const int b = X & 1, x = X >> 1;
+        v = ph[((long)img * 4 * co + 4 * c + 2 * a + b) * ph_plane + (long)(y + a) * (w + 1) + x + b];
+      } else {
+        v = rem[((long)img * cr + (c - co)) * o_plane + (long)Y * W2 + X];
+      }
+    }
+    s[c * (AC + 1) + u] = v;
+  }
+  __syncthreads();
+  float *dst = out + (((long)img * H2 + Y) * W2 + X0) * ct;
+  if ((ct & 3) == 0) {
+    const int cq = ct / 4;
+    for (int e = threadIdx.x; e < ncol * cq; e += 256) {
+      const int u = e / cq, c = 4 * (e % cq);
+      *reinterpret_cast<f32x4 *>(dst + (long)u * ct + c) =
+          f32x4{s[c * (AC + 1) + u], s[(c + 1) * (AC + 1) + u], s[(c + 2) * (AC + 1) + u],
+                s[(c + 3) * (AC + 1) + u]};
+    }
+  } else {
+    for (int e = threadIdx.x; e < ncol * ct; e += 256) {
+      const int u = e / ct, c = e % ct;
+      dst[(long)u * ct + c] = s[c * (AC + 1) + u];
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" int aanet_deconv2x_assemble_nhwc_f32(const float *ph, const float *rem, float *out,
+                                                int n, int co, int cr, int h, int w,
+                                                aanet_stream_t stream) {
+  if (n < 0 || co < 0 || cr < 0 || h < 0 || w < 0) return AANET_EINVAL;
+  if ((long)n * (co + cr) * h * w == 0) return AANET_OK;
+  if (!out || (co && !ph) || (cr && !rem)) return AANET_EINVAL;
+  const long lds = (long)(co + cr) * (AC + 1) * 4;
+  if (lds > 64 * 1024 || 2L * h > 65535 || n > 65535) return AANET_EUNSUPPORTED;
+  hipLaunchKernelGGL(deconv2x_assemble_nhwc_kernel, dim3((unsigned)host_div_up(2 * w, AC), 2 * h, n),
+                     dim3(256), (unsigned)lds, as_hip(stream), ph, rem, out, co, cr, h, w);
+  return aanet_launch_status();
+}
 
 extern "C" int aanet_deconv2x_assemble_f32(const float *ph, const float *rem, float *out, int n,
                                            int co, int cr, int h, int w, aanet_stream_t stream) {

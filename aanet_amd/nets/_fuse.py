@@ -120,11 +120,20 @@ def folded_deconv(conv, bn):
     return w, b, wp
 
 
-def deconv_bn_act(x, conv, bn=None, act=None, rem=None):
+def deconv_bn_act(x, conv, bn=None, act=None, rem=None, out_nhwc=False):
     """act(BN(conv_transpose(x))) [+ the concat with rem] as the engine phase conv + one assembly
-    pass (ops.deconv2x)."""
+    pass (ops.deconv2x); out_nhwc: channels_last result."""
     w, b, wp = folded_deconv(conv, bn)
-    return ops.deconv2x(x, w, b, act, packed_weight=wp, rem=rem)
+    return ops.deconv2x(x, w, b, act, packed_weight=wp, rem=rem, out_nhwc=out_nhwc)
+
+
+def halo_input_ok(conv, c_in):
+    """Whether a plain conv gains from channels-last input: a 3x3 stride-1 pad-1 conv, one group,
+    split-packed weights, 32-channel K chunks -- the engine's halo tile (mdcn.hip HALO), which
+    stages an NHWC input once per chunk instead of an im2col per tap."""
+    return engine_conv(conv) and conv.kernel_size == (3, 3) and \
+        conv.stride == (1, 1) and conv.padding == (1, 1) and conv.dilation == (1, 1) and \
+        conv.groups == 1 and c_in % 32 == 0 and conv.out_channels >= 32
 
 
 def dense_grouped_ok(conv, x):

@@ -11,7 +11,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ._fuse import FusedSequential, conv_bn_act, deconv2x_ok, deconv_bn_act, engine_conv, use_fused
+from ._fuse import (FusedSequential, conv_bn_act, deconv2x_ok, deconv_bn_act, engine_conv,
+                    halo_input_ok, use_fused)
 from .deform import DeformConv2d
 from .._precision import fp32_convs
 
@@ -291,9 +292,14 @@ class Conv2x(nn.Module):
     def forward(self, x, rem):
         c1 = self.conv1
         if self.concat and c1.fused_deconv(x) and rem.shape[2:] == (2 * x.shape[2], 2 * x.shape[3]):
-            # transposed conv + BN + ReLU and the concat: one engine launch + one assembly pass
+            # transposed conv + BN + ReLU and the concat: one engine launch + one assembly pass,
+            # written channels-last when conv2 stages NHWC input (the halo tile; full-resolution
+            # 64 -> 32 conv of the refinement 1136 -> ... us)
+            c2 = self.conv2
+            nhwc = isinstance(c2, BasicConv) and use_fused(c2, x) and \
+                halo_input_ok(c2.conv, c1.conv.out_channels + rem.shape[1])
             x = deconv_bn_act(x, c1.conv, c1.bn if c1.use_bn else None,
-                              "relu" if c1.relu else None, rem=rem)
+                              "relu" if c1.relu else None, rem=rem, out_nhwc=nhwc)
             return self.conv2(x)
         x = self.conv1(x)
         assert x.size() == rem.size()

@@ -523,11 +523,12 @@ def deconv2x_phase_weight(weight, scale=None):
     return g.permute(0, 2, 4, 1, 3, 5).reshape(4 * co, ci, 2, 2).contiguous()
 
 
-def deconv2x(x, phase_weight, bias=None, act=None, packed_weight=None, rem=None):
+def deconv2x(x, phase_weight, bias=None, act=None, packed_weight=None, rem=None, out_nhwc=False):
     """act(ConvTranspose2d(k=4, stride 2, padding 1)(x) + bias) [, rem concatenated after its
     channels] -> [N, co (+ cr), 2H, 2W]: the 2x2 pad-1 phase conv on the HIP engine (weights from
     deconv2x_phase_weight, bias repeated per phase), then aanet_deconv2x_assemble_f32 (phase
-    scatter + the concat).  nets/feature.py:342-376 (Conv2x with deconv=True)."""
+    scatter + the concat).  nets/feature.py:342-376 (Conv2x with deconv=True).  out_nhwc=True:
+    a channels_last result (aanet_deconv2x_assemble_nhwc_f32) for an NHWC-staging consumer."""
     require_gpu(x, phase_weight, bias, packed_weight, rem,
                 names=("input", "weight", "bias", "packed", "rem"))
     N, C, H, W = x.shape
@@ -541,9 +542,10 @@ def deconv2x(x, phase_weight, bias=None, act=None, packed_weight=None, rem=None)
             raise ValueError(f"deconv2x: rem {tuple(rem.shape)} does not match the output "
                              f"{(N, co, 2 * H, 2 * W)}")
         cr = rem.shape[1]
-    out = torch.empty((N, co + cr, 2 * H, 2 * W), device=x.device, dtype=x.dtype)
-    call("aanet_deconv2x_assemble_f32", ptr(ph), ptr(rem), ptr(out), N, co, cr, H, W,
-         stream_of(x))
+    out = torch.empty((N, co + cr, 2 * H, 2 * W), device=x.device, dtype=x.dtype,
+                      memory_format=torch.channels_last if out_nhwc else torch.contiguous_format)
+    call("aanet_deconv2x_assemble_nhwc_f32" if out_nhwc else "aanet_deconv2x_assemble_f32",
+         ptr(ph), ptr(rem), ptr(out), N, co, cr, H, W, stream_of(x))
     return out
 
 

@@ -330,6 +330,10 @@ int aanet_conv3x3s2_terms_f32(const float *x, const void *wsplit, const float *b
  * as channels co .. co+cr-1 (the torch.cat of Conv2x.forward; cr = 0: no skip, rem may be NULL). */
 int aanet_deconv2x_assemble_f32(const float *ph, const float *rem, float *out, int n, int co, int cr,
                                 int h, int w, aanet_stream_t stream);
+/* The same assembly written channels-last: out [n][2h][2w][co + cr] (NHWC), for a consumer conv
+ * that stages NHWC input (Conv2x's conv2 on the halo tile).  EUNSUPPORTED when co + cr > 496. */
+int aanet_deconv2x_assemble_nhwc_f32(const float *ph, const float *rem, float *out, int n, int co,
+                                     int cr, int h, int w, aanet_stream_t stream);
 
 /* The warp-error stem of StereoDRNet / Hourglass refinement (nets/refinement.py:92-99, 148-155):
  *   out_nhwc[n][y][x][0:16]  = act(conv3x3([warped - left, left]; w1) + b1)   (conv1, 6 -> 16)

@@ -50,8 +50,8 @@ def test_deconv2x_vs_torch_fp64(case, with_rem):
 
 @pytest.mark.parametrize("ci,co,h,w", [(128, 96, 8, 26), (48, 32, 24, 78)])
 def test_conv2x_deconv_fused_matches_reference_order(ci, co, h, w):
-    """Conv2x(deconv=True) in eval: the fused path (phase conv + assembly + concat, then the 3x3
-    conv on the engine) against the module's reference op order on the GPU (MIOpen transposed
+    """Conv2x(deconv=True) in eval: the fused path (phase conv + channels-last assembly + concat,
+    then the 3x3 conv on the engine's halo tile, NCHW out) against the module's reference op order on the GPU (MIOpen transposed
     conv + BN + ReLU + torch.cat + conv), nonzero BN statistics."""
     torch.manual_seed(3)
     m = Conv2x(ci, co, deconv=True)
@@ -69,3 +69,25 @@ def test_conv2x_deconv_fused_matches_reference_order(ci, co, h, w):
         m.conv1.aanet_fuse = m.conv2.aanet_fuse = m.aanet_fuse = False
         ref = m(x, rem)
     assert (fused - ref).abs().max().item() <= 1e-4 * (1 + ref.abs().max().item())
+    assert not fused.is_contiguous(memory_format=torch.channels_last) or fused.shape[1] == 1
+
+
+@pytest.mark.parametrize("case", CASES + [(1, 32, 5, 7, 6)])  # + 6 / 12 channels: scalar stores
+@pytest.mark.parametrize("with_rem", [False, True])
+def test_deconv2x_nhwc_assembly_equals_nchw(case, with_rem):
+    """aanet_deconv2x_assemble_nhwc_f32 (channels-last out, for Conv2x's conv2 on the halo tile)
+    moves the same values as the NCHW assembly: bit-identical after the layout change, including
+    rows whose 2w is not a multiple of the 32-column tile."""
+    N, ci, h, w, co = case
+    g = torch.Generator().manual_seed(7 * ci + co)
+    x = torch.randn(N, ci, h, w, generator=g).to(DEV)
+    wt = (torch.randn(ci, co, 4, 4, generator=g) / (ci * 4) ** 0.5).to(DEV)
+    rem = torch.randn(N, co, 2 * h, 2 * w, generator=g).to(DEV) if with_rem else None
+    wd = ops.deconv2x_phase_weight(wt)
+    wp = ops.pack_weight_split(wd)
+    if wp is None:
+        wp = ops.pack_weight(wd)
+    a = ops.deconv2x(x, wd, None, "relu", packed_weight=wp, rem=rem)
+    b = ops.deconv2x(x, wd, None, "relu", packed_weight=wp, rem=rem, out_nhwc=True)
+    assert b.is_contiguous(memory_format=torch.channels_last) and b.shape == a.shape
+    assert torch.equal(a, b)
