@@ -43,6 +43,7 @@ _SIGNATURES = {
     "aanet_resize_bilinear_f32": [_P, _P, _L] + [_I] * 4 + [_P],
     "aanet_deconv2x_assemble_f32": [_P, _P, _P] + [_I] * 5 + [_P],
     "aanet_deconv2x_assemble_nhwc_f32": [_P, _P, _P] + [_I] * 5 + [_P],
+    "aanet_concat_nhwc_f32": [_P, _P, _P] + [_I] * 5 + [_P],
     "aanet_refine_stem_f32": [_P] * 7 + [_I, _P, _I, _I, _I, _P],
     "aanet_conv2d_fused_f32": [_P] * 6 + [_I, _I, _P] + [_I] * 12 + [_P],
     "aanet_conv_weight_pack_f32": [_P, _P, _I, _I, _I, _I, _P],

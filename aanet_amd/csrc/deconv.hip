@@ -61,7 +61,10 @@ __global__ __launch_bounds__(256) void deconv2x_assemble_kernel(const float *__r
 // columns of one output row and every channel: the phase / skip rows are read along x (two or
 // one contiguous segments per channel) into LDS [channel][column], then each column's channel
 // vector is written as contiguous 16-byte quads (the 32 columns' vectors are one contiguous run).
+// PHASE false: the first source is a plain NCHW tensor of the output size (the torch.cat of a
+// non-transposed Conv2x, aanet_concat_nhwc_f32).
 constexpr int AC = 32;  // output columns per workgroup
+template <bool PHASE>
 __global__ __launch_bounds__(256) void deconv2x_assemble_nhwc_kernel(const float *__restrict__ ph,
                                                                      const float *__restrict__ rem,
                                                                      float *__restrict__ out, int co,
@@ -76,9 +79,11 @@ __global__ __launch_bounds__(256) void deconv2x_assemble_nhwc_kernel(const float
     const int c = e / AC, u = e % AC, X = X0 + u;
     float v = 0.f;
     if (u < ncol) {
-      if (c < co) {
+      if (c < co && PHASE) {
         const int b = X & 1, x = X >> 1;
         v = ph[((long)img * 4 * co + 4 * c + 2 * a + b) * ph_plane + (long)(y + a) * (w + 1) + x + b];
+      } else if (c < co) {
+        v = ph[((long)img * co + c) * o_plane + (long)Y * W2 + X];
       } else {
         v = rem[((long)img * cr + (c - co)) * o_plane + (long)Y * W2 + X];
       }
@@ -113,8 +118,21 @@ extern "C" int aanet_deconv2x_assemble_nhwc_f32(const float *ph, const float *re
   if (!out || (co && !ph) || (cr && !rem)) return AANET_EINVAL;
   const long lds = (long)(co + cr) * (AC + 1) * 4;
   if (lds > 64 * 1024 || 2L * h > 65535 || n > 65535) return AANET_EUNSUPPORTED;
-  hipLaunchKernelGGL(deconv2x_assemble_nhwc_kernel, dim3((unsigned)host_div_up(2 * w, AC), 2 * h, n),
+  hipLaunchKernelGGL(deconv2x_assemble_nhwc_kernel<true>, dim3((unsigned)host_div_up(2 * w, AC), 2 * h, n),
                      dim3(256), (unsigned)lds, as_hip(stream), ph, rem, out, co, cr, h, w);
+  return aanet_launch_status();
+}
+
+extern "C" int aanet_concat_nhwc_f32(const float *a, const float *b, float *out, int n, int ca,
+                                     int cb, int h, int w, aanet_stream_t stream) {
+  if (n < 0 || ca < 0 || cb < 0 || h < 0 || w < 0) return AANET_EINVAL;
+  if ((long)n * (ca + cb) * h * w == 0) return AANET_OK;
+  if (!out || (ca && !a) || (cb && !b)) return AANET_EINVAL;
+  const long lds = (long)(ca + cb) * (AC + 1) * 4;
+  if (lds > 64 * 1024 || h > 65535 || n > 65535 || (h & 1) || (w & 1)) return AANET_EUNSUPPORTED;
+  // the kernel works in output (2h', 2w') units: h' = h / 2, w' = w / 2
+  hipLaunchKernelGGL(deconv2x_assemble_nhwc_kernel<false>, dim3((unsigned)host_div_up(w, AC), h, n),
+                     dim3(256), (unsigned)lds, as_hip(stream), a, b, out, ca, cb, h / 2, w / 2);
   return aanet_launch_status();
 }
 

@@ -133,7 +133,7 @@ def halo_input_ok(conv, c_in):
     stages an NHWC input once per chunk instead of an im2col per tap."""
     return engine_conv(conv) and conv.kernel_size == (3, 3) and \
         conv.stride == (1, 1) and conv.padding == (1, 1) and conv.dilation == (1, 1) and \
-        conv.groups == 1 and c_in % 32 == 0 and conv.out_channels >= 32
+        conv.groups == 1 and c_in % 32 == 0 and c_in <= 496 and conv.out_channels >= 32
 
 
 def dense_grouped_ok(conv, x):

@@ -13,6 +13,7 @@ import torch.nn.functional as F
 
 from ._fuse import (FusedSequential, conv_bn_act, deconv2x_ok, deconv_bn_act, engine_conv,
                     halo_input_ok, use_fused)
+from .. import ops
 from .deform import DeformConv2d
 from .._precision import fp32_convs
 
@@ -303,6 +304,12 @@ class Conv2x(nn.Module):
             return self.conv2(x)
         x = self.conv1(x)
         assert x.size() == rem.size()
+        c2 = self.conv2
+        if self.concat and isinstance(c2, BasicConv) and use_fused(c2, x) and \
+                x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and \
+                halo_input_ok(c2.conv, x.shape[1] + rem.shape[1]):
+            # the concat written channels-last: conv2 stages it on the halo tile
+            return c2(ops.concat_nhwc(x, rem))
         x = torch.cat((x, rem), 1) if self.concat else x + rem
         return self.conv2(x)
 

@@ -549,6 +549,21 @@ def deconv2x(x, phase_weight, bias=None, act=None, packed_weight=None, rem=None,
     return out
 
 
+def concat_nhwc(a, b):
+    """torch.cat((a, b), 1) of two NCHW tensors as a channels_last tensor (aanet_concat_nhwc_f32;
+    even H and W, at most 496 channels)."""
+    require_gpu(a, b, names=("a", "b"))
+    N, ca, H, W = a.shape
+    if b.shape[0] != N or tuple(b.shape[2:]) != (H, W):
+        raise ValueError(f"concat_nhwc: {tuple(a.shape)} and {tuple(b.shape)} do not concatenate")
+    cb = b.shape[1]
+    out = torch.empty((N, ca + cb, H, W), device=a.device, dtype=a.dtype,
+                      memory_format=torch.channels_last)
+    call("aanet_concat_nhwc_f32", ptr(a.contiguous()), ptr(b.contiguous()), ptr(out), N, ca, cb,
+         H, W, stream_of(a))
+    return out
+
+
 def refine_stem(warped, left, disp, w1, b1, w2, b2, act="leaky"):
     """torch.cat((act(conv1(cat(warped - left, left))), act(conv2(disp))), 1) as one channels-last
     [N, 32, H, W] tensor (aanet_refine_stem_f32; nets/refinement.py:92-99 with BN folded into

@@ -334,6 +334,12 @@ int aanet_deconv2x_assemble_f32(const float *ph, const float *rem, float *out, i
  * that stages NHWC input (Conv2x's conv2 on the halo tile).  EUNSUPPORTED when co + cr > 496. */
 int aanet_deconv2x_assemble_nhwc_f32(const float *ph, const float *rem, float *out, int n, int co,
                                      int cr, int h, int w, aanet_stream_t stream);
+/* torch.cat((a, b), 1) of two NCHW tensors [n][ca][h][w], [n][cb][h][w] written channels-last
+ * (out [n][h][w][ca + cb]): the concat of a non-transposed Conv2x (nets/feature.py:342-376) for
+ * its conv2 on the halo tile.  EUNSUPPORTED for odd h or w or ca + cb > 496 (callers fall back to
+ * torch.cat). */
+int aanet_concat_nhwc_f32(const float *a, const float *b, float *out, int n, int ca, int cb, int h,
+                          int w, aanet_stream_t stream);
 
 /* The warp-error stem of StereoDRNet / Hourglass refinement (nets/refinement.py:92-99, 148-155):
  *   out_nhwc[n][y][x][0:16]  = act(conv3x3([warped - left, left]; w1) + b1)   (conv1, 6 -> 16)

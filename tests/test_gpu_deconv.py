@@ -91,3 +91,35 @@ def test_deconv2x_nhwc_assembly_equals_nchw(case, with_rem):
     b = ops.deconv2x(x, wd, None, "relu", packed_weight=wp, rem=rem, out_nhwc=True)
     assert b.is_contiguous(memory_format=torch.channels_last) and b.shape == a.shape
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("shape", [(2, 48, 48, 24, 78), (1, 64, 64, 12, 40), (1, 6, 3, 4, 6)])
+def test_concat_nhwc_equals_torch_cat(shape):
+    """aanet_concat_nhwc_f32: torch.cat((a, b), 1) written channels-last, bit-identical."""
+    N, ca, cb, H, W = shape
+    a = torch.randn(N, ca, H, W, device=DEV)
+    b = torch.randn(N, cb, H, W, device=DEV)
+    got = ops.concat_nhwc(a, b)
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(got, torch.cat((a, b), 1))
+
+
+@pytest.mark.parametrize("ci,co,h,w", [(32, 48, 48, 156), (48, 64, 24, 78)])
+def test_conv2x_plain_fused_matches_reference_order(ci, co, h, w):
+    """Conv2x (stride-2 conv, concat, 3x3 conv; the hourglasses' conv1b / conv2b) in eval: the
+    fused path (concat written channels-last, conv2 on the halo tile) against the reference op
+    order on the GPU (MIOpen convs + BN + ReLU + torch.cat)."""
+    torch.manual_seed(5)
+    m = Conv2x(ci, co)
+    with torch.no_grad():
+        for bn in (m.conv1.bn, m.conv2.bn):
+            bn.running_mean.normal_(0, 0.1)
+            bn.running_var.uniform_(0.5, 1.5)
+    m = m.to(DEV).eval()
+    x = torch.randn(2, ci, h, w, device=DEV)
+    rem = torch.randn(2, co, h // 2, w // 2, device=DEV)
+    with torch.no_grad():
+        fused = m(x, rem)
+        m.conv1.aanet_fuse = m.conv2.aanet_fuse = m.aanet_fuse = False
+        ref = m(x, rem)
+    assert (fused - ref).abs().max().item() <= 1e-4 * (1 + ref.abs().max().item())
