@@ -57,38 +57,56 @@ __global__ __launch_bounds__(256) void deconv2x_assemble_kernel(const float *__r
 }
 
 // Channels-last form: the assembled [n][2h][2w][co + cr] tensor, for a consumer conv that stages
-// NHWC input (the Conv2x conv2 3x3 on the engine's halo tile).  A workgroup takes 32 output
-// columns of one output row and every channel: the phase / skip rows are read along x (two or
+// NHWC input (the Conv2x conv2 3x3 on the engine's halo tile).  A workgroup takes 64 output
+// columns (32 past 248 channels) of one output row and every channel: the phase / skip rows are read along x (two or
 // one contiguous segments per channel) into LDS [channel][column], then each column's channel
 // vector is written as contiguous 16-byte quads (the 32 columns' vectors are one contiguous run).
 // PHASE false: the first source is a plain NCHW tensor of the output size (the torch.cat of a
 // non-transposed Conv2x, aanet_concat_nhwc_f32).
-constexpr int AC = 32;  // output columns per workgroup
-template <bool PHASE>
+template <bool PHASE, int AC>  // AC: output columns per workgroup (64, or 32 past 248 channels)
 __global__ __launch_bounds__(256) void deconv2x_assemble_nhwc_kernel(const float *__restrict__ ph,
                                                                      const float *__restrict__ rem,
                                                                      float *__restrict__ out, int co,
                                                                      int cr, int h, int w) {
   extern __shared__ float s[];  // [ct][AC + 1]
+  constexpr int QPC = AC / 4;   // column quads per channel row
   const int W2 = 2 * w, H2 = 2 * h, ct = co + cr;
   const int X0 = blockIdx.x * AC, Y = blockIdx.y, img = blockIdx.z;
   const int a = Y & 1, y = Y >> 1;
   const long ph_plane = (long)(h + 1) * (w + 1), o_plane = (long)H2 * W2;
   const int ncol = min(AC, W2 - X0);
-  for (int e = threadIdx.x; e < ct * AC; e += 256) {
-    const int c = e / AC, u = e % AC, X = X0 + u;
-    float v = 0.f;
-    if (u < ncol) {
-      if (c < co && PHASE) {
-        const int b = X & 1, x = X >> 1;
-        v = ph[((long)img * 4 * co + 4 * c + 2 * a + b) * ph_plane + (long)(y + a) * (w + 1) + x + b];
-      } else if (c < co) {
-        v = ph[((long)img * co + c) * o_plane + (long)Y * W2 + X];
-      } else {
-        v = rem[((long)img * cr + (c - co)) * o_plane + (long)Y * W2 + X];
+  // one item = 4 consecutive columns of one channel; four items' loads are issued before their
+  // LDS stores (16 loads in flight per thread)
+  const int items = ct * QPC;
+  for (int e0 = threadIdx.x; e0 < items; e0 += 4 * 256) {
+    float v[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = e0 + 256 * i, c = e / QPC, u0 = 4 * (e % QPC);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int u = u0 + k, X = X0 + u;
+        float t = 0.f;
+        if (e < items && u < ncol) {
+          if (c < co && PHASE) {
+            const int b = X & 1, x = X >> 1;
+            t = ph[((long)img * 4 * co + 4 * c + 2 * a + b) * ph_plane + (long)(y + a) * (w + 1) + x + b];
+          } else if (c < co) {
+            t = ph[((long)img * co + c) * o_plane + (long)Y * W2 + X];
+          } else {
+            t = rem[((long)img * cr + (c - co)) * o_plane + (long)Y * W2 + X];
+          }
+        }
+        v[i][k] = t;
       }
     }
-    s[c * (AC + 1) + u] = v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = e0 + 256 * i, c = e / QPC, u0 = 4 * (e % QPC);
+      if (e < items)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s[c * (AC + 1) + u0 + k] = v[i][k];
+    }
   }
   __syncthreads();
   float *dst = out + (((long)img * H2 + Y) * W2 + X0) * ct;
@@ -108,6 +126,21 @@ __global__ __launch_bounds__(256) void deconv2x_assemble_nhwc_kernel(const float
   }
 }
 
+template <bool PHASE>
+int launch_nhwc(const float *src, const float *rem, float *out, int n, int co, int cr, int h,
+                int w, hipStream_t st) {
+  const int ct = co + cr;
+  if ((long)ct * 65 * 4 <= 64 * 1024)
+    hipLaunchKernelGGL((deconv2x_assemble_nhwc_kernel<PHASE, 64>), dim3((unsigned)host_div_up(2 * w, 64), 2 * h, n),
+                       dim3(256), (unsigned)(ct * 65 * 4), st, src, rem, out, co, cr, h, w);
+  else if ((long)ct * 33 * 4 <= 64 * 1024)
+    hipLaunchKernelGGL((deconv2x_assemble_nhwc_kernel<PHASE, 32>), dim3((unsigned)host_div_up(2 * w, 32), 2 * h, n),
+                       dim3(256), (unsigned)(ct * 33 * 4), st, src, rem, out, co, cr, h, w);
+  else
+    return AANET_EUNSUPPORTED;
+  return aanet_launch_status();
+}
+
 }  // namespace
 
 extern "C" int aanet_deconv2x_assemble_nhwc_f32(const float *ph, const float *rem, float *out,
@@ -116,11 +149,8 @@ extern "C" int aanet_deconv2x_assemble_nhwc_f32(const float *ph, const float *re
   if (n < 0 || co < 0 || cr < 0 || h < 0 || w < 0) return AANET_EINVAL;
   if ((long)n * (co + cr) * h * w == 0) return AANET_OK;
   if (!out || (co && !ph) || (cr && !rem)) return AANET_EINVAL;
-  const long lds = (long)(co + cr) * (AC + 1) * 4;
-  if (lds > 64 * 1024 || 2L * h > 65535 || n > 65535) return AANET_EUNSUPPORTED;
-  hipLaunchKernelGGL(deconv2x_assemble_nhwc_kernel<true>, dim3((unsigned)host_div_up(2 * w, AC), 2 * h, n),
-                     dim3(256), (unsigned)lds, as_hip(stream), ph, rem, out, co, cr, h, w);
-  return aanet_launch_status();
+  if (2L * h > 65535 || n > 65535) return AANET_EUNSUPPORTED;
+  return launch_nhwc<true>(ph, rem, out, n, co, cr, h, w, as_hip(stream));
 }
 
 extern "C" int aanet_concat_nhwc_f32(const float *a, const float *b, float *out, int n, int ca,
@@ -128,12 +158,9 @@ extern "C" int aanet_concat_nhwc_f32(const float *a, const float *b, float *out,
   if (n < 0 || ca < 0 || cb < 0 || h < 0 || w < 0) return AANET_EINVAL;
   if ((long)n * (ca + cb) * h * w == 0) return AANET_OK;
   if (!out || (ca && !a) || (cb && !b)) return AANET_EINVAL;
-  const long lds = (long)(ca + cb) * (AC + 1) * 4;
-  if (lds > 64 * 1024 || h > 65535 || n > 65535 || (h & 1) || (w & 1)) return AANET_EUNSUPPORTED;
+  if (h > 65535 || n > 65535 || (h & 1) || (w & 1)) return AANET_EUNSUPPORTED;
   // the kernel works in output (2h', 2w') units: h' = h / 2, w' = w / 2
-  hipLaunchKernelGGL(deconv2x_assemble_nhwc_kernel<false>, dim3((unsigned)host_div_up(w, AC), h, n),
-                     dim3(256), (unsigned)lds, as_hip(stream), a, b, out, ca, cb, h / 2, w / 2);
-  return aanet_launch_status();
+  return launch_nhwc<false>(a, b, out, n, ca, cb, h / 2, w / 2, as_hip(stream));
 }
 
 extern "C" int aanet_deconv2x_assemble_f32(const float *ph, const float *rem, float *out, int n,
