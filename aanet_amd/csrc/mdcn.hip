@@ -353,7 +353,7 @@ __host__ __device__ inline long split_frag_offset(int co, int cg, int kk) {
 }
 __host__ __device__ inline long split_frag_count(int co, int cg, int kk, int groups) {
   const int cog = co / groups;
-  return (long)groups * ((cog + 63) / 64) * kk * (cg / 32) * 4 * 3 * 64;
+  return (long)groups * ((cog + 63) / 64) * kk * ((cg + 31) / 32) * 4 * 3 * 64;
 }
 
 // Activations are split two values at a time by common.h split_pair (x = h + m + l exactly).
@@ -453,7 +453,10 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   // PREC 1 (split-bf16 contraction, see split4 / SplitLds): both operand tiles as three bf16
   // piece planes of 32-channel rows, 64 B per row (XOR-swizzled 16-byte quads, no padding)
   constexpr bool SPL = PREC == 1;
-  static_assert(!SPL || (CK == 32 && FULL && PACKED && CO_T >= 32), "split-bf16 configuration");
+  // (partial chunks: plain NCHW convs whose group width is a multiple of 16 but not 32 -- the
+  // zero-padded split pack, rows past the group staged as zeros)
+  static_assert(!SPL || (CK == 32 && (FULL || (MODE == 0 && !INH && !TAIL)) && PACKED && CO_T >= 32),
+                "split-bf16 configuration");
   constexpr int BUF = SPL ? PTT * 48 : (PTT + CO_T) * SP; // floats per LDS buffer
   constexpr int OP = PTT + 4;            // epilogue tile pitch
   static_assert(CO_T * OP <= 2 * BUF, "epilogue tile must fit the staging buffers");
@@ -556,7 +559,7 @@ __global__ __launch_bounds__(FNT, 4) void conv_fwd_kernel(MdcnArgs a) {
   // PREC 1: the wave's A fragments (its NCB 16-row blocks x 3 pieces) come from the pre-split
   // weight fragments in global memory (L2-resident), loaded one chunk ahead of their MFMAs
   bf16x8 fa[SPL ? NCB : 1][3];
-  const int sT = (Cog + 63) / 64, sNCC = Cg / 32;
+  const int sT = (Cog + 63) / 64, sNCC = (Cg + 31) / 32;
   const int st64 = (cot * CO_T) / 64, sbb = ((cot * CO_T) % 64) / 16 + wc0;
   auto load_a = [&](const bf16x8 *frag, long tile_base) {
 #pragma unroll
@@ -2546,6 +2549,13 @@ DcnSmallArgs small_args(const MdcnArgs &a, const float *weight, int packed) {
 template <int MODE, int CO_T, int PTT, int FULL, int CFG>
 void launch_fwd_f(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
   const dim3 blk(FNT);
+  if constexpr (!FULL && MODE == 0 && CFG == 0 && CO_T >= 32) {
+    // plain NCHW conv, group width 16 (mod 32): split-bf16 over zero-padded 32-channel chunks
+    if (a.split && packed && !a.tail_w && a.layout == 0) {
+      hipLaunchKernelGGL((conv_fwd_kernel<0, CO_T, PTT, 1, 0, 1, 0, 0, 0, 1>), grid, blk, 0, st, a);
+      return;
+    }
+  }
   if constexpr (FULL && CFG == 0 && CO_T >= 32) {  // split-bf16 contraction (PREC 1)
     if constexpr (MODE == 0 && PTT == 128) {
       if (a.split && packed && a.halo == 4) {  // phase-strided halo tile (dilation > 2)
@@ -2620,6 +2630,10 @@ int full_cfg(const MdcnArgs &a, int mode, int co_t) {
 template <int MODE, int CO_T, int PTT>
 void launch_fwd_t(const MdcnArgs &a, int packed, dim3 grid, hipStream_t st) {
   const int cfg = full_cfg(a, MODE, CO_T);
+  if (MODE == 0 && CO_T >= 32 && a.split && packed && !a.tail_w && a.layout == 0 && (a.C / a.groups) % 32) {
+    launch_fwd_f<MODE, CO_T, PTT, 0, 0>(a, packed, grid, st);  // zero-padded split chunks
+    return;
+  }
   constexpr bool C1 = CO_T >= 32 && PTT == 128;  // 16-channel chunks: 4 staged values per thread
   if (cfg == 0)
     launch_fwd_f<MODE, CO_T, PTT, 1, 0>(a, packed, grid, st);
@@ -2819,7 +2833,7 @@ void set_split(MdcnArgs &a, int flags, int packed) {
 // one thread per (g, t, k, cc, blk, lane): 8 weights -> their three bf16 pieces
 __global__ void pack_split_kernel(const float *__restrict__ w, bf16x8_t *__restrict__ frag, int Co,
                                   int Cg, int K, int groups) {
-  const int Cog = Co / groups, T = (Cog + 63) / 64, NCC = Cg / 32;
+  const int Cog = Co / groups, T = (Cog + 63) / 64, NCC = (Cg + 31) / 32;  // zero-padded chunks
   const long total = (long)groups * T * K * NCC * 4 * 64;
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const int lane = (int)(e & 63);
@@ -2837,7 +2851,7 @@ __global__ void pack_split_kernel(const float *__restrict__ w, bf16x8_t *__restr
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = 32 * cc + 8 * (lane >> 4) + j;
-      const float v = row < Cog ? w[((long)co * Cg + c) * K + k] : 0.f;
+      const float v = row < Cog && c < Cg ? w[((long)co * Cg + c) * K + k] : 0.f;
       const __bf16 h = (__bf16)v;
       const float r1 = v - (float)h;
       const __bf16 m = (__bf16)r1;
@@ -3187,7 +3201,10 @@ extern "C" int aanet_conv_weight_pack_f32(const float *weight, float *weight_pac
 }
 
 extern "C" long aanet_conv_weight_pack_split_bytes(int co, int cg, int kh, int kw, int groups) {
-  if (co <= 0 || cg <= 0 || kh <= 0 || kw <= 0 || groups <= 0 || co % groups || cg % 32) return 0;
+  // cg a multiple of 32, or of 16 past 32 (48, 80, ...: the last chunk zero-padded; plain NCHW
+  // convs only take the split form then)
+  if (co <= 0 || cg <= 0 || kh <= 0 || kw <= 0 || groups <= 0 || co % groups) return 0;
+  if (cg % 32 && (cg % 16 || cg < 48)) return 0;
   return split_frag_offset(co, cg, kh * kw) + split_frag_count(co, cg, kh * kw, groups) * 16;
 }
 

@@ -43,6 +43,11 @@ def _errs(got, ref64, scale64):
     (1, 96, 13, 30, 64, 3, 1, 1, 1, 1, True),     # 3 channel chunks, element epilogue
     (1, 64, 9, 20, 40, 3, 1, 2, 2, 1, True),      # dilation 2, Co = 40 of a 64 tile
     (2, 32, 8, 16, 32, 3, 1, 1, 1, 1, True),      # one chunk, 32-channel tile, exact tile fit
+    # group width 16 (mod 32): zero-padded last chunk (the hourglasses' 48-channel convs)
+    (2, 48, 24, 52, 64, 3, 1, 1, 1, 1, False),    # 3x3 stride 1
+    (2, 48, 25, 36, 64, 3, 2, 1, 1, 1, False),    # conv2a: stride 2, ragged
+    (1, 48, 13, 30, 128, 2, 1, 1, 1, 1, False),   # deconv1 phase conv: 2x2 pad 1, two co tiles
+    (1, 80, 9, 20, 32, 3, 1, 1, 1, 1, False),     # three chunks, the last half empty
 ])
 def test_split_conv_accuracy_vs_fp64(case):
     N, C, H, W, Co, k, s, p, d, g, nhwc = case
