@@ -69,44 +69,41 @@ __global__ __launch_bounds__(256) void deconv2x_assemble_nhwc_kernel(const float
                                                                      float *__restrict__ out, int co,
                                                                      int cr, int h, int w) {
   extern __shared__ float s[];  // [ct][AC + 1]
-  constexpr int QPC = AC / 4;   // column quads per channel row
   const int W2 = 2 * w, H2 = 2 * h, ct = co + cr;
   const int X0 = blockIdx.x * AC, Y = blockIdx.y, img = blockIdx.z;
   const int a = Y & 1, y = Y >> 1;
   const long ph_plane = (long)(h + 1) * (w + 1), o_plane = (long)H2 * W2;
   const int ncol = min(AC, W2 - X0);
-  // one item = 4 consecutive columns of one channel; four items' loads are issued before their
-  // LDS stores (16 loads in flight per thread)
-  const int items = ct * QPC;
-  for (int e0 = threadIdx.x; e0 < items; e0 += 4 * 256) {
-    float v[4][4];
+  // element e = (channel c, lane-column l) with l fastest: one wave instruction reads a whole
+  // channel row -- for a phase channel, columns of parity b = l / (AC/2) at phase index
+  // j = l % (AC/2) (two contiguous runs, of phases (a, 0) and (a, 1)); for the skip / plain
+  // source, AC contiguous columns.  Four loads in flight per thread before their LDS stores.
+  constexpr int HALF = AC / 2;
+  const int total = ct * AC;
+  for (int e0 = threadIdx.x; e0 < total; e0 += 4 * 256) {
+    float v[4];
+    int so[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int e = e0 + 256 * i, c = e / QPC, u0 = 4 * (e % QPC);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int u = u0 + k, X = X0 + u;
-        float t = 0.f;
-        if (e < items && u < ncol) {
-          if (c < co && PHASE) {
-            const int b = X & 1, x = X >> 1;
-            t = ph[((long)img * 4 * co + 4 * c + 2 * a + b) * ph_plane + (long)(y + a) * (w + 1) + x + b];
-          } else if (c < co) {
-            t = ph[((long)img * co + c) * o_plane + (long)Y * W2 + X];
-          } else {
-            t = rem[((long)img * cr + (c - co)) * o_plane + (long)Y * W2 + X];
-          }
-        }
-        v[i][k] = t;
+      const int e = e0 + 256 * i, c = e / AC, l = e % AC;
+      int u = l;
+      float t = 0.f;
+      if (c < co && PHASE) {
+        const int b = l / HALF, jx = l % HALF;
+        u = 2 * jx + b;
+        if (e < total && u < ncol)
+          t = ph[((long)img * 4 * co + 4 * c + 2 * a + b) * ph_plane + (long)(y + a) * (w + 1) +
+                 X0 / 2 + jx + b];
+      } else if (e < total && u < ncol) {
+        t = c < co ? ph[((long)img * co + c) * o_plane + (long)Y * W2 + X0 + u]
+                   : rem[((long)img * cr + (c - co)) * o_plane + (long)Y * W2 + X0 + u];
       }
+      v[i] = t;
+      so[i] = e < total ? c * (AC + 1) + u : -1;
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = e0 + 256 * i, c = e / QPC, u0 = 4 * (e % QPC);
-      if (e < items)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s[c * (AC + 1) + u0 + k] = v[i][k];
-    }
+    for (int i = 0; i < 4; ++i)
+      if (so[i] >= 0) s[so[i]] = v[i];
   }
   __syncthreads();
   float *dst = out + (((long)img * H2 + Y) * W2 + X0) * ct;
