@@ -18,7 +18,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from ._fuse import FoldCacheMixin, bn_affine, conv_bn_act, folded, offset_conv_eval, use_fused
+from ._fuse import (FoldCacheMixin, bn_affine, conv_bn_act, folded, halo_input_ok,
+                    offset_conv_eval, use_fused)
 from .deform_conv import DeformConv, ModulatedDeformConv
 from .._precision import fp32_convs
 
@@ -161,7 +162,10 @@ class _BottleneckBase(FoldCacheMixin, nn.Module):
         else:
             pw = c2.groups == 1 and width <= 64 and w3.shape[0] <= 64 and \
                 c2.stride[0] == c2.stride[1] and c2.padding[0] == c2.padding[1]
-            nhwc = pw and width % 32 == 0
+            # the ResNet bottlenecks (x4 expansion, no tail kernel): conv1 still writes
+            # channels-last when conv2 is a plain 3x3 stride-1 conv, which then stages it on the
+            # engine's halo tile (AANetFeature layer1 / layer2)
+            nhwc = (pw or halo_input_ok(c2, width)) and width % 32 == 0
         prep = prep if deform and self.conv2.modulation and pw else None
         main = torch.cuda.current_stream(x.device) if prep is not None else None
         if prep is not None:
