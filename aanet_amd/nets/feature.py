@@ -177,11 +177,18 @@ class FeaturePyramidNetwork(nn.Module):
         if use_fused(self, inputs[0]):
             # top-down from the coarsest level: each lateral conv adds the upsampled coarser
             # lateral in its epilogue (residual), so no separate add pass
+            # The laterals are written channels-last when the 3x3 output convs can stage NHWC
+            # input (the engine's halo tile); nearest upsampling keeps channels-last.
+            nhwc = all(isinstance(f[0], nn.Conv2d) and
+                       halo_input_ok(f[0], f[0].in_channels) for f in self.fpn_convs)
             lat = [None] * n
-            lat[n - 1] = conv_bn_act(inputs[n - 1], self.lateral_convs[n - 1])
+            lat[n - 1] = conv_bn_act(inputs[n - 1], self.lateral_convs[n - 1], out_nhwc=nhwc)
             for i in range(n - 1, 0, -1):
                 up = F.interpolate(lat[i], scale_factor=2, mode='nearest')
-                lat[i - 1] = conv_bn_act(inputs[i - 1], self.lateral_convs[i - 1], residual=up)
+                if nhwc:
+                    up = up.contiguous(memory_format=torch.channels_last)
+                lat[i - 1] = conv_bn_act(inputs[i - 1], self.lateral_convs[i - 1], residual=up,
+                                         out_nhwc=nhwc)
             return [self.fpn_convs[i](lat[i]) for i in range(n)]
         lat = [conv(inputs[i]) for i, conv in enumerate(self.lateral_convs)]
         for i in range(n - 1, 0, -1):
