@@ -127,6 +127,19 @@ def deconv_bn_act(x, conv, bn=None, act=None, rem=None, out_nhwc=False):
     return ops.deconv2x(x, w, b, act, packed_weight=wp, rem=rem, out_nhwc=out_nhwc)
 
 
+def conv_bn_act_s2(x, conv, bn=None, act=None, owner=None):
+    """act(BN(conv(x))) of a 3x3 stride-2 pad-1 conv on the dedicated stride-2 kernel
+    (ops.conv3x3_s2: whole-Co tiles, im2col straight into MFMA fragments), or None when the
+    shape is outside it (s2_conv_ok, co <= 96); the pack is cached on `owner` (default: conv)."""
+    if not s2_conv_ok(conv) or act not in (None, "relu", "leaky"):
+        return None
+    pk = s2_pack(owner if owner is not None else conv, [(conv, bn)])
+    if pk is None:
+        return None
+    co = conv.out_channels
+    return ops.conv3x3_s2(x.contiguous(), pk[0], pk[1], co, co, act_a=act)[0]
+
+
 def halo_input_ok(conv, c_in):
     """Whether a plain conv gains from channels-last input: a 3x3 stride-1 pad-1 conv, one group,
     split-packed weights, 32-channel K chunks -- the engine's halo tile (mdcn.hip HALO), which

@@ -18,8 +18,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from ._fuse import (FoldCacheMixin, bn_affine, conv_bn_act, folded, halo_input_ok,
-                    offset_conv_eval, use_fused)
+from ._fuse import (FoldCacheMixin, bn_affine, conv_bn_act, conv_bn_act_s2, folded,
+                    halo_input_ok, offset_conv_eval, use_fused)
 from .deform_conv import DeformConv, ModulatedDeformConv
 from .._precision import fp32_convs
 
@@ -209,7 +209,8 @@ class _BottleneckBase(FoldCacheMixin, nn.Module):
                                   c2.stride[0], c2.padding[0], c2.dilation[0], csa_up=csa_up,
                                   post=post if csa_up is not None else None)
                 return _take_post(r, post)
-            out = conv_bn_act(out, self.conv2, self.bn2, "relu")
+            y = conv_bn_act_s2(out, self.conv2, self.bn2, "relu")
+            out = y if y is not None else conv_bn_act(out, self.conv2, self.bn2, "relu")
         out = conv_bn_act(out, self.conv3, self.bn3, "relu", residual=identity)
         return out if csa_up is None else (out, None)
 

@@ -11,8 +11,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ._fuse import (FusedSequential, conv_bn_act, deconv2x_ok, deconv_bn_act, engine_conv,
-                    halo_input_ok, use_fused)
+from ._fuse import (FusedSequential, conv_bn_act, conv_bn_act_s2, deconv2x_ok, deconv_bn_act,
+                    engine_conv, halo_input_ok, use_fused)
 from .. import ops
 from .deform import DeformConv2d
 from .._precision import fp32_convs
@@ -265,8 +265,9 @@ class BasicConv(nn.Module):
     @fp32_convs
     def forward(self, x):
         if use_fused(self, x) and engine_conv(self.conv):
-            return conv_bn_act(x, self.conv, self.bn if self.use_bn else None,
-                               "relu" if self.relu else None)
+            bn, act = self.bn if self.use_bn else None, "relu" if self.relu else None
+            y = conv_bn_act_s2(x, self.conv, bn, act) if x.dim() == 4 else None
+            return y if y is not None else conv_bn_act(x, self.conv, bn, act)
         if self.fused_deconv(x):
             return deconv_bn_act(x, self.conv, self.bn if self.use_bn else None,
                                  "relu" if self.relu else None)
