@@ -21,6 +21,7 @@ from .. import ops
 from ._fuse import (FoldCacheMixin, bn_affine, conv_bn_act, conv_bn_act_s2, folded,
                     halo_input_ok, offset_conv_eval, use_fused)
 from .deform_conv import DeformConv, ModulatedDeformConv
+from .._lib import is_nhwc
 from .._precision import fp32_convs
 
 
@@ -100,7 +101,8 @@ class DeformConv2d(FoldCacheMixin, nn.Module):
         offset_mask = offset_conv_eval(x, self.offset_conv)
         ps, psh = bn_affine(bn) if bn is not None else (None, None)
         _, _, wp = folded(dc, None)
-        return ops.mdcn_forward_fused(x.contiguous(), offset_mask.contiguous(), dc.weight,
+        xin = x if is_nhwc(x) else x.contiguous()  # channels-last x: the NHWC window form
+        return ops.mdcn_forward_fused(xin, offset_mask.contiguous(), dc.weight,
                                       dc.bias, ps, psh, act, dc.stride, dc.padding, dc.dilation,
                                       self.deformable_groups,
                                       2.0 if self.double_mask else 1.0, packed_weight=wp,

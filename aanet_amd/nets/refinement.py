@@ -92,7 +92,8 @@ class _WarpErrorStem(nn.Module):
 
     # whether the eval stem emits its 32 channels channels-last in one kernel (StereoDRNet: the
     # dilated stack reads NHWC, the concat and the NHWC copy go away, AANet 24.0 -> 23.4 ms;
-    # Hourglass: its conv_start DCN + offset conv on channels-last input measured 0.6 ms slower)
+    # Hourglass: conv_start's offset conv on the halo tile and its DCN on the NHWC window form,
+    # 1,136 + 1,134 -> 789 + 928 us at full resolution, tools/refine_dcn_layout_bench.py)
     _stem_nhwc = False
 
     def _stem(self, low_disp, left_img, right_img):
@@ -141,6 +142,7 @@ class StereoDRNetRefinement(_WarpErrorStem):
 
 class HourglassRefinement(_WarpErrorStem):
     """refinement.py:111-202 (AANet+).  Height and width must be divisible by 16."""
+    _stem_nhwc = True
 
     def __init__(self):
         super(HourglassRefinement, self).__init__()
