@@ -352,7 +352,16 @@ class GANetFeature(nn.Module):
 
     @fp32_convs
     def forward(self, x):
-        return _hourglass2(self, self.conv_start(x))
+        cs = self.conv_start
+        third, c5 = cs[2], cs[1]
+        if isinstance(third, DeformConv2d) and third.modulation and use_fused(third, x) and \
+                use_fused(c5, x) and engine_conv(c5.conv) and c5.conv.out_channels % 4 == 0:
+            # the 5x5 stride-3 conv writes channels-last: the DCN's offset conv stages it on the
+            # halo tile and the DCN reads it with the NHWC window form
+            y = conv_bn_act(cs[0](x), c5.conv, c5.bn if c5.use_bn else None,
+                            "relu" if c5.relu else None, out_nhwc=True)
+            return _hourglass2(self, third(y))
+        return _hourglass2(self, cs(x))
 
 
 def _hourglass2(m, x):
