@@ -298,7 +298,9 @@ class Conv2x(nn.Module):
                                    stride=1, padding=1)
 
     @fp32_convs
-    def forward(self, x, rem):
+    def forward(self, x, rem, out_nhwc=False):
+        """out_nhwc (eval fast path, BasicConv conv2 only): return conv2's output channels-last
+        for a consumer that reads NHWC (the refinement's final_conv)."""
         c1 = self.conv1
         if self.concat and c1.fused_deconv(x) and rem.shape[2:] == (2 * x.shape[2], 2 * x.shape[3]):
             # transposed conv + BN + ReLU and the concat: one engine launch + one assembly pass,
@@ -309,6 +311,9 @@ class Conv2x(nn.Module):
                 halo_input_ok(c2.conv, c1.conv.out_channels + rem.shape[1])
             x = deconv_bn_act(x, c1.conv, c1.bn if c1.use_bn else None,
                               "relu" if c1.relu else None, rem=rem, out_nhwc=nhwc)
+            if out_nhwc and nhwc:
+                return conv_bn_act(x, c2.conv, c2.bn if c2.use_bn else None,
+                                   "relu" if c2.relu else None, out_nhwc=True)
             return self.conv2(x)
         x = self.conv1(x)
         assert x.size() == rem.size()
@@ -364,9 +369,10 @@ class GANetFeature(nn.Module):
         return _hourglass2(self, cs(x))
 
 
-def _hourglass2(m, x):
+def _hourglass2(m, x, last_nhwc=False):
     """Shared two-pass hourglass of GANetFeature.forward (feature.py:426-460) and
-    HourglassRefinement.forward (refinement.py:160-197): down a, up a, down b, up b."""
+    HourglassRefinement.forward (refinement.py:160-197): down a, up a, down b, up b.
+    last_nhwc: the last block may return its output channels-last (Conv2x out_nhwc)."""
     rem = [x]
     for name in ("conv1a", "conv2a", "conv3a", "conv4a"):
         x = getattr(m, name)(x)
@@ -379,7 +385,7 @@ def _hourglass2(m, x):
         rem[i] = x
     x = m.conv4b(x, rem[4])
     for i in (4, 3, 2, 1):
-        x = getattr(m, f"deconv{i}b")(x, rem[i - 1])
+        x = getattr(m, f"deconv{i}b")(x, rem[i - 1], out_nhwc=last_nhwc and i == 1)
     return x
 
 

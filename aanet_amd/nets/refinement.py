@@ -166,4 +166,6 @@ class HourglassRefinement(_WarpErrorStem):
     @fp32_convs
     def forward(self, low_disp, left_img, right_img):
         disp, x = self._stem(low_disp, left_img, right_img)
-        return _residual_out(self, _hourglass2(self, self.conv_start(x)), disp)
+        # the last block's output channels-last: final_conv (32 -> 1) reads it NHWC
+        feat = _hourglass2(self, self.conv_start(x), last_nhwc=use_fused(self, x))
+        return _residual_out(self, feat, disp)
