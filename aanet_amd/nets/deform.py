@@ -161,6 +161,12 @@ class _BottleneckBase(FoldCacheMixin, nn.Module):
                 width <= 64 and w3.shape[0] <= 64
             cpg = width // c2.deformable_groups  # 32k-channel groups, or pairs of 16-channel ones
             nhwc = pw and width % 32 == 0 and (cpg % 32 == 0 or cpg == 16)
+            # no tail kernel (AANetFeature layer3, width 128): a stride-1 modulated DCN still
+            # reads conv1's output channels-last -- the grouped offset conv (conv_g3) and the NHWC
+            # window form of the DCN
+            dc0 = c2.deform_conv
+            nhwc = nhwc or (not pw and c2.modulation and dc0.stride in (1, (1, 1)) and
+                            dc0.groups == 1 and width % 32 == 0 and cpg % 32 == 0)
         else:
             pw = c2.groups == 1 and width <= 64 and w3.shape[0] <= 64 and \
                 c2.stride[0] == c2.stride[1] and c2.padding[0] == c2.padding[1]
