@@ -21,6 +21,10 @@
 
 #include "split.h"
 
+#ifndef AANET_PW_GCAP
+#define AANET_PW_GCAP 1024  // workgroups per co tile of the Co > 64 streaming form
+#endif
+
 namespace {
 
 __device__ __forceinline__ float pw_act(float v, int act) {
@@ -34,7 +38,8 @@ __device__ __forceinline__ float pw_act(float v, int act) {
 template <int NB, int ONH>
 __device__ __forceinline__ void pw_store(const PwArgs &a, const f32x4 (&acc)[NB],
                                          const float (&eb)[NB][4], int t, int half, int kr, int n,
-                                         int p, int co_base = 0) {
+                                         int p, int co_base = 0, bool pre = false,
+                                         f32x4 rpre = f32x4{0.f, 0.f, 0.f, 0.f}) {
   const int T = a.N * a.P, P = a.P, Co = a.Co;
   if (t >= T) return;
 #pragma unroll
@@ -62,7 +67,10 @@ __device__ __forceinline__ void pw_store(const PwArgs &a, const f32x4 (&acc)[NB]
       // a load issued after a store waited for it -- one memory round trip per channel (the
       // bottleneck conv3 with its identity ran 3.4x the time of the plain conv)
       float rv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (a.residual) {
+      if (pre) {  // NB == 1: the caller's prefetched identity values
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rv[r] = rpre[r];
+      } else if (a.residual) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (c0 + r < Co) rv[r] = a.residual[((long)n * Co + c0 + r) * P + p];
@@ -342,6 +350,25 @@ __global__ __launch_bounds__(256) void pw_conv_nchw_s_kernel(PwArgs a) {
     if (b + 1 < b1) load(b + 1);
     const __bf16 *xs = sB[buf];
     const int n0b = __builtin_amdgcn_readfirstlane((b * BP) / P), p0b = b * BP - n0b * P;
+    // the block's identity values (NCHW out) load before its MFMAs: issued per 16-pixel group at
+    // its store, each group waited a full memory round trip (32 -> 128 with identity 138 us vs
+    // 58 without)
+    f32x4 rpf[SW / 16];
+    if (!ONH && a.residual) {
+#pragma unroll
+      for (int g = 0; g < SW / 16; ++g) {
+        const int off = SW * sub + 16 * g + jj, t = b * BP + off;
+        int nn = n0b, pp = p0b + off;
+        while (pp >= P) {
+          pp -= P;
+          ++nn;
+        }
+        const int c0 = co_base + 16 * cb + 4 * kr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          rpf[g][r] = (t < T && c0 + r < Co) ? a.residual[((long)nn * Co + c0 + r) * P + pp] : 0.f;
+      }
+    }
 #pragma unroll
     for (int g = 0; g < SW / 16; ++g) {
       const int px = SW * sub + 16 * g + jj;
@@ -360,7 +387,8 @@ __global__ __launch_bounds__(256) void pw_conv_nchw_s_kernel(PwArgs a) {
         pp -= P;
         ++nn;
       }
-      pw_store<1, ONH>(a, acc, eb, b * BP + off, cb, kr, nn, pp, co_base);
+      pw_store<1, ONH>(a, acc, eb, b * BP + off, cb, kr, nn, pp, co_base, !ONH && a.residual,
+                       (!ONH && a.residual) ? rpf[g] : f32x4{0.f, 0.f, 0.f, 0.f});
     }
     if (b + 1 < b1) {
       stage(buf ^ 1);
@@ -432,7 +460,7 @@ int pw_conv_launch(const PwArgs &a, hipStream_t st) {
     if (a.in_nhwc) return AANET_EUNSUPPORTED;
     const long nblk = ((long)a.N * a.P + 63) / 64;
     long g = (nblk + 3) / 4;
-    if (g > 1024) g = 1024;
+    if (g > AANET_PW_GCAP) g = AANET_PW_GCAP;
     const dim3 grid((unsigned)g, (unsigned)(a.Co / 64)), blk(256);
     if (a.C == 32) {
       if (a.out_nhwc)
