@@ -167,5 +167,7 @@ class HourglassRefinement(_WarpErrorStem):
     def forward(self, low_disp, left_img, right_img):
         disp, x = self._stem(low_disp, left_img, right_img)
         # the last block's output channels-last: final_conv (32 -> 1) reads it NHWC
+        if not use_fused(self.conv_start, x):
+            x = x.contiguous()  # the stem's channels-last output goes to a reference-order DCN
         feat = _hourglass2(self, self.conv_start(x), last_nhwc=use_fused(self, x))
         return _residual_out(self, feat, disp)
